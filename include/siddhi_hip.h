@@ -1,0 +1,110 @@
+/*
+ * siddhi_hip.h — C-ABI of libsiddhi_hip.so, the MI355X engine for Siddhi's
+ * pattern/sequence path (io.siddhi.core.query.input.stream.state).
+ *
+ * Drop-in boundary. The reference has no plugin SPI for state
+ * runtimes: a StateStreamRuntime is built at
+ *   modules/siddhi-core/src/main/java/io/siddhi/core/util/parser/InputStreamParser.java:88-93
+ * and fed through StreamJunction.Receiver.receive(...)
+ *   modules/siddhi-core/src/main/java/io/siddhi/core/stream/StreamJunction.java:443-456
+ * by the Pattern/Sequence{Single,Multi}ProcessStreamReceivers
+ *   modules/siddhi-core/src/main/java/io/siddhi/core/query/input/stream/state/receiver/*.java
+ * and emits one StateEvent per match into QuerySelector.process
+ *   modules/siddhi-core/src/main/java/io/siddhi/core/query/selector/QuerySelector.java:76-99.
+ * The entry points below replace, respectively:
+ *   shp_engine_create   StateInputStreamParser.parseInputStream (:76-146) + QueryRuntimeImpl.start
+ *   shp_push_batch      ProcessStreamReceiver.receive(long, Object[]) for a run of sends, including
+ *                       PartitionStreamReceiver.send (core/partition/PartitionStreamReceiver.java:262-283)
+ *                       and the playback clock (core/stream/input/InputHandler.java:59-70)
+ *   shp_advance_clock   TimestampGeneratorImpl.setCurrentTimestamp (core/util/timestamp/
+ *                       TimestampGeneratorImpl.java:105-121) with no event (timer flush)
+ *   shp_engine_destroy  SiddhiAppRuntime.shutdown for the query
+ * Errors are status codes (no exceptions cross the ABI); shp_last_error() gives text.
+ * A single engine is not re-entrant (the reference serialises a query with
+ * synchronized(patternSyncObject), SingleProcessStreamReceiver.java:52).
+ */
+#ifndef SIDDHI_HIP_H
+#define SIDDHI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHP_OK 0
+#define SHP_ERR_ARG -1          /* bad argument / malformed program JSON */
+#define SHP_ERR_UNSUPPORTED -2  /* construct outside the state path */
+#define SHP_ERR_CAPACITY -3     /* a per-key table overflowed (partials, chains, timers) */
+#define SHP_ERR_OUTPUT -4       /* match buffer too small for this batch */
+#define SHP_ERR_DEVICE -5       /* HIP runtime error */
+#define SHP_ERR_KEYS -6         /* key id >= cfg.max_keys */
+
+typedef struct shp_engine shp_engine;
+
+typedef struct shp_config {
+  int32_t device;          /* HIP device ordinal */
+  int32_t max_keys;        /* partition-key dictionary capacity (1 when not partitioned) */
+  int64_t max_batch;       /* largest n accepted by one push */
+  int64_t max_matches;     /* match-record capacity per push */
+  int64_t start_clock;     /* event-time clock at start() (0 in playback mode) */
+  int32_t force_general;   /* 1: never use the specialised 2-state kernel */
+  int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
+} shp_config;
+
+/* One batch of events in SoA form. Column c follows program["columns"][c]:
+ * int->int32, long->int64, float->float32, double->float64, bool->uint8,
+ * string->int32 (dictionary id, host owns the strings). nulls[c] may be NULL. */
+typedef struct shp_batch {
+  int64_t n;
+  const int64_t* ts;
+  const int32_t* key;      /* partition key id per event (0 when not partitioned) */
+  const int32_t* stream;   /* stream index per event (program["streams"] order) */
+  const void* const* cols;
+  const uint8_t* const* nulls;
+} shp_batch;
+
+/* Engine-owned match records (valid until the next call on the engine).
+ * Per key, records are in reference emission order; across keys unspecified.
+ * Slot s of match i holds slot_len[i*S+s] event sequence numbers starting at
+ * refs[ref_off[i]] + sum_{t<s} slot_len[i*S+t]; seq -1 = an empty event. */
+typedef struct shp_matches {
+  int64_t m;
+  int32_t num_states;      /* S */
+  const int32_t* key;
+  const int64_t* ts;       /* StateEvent timestamp (last matched event ts or timer due time) */
+  const int8_t* type;      /* 0 CURRENT, 1 EXPIRED */
+  const int64_t* pos;      /* event seq during (before, for timers) which the match was emitted */
+  const int64_t* ref_off;
+  const int16_t* slot_len;
+  const int64_t* refs;
+} shp_matches;
+
+int shp_engine_create(const char* nfa_program_json, const shp_config* cfg, shp_engine** out);
+/* Host-memory batch: copied to HBM, processed, matches copied back to host memory. */
+int shp_push_batch(shp_engine* e, const shp_batch* in, shp_matches* out);
+/* HBM-resident batch (device pointers); matches stay in HBM (out holds device pointers). */
+int shp_push_batch_device(shp_engine* e, const shp_batch* in, shp_matches* out);
+/* Copy the matches of the last shp_push_batch_device to host memory. */
+int shp_fetch_matches(shp_engine* e, shp_matches* out);
+int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out);
+int shp_engine_num_states(const shp_engine* e);
+/* Which kernel the engine runs: 1 = specialised 2-state scan, 0 = general NFA lanes. */
+int shp_engine_path(const shp_engine* e);
+/* Bench/test utility (not part of the reference boundary): fill device buffers with events
+ * start..start+count-1 of the SURVEY.md §8d synthetic stream (PCG32, bit-identical to
+ * siddhi_amd/synth.py). Any output pointer may be NULL. hip_stream: a hipStream_t or NULL. */
+int shp_synth_fill(int config, int64_t start, int64_t count, int64_t keys, int n_streams, int dense,
+                   int64_t* ts, int32_t* key, float* price, int64_t* volume, int32_t* stream, void* hip_stream);
+/* Device time (ms) of the last push measured with HIP events on the engine stream:
+ * which = "total" | "partition" | "nfa" | a kernel name (needs cfg.profile_kernels), e.g.
+ * "radix_sort", "nfa_lanes", "fast_search", "fast_emit". */
+double shp_last_kernel_ms(const shp_engine* e, const char* which);
+const char* shp_last_error(const shp_engine* e);
+void shp_engine_destroy(shp_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIDDHI_HIP_H */

@@ -1,0 +1,37 @@
+"""Build libsiddhi_hip.so for gfx950 (hipcc), in-tree so it travels with the repo snapshot."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "libsiddhi_hip.so")
+SRC = os.path.join(HERE, "csrc")
+DEPS = ["engine.hip", "synth.hip", "nfa_lane.h", "fastpath.h", "prog.h", "compile.h", "jsonv.h"]
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    srcs = [os.path.join(SRC, d) for d in DEPS] + [os.path.join(ROOT, "include", "siddhi_hip.h")]
+    return any(os.path.getmtime(s) > t for s in srcs if os.path.exists(s))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-o", LIB + ".tmp", os.path.join(SRC, "engine.hip"), os.path.join(SRC, "synth.hip")]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

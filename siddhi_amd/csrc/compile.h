@@ -1,0 +1,413 @@
+// siddhi-hip: host-side NFA program compiler (program JSON -> DevProg).
+//
+// Reproduces the build-time wiring of StateInputStreamParser.parse
+// (core/util/parser/StateInputStreamParser.java:148-408): processor creation per
+// state element, next/every/partner links, within + start-state ids (:129-141),
+// the first processor's thisLastProcessor (:142-143), the selector attachment of
+// InnerStateRuntime.setQuerySelector and the receiver registration order of
+// InnerStateRuntime.setup (state/runtime/*.java).  Condition trees are lowered to
+// the predicate bytecode of prog.h (Java typing is already resolved in the JSON).
+#pragma once
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "jsonv.h"
+#include "prog.h"
+
+namespace shp {
+
+struct CompileError : std::runtime_error {
+  int code;
+  CompileError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+class ProgramCompiler {
+ public:
+  DevProg P{};
+  FastShape fast{};
+
+  void compile(const char* json) {
+    JV root = JReader(json).read();
+    P.type = root.get("type").sv == "sequence" ? SEQUENCE : PATTERN;
+    P.within = root.get("within").i();
+    P.playback = root.get("playback").b();
+    P.partitioned = root.get("partitioned").b();
+    const JV& states = root.get("states");
+    P.nstates = (int)states.size();
+    if (P.nstates < 1 || P.nstates > MAXS) throw CompileError(-2, "states: 1..8 supported");
+    P.nstream = (int)root.get("streams").size();
+    if (P.nstream > MAXSTREAM) throw CompileError(-2, "too many streams");
+    const JV& cols = root.get("columns");
+    P.ncol = (int)cols.size();
+    if (P.ncol > MAXCOL) throw CompileError(-2, "too many predicate columns");
+    for (int c = 0; c < P.ncol; c++) {
+      int s = (int)cols[c].get("stream").i();
+      P.colStream[c] = (int8_t)s;
+      P.colTag[c] = tagOf(cols[c].get("type").sv);
+      if (P.streamNcol[s] >= NV) throw CompileError(-2, "too many predicate columns on one stream");
+      P.colPos[c] = P.streamNcol[s];
+      P.streamCols[s][P.streamNcol[s]++] = (int8_t)c;
+    }
+    states_ = &states;
+    for (int i = 0; i < P.nstates; i++) {
+      filterPc_.push_back(-1);
+      if (states[i].present("filter")) {
+        filterPc_[i] = (int)code_.size();
+        emit(states[i].get("filter"));
+        code_.push_back(Instr{OP_END, 0, 0, 0, 0, 0});
+      }
+    }
+    if ((int)code_.size() > MAXCODE) throw CompileError(-2, "predicate program too long");
+    P.ncode = (int)code_.size();
+    for (size_t i = 0; i < code_.size(); i++) P.code[i] = code_[i];
+    std::vector<int> all;
+    Rt r = parse(root.get("tree"), -1, -1, true, all);
+    for (int p : all) P.expireOrder[P.nexpire++] = (int8_t)p;
+    if (P.within != -1) {
+      for (int p : all)
+        if (P.pre[p].isStart) P.startIds[P.nstart++] = P.pre[p].stateId;
+    }
+    P.pre[r.first].thisLast = (int16_t)r.last;
+    setQuerySelector(r.node);
+    setup(r.node);
+    initOrder(r.node);
+    resetOrder(r.node);
+    updateOrder(r.node);
+    for (int s = 0; s < P.nstream; s++) {
+      P.recvMulti[s] = P.recvCount[s] > 1;
+      if (P.recvCount[s] == 0) continue;
+      if (P.recvMulti[s]) {
+        int last = P.recvPre[s][P.recvCount[s] - 1];
+        P.recvSelector[s] = P.post[P.pre[last].thisPost].hasNext;
+      } else {
+        int p = P.recvPre[s][0];
+        P.recvSelector[s] = P.post[P.pre[p].thisLast].hasNext;
+      }
+    }
+    detectFast(root);
+  }
+
+ private:
+  const JV* states_ = nullptr;
+  std::vector<Instr> code_;
+  std::vector<int> filterPc_;
+
+  struct TNode {
+    enum T { STREAM, NEXT, EVERY, LOGICAL, COUNT } t;
+    int first = -1, last = -1, leaf = -1;
+    TNode *a = nullptr, *b = nullptr;
+  };
+  std::vector<std::unique_ptr<TNode>> nodes_;
+  struct Rt {
+    int first, last;
+    TNode* node;
+  };
+
+  static int8_t tagOf(const std::string& t) {
+    if (t == "int") return T_INT;
+    if (t == "long") return T_LONG;
+    if (t == "float") return T_FLOAT;
+    if (t == "double") return T_DOUBLE;
+    if (t == "bool") return T_BOOL;
+    if (t == "string") return T_STR;
+    return T_NULL;
+  }
+
+  void emit(const JV& e) {
+    const std::string& op = e.get("op").sv;
+    Instr in{};
+    if (op == "const") {
+      in.op = OP_CONST;
+      in.a = (uint8_t)tagOf(e.get("type").sv);
+      const JV& v = e.get("v");
+      switch (in.a) {
+        case T_FLOAT: { float f = (float)v.d(); uint32_t u; memcpy(&u, &f, 4); in.imm = u; break; }
+        case T_DOUBLE: { double d = v.d(); memcpy(&in.imm, &d, 8); break; }
+        case T_BOOL: in.imm = v.t == JV::BOOLEAN ? v.bv : v.i() != 0; break;
+        default: in.imm = v.i(); break;
+      }
+      code_.push_back(in);
+    } else if (op == "var") {
+      in.op = OP_VAR;
+      in.a = (uint8_t)e.get("state").i();
+      in.b = (uint8_t)(int8_t)e.get("index").i();
+      in.c = (uint8_t)e.get("col").i();
+      code_.push_back(in);
+    } else if (op == "isnullstate") {
+      in.op = OP_ISNULLSTATE;
+      in.a = (uint8_t)e.get("state").i();
+      in.b = (uint8_t)(int8_t)e.get("index").i();
+      code_.push_back(in);
+    } else if (op == "and" || op == "or") {
+      emit(e.get("a"));
+      size_t j = code_.size();
+      in.op = op == "and" ? OP_AND : OP_OR;
+      code_.push_back(in);
+      emit(e.get("b"));
+      Instr end{};
+      end.op = op == "and" ? OP_ANDEND : OP_OREND;
+      code_.push_back(end);
+      code_[j].d = (int32_t)code_.size();
+    } else if (op == "not" || op == "isnull") {
+      emit(e.get("a"));
+      in.op = op == "not" ? OP_NOT : OP_ISNULL;
+      code_.push_back(in);
+    } else if (op == "cmp") {
+      emit(e.get("a"));
+      emit(e.get("b"));
+      static const char* names[] = {"gt", "ge", "lt", "le", "eq", "ne"};
+      in.op = OP_CMP;
+      for (int i = 0; i < 6; i++)
+        if (e.get("cmp").sv == names[i]) in.a = (uint8_t)i;
+      in.b = promote(tagExpr(e.get("a")), tagExpr(e.get("b")));
+      code_.push_back(in);
+    } else if (op == "add" || op == "sub" || op == "mul" || op == "div" || op == "mod") {
+      emit(e.get("a"));
+      emit(e.get("b"));
+      in.op = OP_ARITH;
+      in.a = op == "add" ? 0 : op == "sub" ? 1 : op == "mul" ? 2 : op == "div" ? 3 : 4;
+      in.b = (uint8_t)tagOf(e.get("type").sv);
+      code_.push_back(in);
+    } else {
+      throw CompileError(-2, "unsupported predicate op " + op);
+    }
+  }
+
+  int8_t tagExpr(const JV& e) {
+    const std::string& op = e.get("op").sv;
+    if (op == "const" || op == "var" || op == "add" || op == "sub" || op == "mul" || op == "div" || op == "mod")
+      return tagOf(e.get("type").sv);
+    return T_BOOL;
+  }
+  static uint8_t promote(int8_t a, int8_t b) {
+    if (a == T_STR || b == T_STR) return T_STR;
+    if (a == T_BOOL || b == T_BOOL) return T_BOOL;
+    if (a == T_NULL || b == T_NULL) return T_NULL;
+    if (a == T_DOUBLE || b == T_DOUBLE) return T_DOUBLE;
+    if (a == T_FLOAT || b == T_FLOAT) return T_FLOAT;
+    if (a == T_LONG || b == T_LONG) return T_LONG;
+    return T_INT;
+  }
+
+  int npost_ = 0;
+  int newPre(int8_t kind) {
+    if (P.npre >= MAXP) throw CompileError(-2, "too many processors");
+    int id = P.npre++;
+    DPre& p = P.pre[id];
+    p.kind = kind;
+    p.withinEvery = p.thisPost = p.thisLast = p.partner = p.countPost = -1;
+    p.sched = -1;
+    p.waiting = -1;
+    return id;
+  }
+  int newPost(int8_t kind) {
+    if (npost_ >= MAXP) throw CompileError(-2, "too many processors");
+    int id = npost_++;
+    DPost& q = P.post[id];
+    q.kind = kind;
+    q.nextState = q.nextEvery = q.thisPre = q.callbackPre = q.partnerPre = q.partnerPost = -1;
+    return id;
+  }
+  int newSched(int pre) {
+    if (P.nsched >= MAXQ) throw CompileError(-2, "too many absent states");
+    P.schedPre[P.nsched] = (int8_t)pre;
+    P.startup[P.nstartup++] = (int8_t)pre;
+    return P.nsched++;
+  }
+  void setNextState(int q, int p) {
+    DPost& Q = P.post[q];
+    Q.nextState = (int16_t)p;
+    if (Q.kind == K_LOGICAL || Q.kind == K_ABSENT_LOGICAL) {
+      P.post[Q.partnerPost].nextState = (int16_t)p;
+    } else if (Q.kind == K_COUNT) {
+      DPre& tp = P.pre[Q.thisPre];
+      if (tp.isStart && P.type == SEQUENCE && Q.minCount == 0) P.post[P.pre[p].thisPost].callbackPre = Q.thisPre;
+    }
+  }
+  void setNextEvery(int q, int p) {
+    DPost& Q = P.post[q];
+    Q.nextEvery = (int16_t)p;
+    if (Q.kind == K_LOGICAL || Q.kind == K_ABSENT_LOGICAL) P.post[Q.partnerPost].nextEvery = (int16_t)p;
+  }
+
+  TNode* mk(TNode::T t) {
+    nodes_.push_back(std::make_unique<TNode>());
+    nodes_.back()->t = t;
+    return nodes_.back().get();
+  }
+
+  Rt parse(const JV& t, int pre, int post, bool isStart, std::vector<int>& list) {
+    const std::string& k = t.get("t").sv;
+    if (k == "stream" || k == "absent") {
+      int sid = (int)t.get("state").i();
+      const JV& sj = (*states_)[sid];
+      bool absent = k == "absent";
+      if (pre < 0) {
+        if (absent) {
+          pre = newPre(K_ABSENT_STREAM);
+          P.pre[pre].waiting = sj.get("waiting").i();
+          P.pre[pre].sched = (int8_t)newSched(pre);
+        } else {
+          pre = newPre(K_STREAM);
+        }
+      }
+      DPre& p = P.pre[pre];
+      p.stateId = (int8_t)sid;
+      p.stream = (int8_t)sj.get("stream").i();
+      p.isStart = isStart;
+      p.filterPc = (int16_t)filterPc_[sid];
+      if (post < 0) post = newPost(absent ? K_ABSENT_STREAM : K_STREAM);
+      P.post[post].stateId = (int8_t)sid;
+      P.post[post].thisPre = (int16_t)pre;
+      p.thisPost = (int16_t)post;
+      p.thisLast = (int16_t)post;
+      list.push_back(pre);
+      TNode* n = mk(TNode::STREAM);
+      n->first = pre;
+      n->last = post;
+      n->leaf = pre;
+      return {pre, post, n};
+    }
+    if (k == "next") {
+      Rt a = parse(t.get("a"), pre, post, isStart, list);
+      Rt b = parse(t.get("b"), pre, post, false, list);
+      setNextState(a.last, b.first);
+      TNode* n = mk(TNode::NEXT);
+      n->a = a.node;
+      n->b = b.node;
+      n->first = a.first;
+      n->last = b.last;
+      return {a.first, b.last, n};
+    }
+    if (k == "every") {
+      std::vector<int> inner;
+      Rt a = parse(t.get("x"), pre, post, isStart, inner);
+      setNextEvery(a.last, a.first);
+      for (int p : inner) P.pre[p].withinEvery = (int16_t)a.first;
+      list.insert(list.end(), inner.begin(), inner.end());
+      TNode* n = mk(TNode::EVERY);
+      n->a = a.node;
+      n->first = a.first;
+      n->last = a.last;
+      return {a.first, a.last, n};
+    }
+    if (k == "logical") {
+      int8_t lt = t.get("op").sv == "or" ? L_OR : L_AND;
+      const JV& e1 = t.get("s1");
+      const JV& e2 = t.get("s2");
+      int p1, p2, q1, q2;
+      auto make = [&](const JV& e, int& lp, int& lq) {
+        bool abs = e.get("t").sv == "absent";
+        lp = newPre(abs ? K_ABSENT_LOGICAL : K_LOGICAL);
+        if (abs) {
+          P.pre[lp].waiting = (*states_)[(int)e.get("state").i()].get("waiting").i();
+          P.pre[lp].sched = (int8_t)newSched(lp);
+        }
+        P.pre[lp].logical = lt;
+        lq = newPost(abs ? K_ABSENT_LOGICAL : K_LOGICAL);
+        P.post[lq].logical = lt;
+      };
+      make(e1, p1, q1);
+      make(e2, p2, q2);
+      P.post[q1].partnerPre = (int16_t)p2;
+      P.post[q2].partnerPre = (int16_t)p1;
+      P.post[q1].partnerPost = (int16_t)q2;
+      P.post[q2].partnerPost = (int16_t)q1;
+      P.pre[p1].partner = (int16_t)p2;
+      P.pre[p2].partner = (int16_t)p1;
+      Rt r2 = parse(e2, p2, q2, isStart, list);
+      Rt r1 = parse(e1, p1, q1, isStart, list);
+      TNode* n = mk(TNode::LOGICAL);
+      n->a = r1.node;
+      n->b = r2.node;
+      n->first = r1.first;
+      n->last = r2.last;
+      return {r1.first, r2.last, n};
+    }
+    if (k == "count") {
+      int cp = newPre(K_COUNT), cq = newPost(K_COUNT);
+      int mn = (int)t.get("min").i(), mx = (int)t.get("max").i();
+      P.pre[cp].minCount = P.post[cq].minCount = mn;
+      P.pre[cp].maxCount = P.post[cq].maxCount = mx < 0 ? 0x7fffffff : mx;
+      P.pre[cp].countPost = (int16_t)cq;
+      JV leaf;
+      leaf.t = JV::OBJECT;
+      JV ts;
+      ts.t = JV::STRING;
+      ts.sv = "stream";
+      leaf.ov.emplace_back("t", ts);
+      leaf.ov.emplace_back("state", t.get("state"));
+      Rt r = parse(leaf, cp, cq, isStart, list);
+      r.node->t = TNode::COUNT;
+      return r;
+    }
+    throw CompileError(-2, "unsupported state element " + k);
+  }
+
+  void setQuerySelector(TNode* n) {
+    switch (n->t) {
+      case TNode::STREAM:
+      case TNode::COUNT: P.post[n->last].hasNext = 1; break;
+      case TNode::NEXT: setQuerySelector(n->b); break;
+      case TNode::EVERY: setQuerySelector(n->a); break;
+      case TNode::LOGICAL: setQuerySelector(n->b); setQuerySelector(n->a); break;
+    }
+  }
+  void setup(TNode* n) {
+    switch (n->t) {
+      case TNode::STREAM:
+      case TNode::COUNT: {
+        int s = P.pre[n->leaf].stream;
+        P.recvPre[s][P.recvCount[s]++] = (int8_t)n->leaf;
+        break;
+      }
+      case TNode::NEXT: setup(n->a); setup(n->b); break;
+      case TNode::EVERY: setup(n->a); break;
+      case TNode::LOGICAL: setup(n->b); setup(n->a); break;
+    }
+  }
+  void initOrder(TNode* n) {
+    switch (n->t) {
+      case TNode::STREAM:
+      case TNode::COUNT: P.initOrder[P.ninit++] = (int8_t)n->leaf; break;
+      case TNode::NEXT: initOrder(n->a); initOrder(n->b); break;
+      case TNode::EVERY: initOrder(n->a); break;
+      case TNode::LOGICAL: initOrder(n->b); initOrder(n->a); break;
+    }
+  }
+  void resetOrder(TNode* n) {
+    switch (n->t) {
+      case TNode::NEXT: resetOrder(n->b); resetOrder(n->a); break;
+      case TNode::LOGICAL: resetOrder(n->b); break;
+      default: P.resetOrder[P.nreset++] = (int8_t)n->first; break;
+    }
+  }
+  void updateOrder(TNode* n) {
+    switch (n->t) {
+      case TNode::NEXT: updateOrder(n->a); updateOrder(n->b); break;
+      case TNode::LOGICAL: updateOrder(n->b); break;
+      default: P.updateOrder[P.nupdate++] = (int8_t)n->first; break;
+    }
+  }
+
+  // every e1=S[f1] -> e2=S[f2] within W  (SURVEY.md Appendix A.7 closed form)
+  void detectFast(const JV& root) {
+    fast.ok = 0;
+    const JV& t = root.get("tree");
+    if (P.type != PATTERN || P.nstates != 2 || P.within < 0 || P.nsched != 0) return;
+    if (t.get("t").sv != "next") return;
+    const JV& a = t.get("a");
+    const JV& b = t.get("b");
+    if (a.get("t").sv != "every" || a.get("x").get("t").sv != "stream" || b.get("t").sv != "stream") return;
+    if (a.get("x").get("state").i() != 0 || b.get("state").i() != 1) return;
+    if (P.pre[0].stream != P.pre[1].stream) return;
+    if (P.ncol > 2) return;
+    fast.ok = 1;
+    fast.stream = P.pre[0].stream;
+    fast.within = P.within;
+  }
+};
+
+}  // namespace shp

@@ -1,0 +1,563 @@
+// siddhi-hip engine: libsiddhi_hip.so (gfx950).
+//
+// Per push (shp_push_batch / shp_push_batch_device):
+//   1. clock:     rmax = inclusive max-scan of ts seeded with the carried clock
+//                 (TimestampGeneratorImpl.setCurrentTimestamp, playback)
+//   2. partition: stable radix sort of (key, seq) -> perm; per-key [kbeg, kbeg+kcnt)
+//                 (PartitionStreamReceiver routes each event to its key's state, and a
+//                 key's events keep arrival order)
+//   3a. general:  k_nfa_lanes — one lane per key replays the processor chain (nfa_lane.h)
+//   3b. fast:     k_fast_* — the closed form of `every e1=S[f1] -> e2=S[f2] within W`
+//                 (fastpath.h), chosen at create time when the program has that shape
+//   4. matches are appended to an HBM match table; host pushes copy them back.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <numeric>
+#include <rocprim/rocprim.hpp>
+#include <string>
+#include <vector>
+
+#include "../../include/siddhi_hip.h"
+#include "compile.h"
+#include "fastpath.h"
+#include "nfa_lane.h"
+
+using namespace shp;
+
+#define HIP_OK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) throw DevError(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DevError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// ---------------------------------------------------------------- kernels
+__global__ void k_iota(uint32_t* v, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) v[i] = (uint32_t)i;
+}
+
+__global__ void k_key_hist(const int32_t* key, const int32_t* stream, int64_t n, uint32_t* cnt, int32_t max_keys,
+                           int partitioned, int* err) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int32_t k = partitioned ? key[i] : 0;
+    if (stream[i] < 0) continue;  // clock-only event (advance)
+    if (k < 0 || k >= max_keys) {
+      atomicOr(err, 1 << 20);
+      continue;
+    }
+    atomicAdd(&cnt[k], 1u);
+  }
+}
+
+__global__ void k_sort_keys(const int32_t* key, const int32_t* stream, int64_t n, uint32_t* out, int partitioned,
+                            uint32_t nokey) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = stream[i] < 0 ? nokey : (partitioned ? (uint32_t)key[i] : 0u);
+}
+
+__global__ void k_clamp_clock(int64_t* rmax, int64_t n, int64_t clock0) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (rmax[i] < clock0) rmax[i] = clock0;
+}
+
+__global__ __launch_bounds__(64) void k_nfa_lanes(const DevProg* __restrict__ Pp, LaneLayout Y, char* arena,
+                                                  BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
+                                                  const uint32_t* __restrict__ kbeg,
+                                                  const uint32_t* __restrict__ kcnt, int32_t nlanes, int* err) {
+  int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nlanes) return;
+  const DevProg& P = *Pp;
+  Lane ln(P, Y, arena, k, k, B, O);
+  if (!B.partitioned && !ln.at<uint8_t>(Y.o_kinit, 0)) {
+    ln.clock = B.init_clock;
+    ln.emit_pos = B.seq0;
+    ln.init_partition();
+  }
+  int64_t lo = 0;
+  uint32_t b = kbeg[k], e = b + kcnt[k];
+  for (uint32_t p = b; p < e && !ln.err; p++) {
+    int64_t g = perm[p];
+    ln.maybe_gc();
+    ln.timers(lo, g);
+    ln.on_event(g);
+    lo = g + 1;
+  }
+  if (!ln.err) {
+    ln.maybe_gc();
+    ln.timers(lo, B.n - 1);
+  }
+  ln.flush_ret();
+  if (ln.err) {
+    ln.at<int32_t>(Y.o_err, 0) |= ln.err;
+    atomicOr(err, ln.err);
+  }
+}
+
+// ---------------------------------------------------------------- engine
+struct shp_engine {
+  KTimer kt;
+  ProgramCompiler comp;
+  DevProg* dprog = nullptr;
+  shp_config cfg{};
+  LaneLayout Y{};
+  char* arena = nullptr;
+  int fast = 0;
+  FastState fs{};
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  std::string err;
+
+  // batch buffers
+  int64_t cap = 0;
+  int64_t* d_ts = nullptr;
+  int32_t* d_key = nullptr;
+  int32_t* d_stream = nullptr;
+  void* d_cols[MAXCOL] = {};
+  uint8_t* d_nulls[MAXCOL] = {};
+  int64_t* d_rmax = nullptr;
+  uint32_t *d_skey = nullptr, *d_skey2 = nullptr, *d_idx = nullptr, *d_perm = nullptr;
+  uint32_t *d_kcnt = nullptr, *d_kbeg = nullptr;
+  void* d_tmp = nullptr;
+  size_t tmp_bytes = 0;
+  int* d_err = nullptr;
+  // match table
+  int64_t mcap = 0, rcap = 0;
+  unsigned long long* d_mcount = nullptr;
+  int32_t* d_mkey = nullptr;
+  int64_t *d_mts = nullptr, *d_mpos = nullptr, *d_moff = nullptr, *d_refs = nullptr;
+  int8_t* d_mtype = nullptr;
+  int16_t* d_mslot = nullptr;
+  // host copies
+  std::vector<int32_t> h_key;
+  std::vector<int64_t> h_ts, h_pos, h_off, h_refs;
+  std::vector<int8_t> h_type;
+  std::vector<int16_t> h_slot;
+  int64_t h_m = 0;
+  // run state
+  int64_t seq = 0;
+  int64_t clock = 0;
+  int key_bits = 1;
+  double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
+  int64_t last_m = 0;
+
+  ~shp_engine() { release(); }
+
+  void release() {
+    auto F = [](void* p) {
+      if (p) (void)hipFree(p);
+    };
+    F(dprog);
+    F(arena);
+    F(d_ts);
+    F(d_key);
+    F(d_stream);
+    for (int c = 0; c < MAXCOL; c++) {
+      F(d_cols[c]);
+      F(d_nulls[c]);
+    }
+    F(d_rmax);
+    F(d_skey);
+    F(d_skey2);
+    F(d_idx);
+    F(d_perm);
+    F(d_kcnt);
+    F(d_kbeg);
+    F(d_tmp);
+    F(d_err);
+    F(d_mcount);
+    F(d_mkey);
+    F(d_mts);
+    F(d_mpos);
+    F(d_moff);
+    F(d_refs);
+    F(d_mtype);
+    F(d_mslot);
+    fs.release();
+    kt.release();
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (ev2) (void)hipEventDestroy(ev2);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  template <class T>
+  void alloc(T*& p, int64_t elems) {
+    HIP_OK(hipMalloc((void**)&p, std::max<int64_t>(elems, 1) * sizeof(T)));
+  }
+
+  static int colBytes(int8_t tag) {
+    switch (tag) {
+      case T_LONG:
+      case T_DOUBLE: return 8;
+      case T_BOOL: return 1;
+      default: return 4;
+    }
+  }
+
+  void create(const char* json, const shp_config* c) {
+    cfg = *c;
+    if (cfg.max_keys < 1) cfg.max_keys = 1;
+    if (cfg.max_batch < 1) cfg.max_batch = 1 << 16;
+    if (cfg.max_matches < 1) cfg.max_matches = std::max<int64_t>(cfg.max_batch, 1 << 16);
+    comp.compile(json);
+    if (!comp.P.partitioned) cfg.max_keys = 1;
+    HIP_OK(hipSetDevice(cfg.device));
+    HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&ev0));
+    HIP_OK(hipEventCreate(&ev1));
+    HIP_OK(hipEventCreate(&ev2));
+    alloc(dprog, 1);
+    HIP_OK(hipMemcpy(dprog, &comp.P, sizeof(DevProg), hipMemcpyHostToDevice));
+    clock = cfg.start_clock;
+    while ((1ll << key_bits) <= cfg.max_keys) key_bits++;  // + one sentinel key for clock-only events
+    fast = comp.fast.ok && !cfg.force_general;
+    kt.enabled = cfg.profile_kernels != 0;
+    cap = cfg.max_batch + 1;
+    alloc(d_ts, cap);
+    alloc(d_key, cap);
+    alloc(d_stream, cap);
+    for (int i = 0; i < comp.P.ncol; i++) {
+      HIP_OK(hipMalloc(&d_cols[i], cap * colBytes(comp.P.colTag[i])));
+      alloc(d_nulls[i], cap);
+    }
+    alloc(d_rmax, cap);
+    alloc(d_skey, cap);
+    alloc(d_skey2, cap);
+    alloc(d_idx, cap);
+    alloc(d_perm, cap);
+    alloc(d_kcnt, cfg.max_keys + 1);
+    alloc(d_kbeg, cfg.max_keys + 1);
+    alloc(d_err, 1);
+    mcap = cfg.max_matches;
+    rcap = mcap * comp.P.nstates * 2 + 64;
+    alloc(d_mcount, 2);
+    alloc(d_mkey, mcap);
+    alloc(d_mts, mcap);
+    alloc(d_mpos, mcap);
+    alloc(d_moff, mcap);
+    alloc(d_refs, rcap);
+    alloc(d_mtype, mcap);
+    alloc(d_mslot, mcap * MAXS);
+    // scratch for rocPRIM
+    size_t b1 = 0, b2 = 0, b3 = 0;
+    HIP_OK(rocprim::radix_sort_pairs(nullptr, b1, d_skey, d_skey2, d_idx, d_perm, (size_t)cap, 0, key_bits + 1,
+                                     stream));
+    HIP_OK(rocprim::inclusive_scan(nullptr, b2, d_ts, d_rmax, (size_t)cap, rocprim::maximum<int64_t>(), stream));
+    HIP_OK(rocprim::exclusive_scan(nullptr, b3, d_kcnt, d_kbeg, 0u, (size_t)cfg.max_keys, rocprim::plus<uint32_t>(),
+                                   stream));
+    tmp_bytes = std::max(b1, std::max(b2, b3));
+    if (fast) tmp_bytes = std::max(tmp_bytes, fs.scratch_bytes(cap, cfg.max_keys, stream));
+    HIP_OK(hipMalloc(&d_tmp, tmp_bytes));
+    if (fast) {
+      fs.create(comp.P, comp.fast, cfg.max_keys, cap, mcap, stream);
+    } else {
+      Y.build(cfg.max_keys);
+      HIP_OK(hipMalloc((void**)&arena, Y.bytes));
+      HIP_OK(hipMemsetAsync(arena, 0, Y.bytes, stream));
+    }
+    HIP_OK(hipStreamSynchronize(stream));
+  }
+
+  // runs the pipeline over n events at device pointers `in` (engine buffers after stage(), or
+  // the caller's HBM columns for shp_push_batch_device); leaves matches in HBM
+  int run(int64_t n, bool clock_only = false, const shp_batch* in = nullptr) {
+    const DevProg& P = comp.P;
+    const int64_t* x_ts = in ? in->ts : d_ts;
+    const int32_t* x_key = in ? (P.partitioned ? in->key : d_key) : d_key;
+    const int32_t* x_stream = in ? in->stream : d_stream;
+    if (in && !P.partitioned) HIP_OK(hipMemsetAsync(d_key, 0, n * 4, stream));
+    HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), stream));
+    HIP_OK(hipMemsetAsync(d_mcount, 0, 2 * sizeof(unsigned long long), stream));
+    kt.begin_push();
+    HIP_OK(hipEventRecord(ev0, stream));
+    int gb = (int)std::min<int64_t>((n + 255) / 256, 2048);
+    if (gb < 1) gb = 1;
+    // 1. clock
+    size_t tb = tmp_bytes;
+    kt.mark("clock_scan", stream);
+    HIP_OK(rocprim::inclusive_scan(d_tmp, tb, x_ts, d_rmax, (size_t)n, rocprim::maximum<int64_t>(), stream));
+    kt.mark("clamp_clock", stream);
+    k_clamp_clock<<<gb, 256, 0, stream>>>(d_rmax, n, clock);
+    // 2. partition by key (stable)
+    HIP_OK(hipMemsetAsync(d_kcnt, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
+    kt.mark("key_hist", stream);
+    k_key_hist<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_kcnt, cfg.max_keys, P.partitioned, d_err);
+    tb = tmp_bytes;
+    kt.mark("key_scan", stream);
+    HIP_OK(rocprim::exclusive_scan(d_tmp, tb, d_kcnt, d_kbeg, 0u, (size_t)cfg.max_keys, rocprim::plus<uint32_t>(),
+                                   stream));
+    kt.mark("sort_keys", stream);
+    k_sort_keys<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_skey, P.partitioned, (uint32_t)cfg.max_keys);
+    kt.mark("iota", stream);
+    k_iota<<<gb, 256, 0, stream>>>(d_idx, n);
+    tb = tmp_bytes;
+    kt.mark("radix_sort", stream);
+    HIP_OK(rocprim::radix_sort_pairs(d_tmp, tb, d_skey, d_skey2, d_idx, d_perm, (size_t)n, 0, key_bits + 1, stream));
+    kt.mark(nullptr, stream);
+    HIP_OK(hipEventRecord(ev1, stream));
+    // 3. NFA
+    BatchView B{};
+    B.n = n;
+    B.seq0 = seq;
+    B.clock0 = clock;
+    B.init_clock = cfg.start_clock;
+    B.partitioned = P.partitioned;
+    B.ts = x_ts;
+    B.stream = x_stream;
+    B.rmax = d_rmax;
+    for (int c = 0; c < P.ncol; c++) {
+      B.cols[c] = in ? in->cols[c] : d_cols[c];
+      B.nulls[c] = in ? (in->nulls ? in->nulls[c] : nullptr) : d_nulls[c];
+    }
+    MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs};
+    if (fast) {
+      fs.run(P, B, O, d_perm, d_kbeg, d_kcnt, cfg.max_keys, d_tmp, tmp_bytes, d_err, stream, d_skey2, dprog, kt);
+    } else {
+      int L = cfg.max_keys;
+      kt.mark("nfa_lanes", stream);
+      k_nfa_lanes<<<(L + 63) / 64, 64, 0, stream>>>(dprog, Y, arena, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+      kt.mark(nullptr, stream);
+    }
+    HIP_OK(hipEventRecord(ev2, stream));
+    HIP_OK(hipGetLastError());
+    int herr = 0;
+    unsigned long long cnt[2];
+    HIP_OK(hipMemcpyAsync(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipMemcpyAsync(cnt, d_mcount, sizeof(cnt), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    float a = 0, b = 0;
+    HIP_OK(hipEventElapsedTime(&a, ev0, ev1));
+    HIP_OK(hipEventElapsedTime(&b, ev1, ev2));
+    last_ms_part = a;
+    last_ms_nfa = b;
+    last_ms_total = a + b;
+    kt.collect();
+    // carry the clock: last rmax
+    if (n > 0) HIP_OK(hipMemcpy(&clock, d_rmax + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost));
+    if (!clock_only) seq += n;
+    last_m = (int64_t)cnt[0];
+    if (herr) {
+      if (herr & (1 << 20)) return fail(SHP_ERR_KEYS, "partition key id >= max_keys");
+      if (herr & E_OUT) return fail(SHP_ERR_OUTPUT, "match buffer too small for this batch (max_matches)");
+      if (herr & (1 << 21)) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state fast path");
+      return fail(SHP_ERR_CAPACITY, "per-key table capacity exceeded (code " + std::to_string(herr) + ")");
+    }
+    return SHP_OK;
+  }
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+
+  void stage(const shp_batch* in, hipMemcpyKind kind) {
+    const DevProg& P = comp.P;
+    int64_t n = in->n;
+    HIP_OK(hipMemcpyAsync(d_ts, in->ts, n * 8, kind, stream));
+    if (P.partitioned) HIP_OK(hipMemcpyAsync(d_key, in->key, n * 4, kind, stream));
+    else HIP_OK(hipMemsetAsync(d_key, 0, n * 4, stream));
+    HIP_OK(hipMemcpyAsync(d_stream, in->stream, n * 4, kind, stream));
+    for (int c = 0; c < P.ncol; c++) {
+      HIP_OK(hipMemcpyAsync(d_cols[c], in->cols[c], n * colBytes(P.colTag[c]), kind, stream));
+      if (in->nulls && in->nulls[c]) HIP_OK(hipMemcpyAsync(d_nulls[c], in->nulls[c], n, kind, stream));
+      else HIP_OK(hipMemsetAsync(d_nulls[c], 0, n, stream));
+    }
+  }
+
+  void fill_device(shp_matches* out) {
+    out->m = last_m;
+    out->num_states = comp.P.nstates;
+    out->key = d_mkey;
+    out->ts = d_mts;
+    out->type = d_mtype;
+    out->pos = d_mpos;
+    out->ref_off = d_moff;
+    out->slot_len = d_mslot;
+    out->refs = d_refs;
+  }
+
+  // copy to host and order by (pos, per-lane order) so callbacks follow reference emission order
+  void fetch(shp_matches* out) {
+    int64_t m = last_m;
+    int S = comp.P.nstates;
+    std::vector<int32_t> k(m);
+    std::vector<int64_t> ts(m), pos(m), off(m);
+    std::vector<int8_t> ty(m);
+    std::vector<int16_t> sl(m * MAXS);
+    unsigned long long cnt[2];
+    HIP_OK(hipMemcpy(cnt, d_mcount, sizeof(cnt), hipMemcpyDeviceToHost));
+    int64_t r = (int64_t)cnt[1];
+    std::vector<int64_t> refs(r);
+    if (m) {
+      HIP_OK(hipMemcpy(k.data(), d_mkey, m * 4, hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(ts.data(), d_mts, m * 8, hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(pos.data(), d_mpos, m * 8, hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(off.data(), d_moff, m * 8, hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(ty.data(), d_mtype, m, hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(sl.data(), d_mslot, m * MAXS * 2, hipMemcpyDeviceToHost));
+      if (r) HIP_OK(hipMemcpy(refs.data(), d_refs, r * 8, hipMemcpyDeviceToHost));
+    }
+    // per-key order is the append order; stable-sort by (pos, key-append-order)
+    std::vector<int64_t> idx(m);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
+      if (pos[a] != pos[b]) return pos[a] < pos[b];
+      if (k[a] != k[b]) return k[a] < k[b];
+      return a < b;
+    });
+    h_key.resize(m);
+    h_ts.resize(m);
+    h_pos.resize(m);
+    h_off.resize(m);
+    h_type.resize(m);
+    h_slot.resize(m * S);
+    h_refs.clear();
+    for (int64_t i = 0; i < m; i++) {
+      int64_t j = idx[i];
+      h_key[i] = k[j];
+      h_ts[i] = ts[j];
+      h_pos[i] = pos[j];
+      h_type[i] = ty[j];
+      h_off[i] = (int64_t)h_refs.size();
+      int64_t o = off[j];
+      for (int s = 0; s < S; s++) {
+        int16_t l = sl[j * MAXS + s];
+        h_slot[i * S + s] = l;
+        for (int t = 0; t < l; t++) h_refs.push_back(refs[o++]);
+      }
+    }
+    h_m = m;
+    out->m = m;
+    out->num_states = S;
+    out->key = h_key.data();
+    out->ts = h_ts.data();
+    out->type = h_type.data();
+    out->pos = h_pos.data();
+    out->ref_off = h_off.data();
+    out->slot_len = h_slot.data();
+    out->refs = h_refs.data();
+  }
+};
+
+// ---------------------------------------------------------------- C-ABI
+extern "C" {
+
+int shp_engine_create(const char* json, const shp_config* cfg, shp_engine** out) {
+  if (!json || !cfg || !out) return SHP_ERR_ARG;
+  auto* e = new shp_engine();
+  try {
+    e->create(json, cfg);
+  } catch (CompileError& ce) {
+    fprintf(stderr, "shp_engine_create: %s\n", ce.what());
+    delete e;
+    *out = nullptr;
+    return ce.code == -2 ? SHP_ERR_UNSUPPORTED : SHP_ERR_ARG;
+  } catch (DevError& de) {
+    fprintf(stderr, "shp_engine_create: %s\n", de.what());
+    delete e;
+    *out = nullptr;
+    return SHP_ERR_DEVICE;
+  } catch (std::exception& ex) {
+    fprintf(stderr, "shp_engine_create: %s\n", ex.what());
+    delete e;
+    *out = nullptr;
+    return SHP_ERR_ARG;
+  }
+  *out = e;
+  return SHP_OK;
+}
+
+static int guarded(shp_engine* e, const std::function<int()>& f) {
+  try {
+    return f();
+  } catch (DevError& de) {
+    e->err = de.what();
+    return SHP_ERR_DEVICE;
+  } catch (std::exception& ex) {
+    e->err = ex.what();
+    return SHP_ERR_ARG;
+  }
+}
+
+int shp_push_batch(shp_engine* e, const shp_batch* in, shp_matches* out) {
+  if (!e || !in || !out) return SHP_ERR_ARG;
+  return guarded(e, [&]() {
+    int64_t done = 0;
+    std::vector<int32_t> keys;
+    // one device batch per max_batch events
+    int64_t n = in->n;
+    if (n > e->cfg.max_batch) return e->fail(SHP_ERR_ARG, "batch larger than max_batch");
+    e->stage(in, hipMemcpyHostToDevice);
+    int rc = e->run(n);
+    if (rc != SHP_OK) return rc;
+    e->fetch(out);
+    (void)done;
+    return SHP_OK;
+  });
+}
+
+int shp_push_batch_device(shp_engine* e, const shp_batch* in, shp_matches* out) {
+  if (!e || !in || !out) return SHP_ERR_ARG;
+  return guarded(e, [&]() {
+    if (in->n > e->cfg.max_batch) return e->fail(SHP_ERR_ARG, "batch larger than max_batch");
+    int rc = e->run(in->n, false, in);  // zero-copy: the kernels read the caller's HBM columns
+    if (rc != SHP_OK) return rc;
+    e->fill_device(out);
+    return SHP_OK;
+  });
+}
+
+int shp_fetch_matches(shp_engine* e, shp_matches* out) {
+  if (!e || !out) return SHP_ERR_ARG;
+  return guarded(e, [&]() {
+    e->fetch(out);
+    return SHP_OK;
+  });
+}
+
+int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out) {
+  if (!e || !out) return SHP_ERR_ARG;
+  return guarded(e, [&]() {
+    // a clock-only event: stream -1, no key; lanes see it as a (possible) onTimeChange call
+    int64_t ts = now;
+    int32_t st = -1, k = 0;
+    std::vector<const void*> cols(MAXCOL, nullptr);
+    std::vector<std::vector<uint8_t>> zero(e->comp.P.ncol, std::vector<uint8_t>(8, 0));
+    for (int c = 0; c < e->comp.P.ncol; c++) cols[c] = zero[c].data();
+    shp_batch b{1, &ts, &k, &st, cols.data(), nullptr};
+    e->stage(&b, hipMemcpyHostToDevice);
+    int rc = e->run(1, true);
+    if (rc != SHP_OK) return rc;
+    e->fetch(out);
+    return SHP_OK;
+  });
+}
+
+int shp_engine_num_states(const shp_engine* e) { return e ? e->comp.P.nstates : 0; }
+int shp_engine_path(const shp_engine* e) { return e ? e->fast : -1; }
+
+double shp_last_kernel_ms(const shp_engine* e, const char* which) {
+  if (!e) return -1;
+  std::string w = which ? which : "total";
+  if (w == "partition") return e->last_ms_part;
+  if (w == "nfa") return e->last_ms_nfa;
+  if (w == "total") return e->last_ms_total;
+  return e->kt.get(w);
+}
+
+const char* shp_last_error(const shp_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+void shp_engine_destroy(shp_engine* e) { delete e; }
+}

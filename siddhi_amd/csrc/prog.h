@@ -1,0 +1,104 @@
+// siddhi-hip: compiled NFA program (host-built, device-resident, POD).
+//
+// The program is the flattened processor graph that the reference builds in
+// StateInputStreamParser.parse (core/util/parser/StateInputStreamParser.java:148-408)
+// plus the condition trees of its FilterProcessors, lowered to a predicate bytecode.
+#pragma once
+#include <stdint.h>
+
+#ifndef SHP_HD
+#if defined(__HIPCC__)
+#define SHP_HD __host__ __device__
+#else
+#define SHP_HD
+#endif
+#endif
+
+namespace shp {
+
+constexpr int MAXS = 8;       // states (StateEvent slots)
+constexpr int MAXP = 8;       // pre/post processors
+constexpr int MAXQ = 4;       // schedulers (absent processors)
+constexpr int MAXCOL = 8;     // predicate input columns
+constexpr int MAXSTREAM = 8;  // input streams
+constexpr int NV = 4;         // attribute values captured per StreamEvent node
+constexpr int MAXCODE = 192;  // bytecode instructions
+constexpr int MAXSTACK = 12;  // predicate VM stack depth
+
+enum Kind : int8_t { K_STREAM = 0, K_COUNT, K_LOGICAL, K_ABSENT_STREAM, K_ABSENT_LOGICAL };
+enum SeqType : int8_t { PATTERN = 0, SEQUENCE = 1 };
+enum LType : int8_t { L_AND = 0, L_OR = 1 };
+enum Tag : int8_t { T_NULL = 0, T_INT, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL, T_STR };
+
+enum Op : uint8_t {
+  OP_END = 0,
+  OP_CONST,        // push imm, tag a
+  OP_VAR,          // a=state, b=(int8)index, c=column
+  OP_ISNULLSTATE,  // a=state, b=(int8)index
+  OP_AND,          // short-circuit: pop x; if !TRUE push FALSE, jump d
+  OP_ANDEND,       // pop y; push y==TRUE
+  OP_OR,           // pop x; if TRUE push TRUE, jump d
+  OP_OREND,        // pop y; push y==TRUE
+  OP_NOT,          // pop x; push !(x==TRUE)
+  OP_ISNULL,       // pop x; push x==NULL
+  OP_CMP,          // a=cmp(0 gt 1 ge 2 lt 3 le 4 eq 5 ne), b=promoted tag
+  OP_ARITH,        // a=op(0 add 1 sub 2 mul 3 div 4 mod), b=result tag
+};
+
+struct Instr {
+  uint8_t op, a, b, c;
+  int32_t d;
+  int64_t imm;
+};
+
+struct DPre {
+  int8_t kind, stateId, isStart, stream;
+  int8_t logical, sched, pad0, pad1;
+  int16_t withinEvery, thisPost, thisLast, partner, countPost, filterPc;
+  int32_t minCount, maxCount;
+  int64_t waiting;
+};
+
+struct DPost {
+  int8_t kind, stateId, hasNext, logical;
+  int16_t nextState, nextEvery, thisPre, callbackPre, partnerPre, partnerPost;
+  int32_t minCount, maxCount;
+};
+
+struct DevProg {
+  int32_t type, nstates, npre, nsched, nstream, ncol, ncode;
+  int32_t playback, partitioned;
+  int64_t within;
+  int8_t startIds[MAXS];
+  int32_t nstart;
+  DPre pre[MAXP];
+  DPost post[MAXP];
+  int8_t expireOrder[MAXP];
+  int8_t initOrder[MAXP];
+  int8_t resetOrder[MAXP];
+  int8_t updateOrder[MAXP];
+  int8_t nexpire, ninit, nreset, nupdate;
+  int8_t startup[MAXQ];
+  int8_t schedPre[MAXQ];
+  int8_t nstartup, pad2, pad3, pad4;
+  int8_t recvCount[MAXSTREAM];
+  int8_t recvMulti[MAXSTREAM];
+  int8_t recvSelector[MAXSTREAM];
+  int8_t recvPre[MAXSTREAM][MAXP];
+  int8_t colStream[MAXCOL];
+  int8_t colTag[MAXCOL];
+  int8_t colPos[MAXCOL];
+  int8_t streamNcol[MAXSTREAM];
+  int8_t streamCols[MAXSTREAM][NV];
+  Instr code[MAXCODE];
+};
+
+// Recognised shape for the specialised kernel (2-state `every e1=S[f1] -> e2=S[f2] within W`,
+// same stream, both states plain stream states).
+struct FastShape {
+  int32_t ok;
+  int32_t stream;
+  int64_t within;
+};
+
+}  // namespace shp

@@ -1,0 +1,170 @@
+"""ctypes binding of libsiddhi_hip.so (include/siddhi_hip.h).
+
+This is the product path: there is no CPU fallback.  Loading fails loudly when
+the library is missing, and engine creation fails when no HIP device is present.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsiddhi_hip.so")
+_lib = None
+
+SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACITY",
+              -4: "SHP_ERR_OUTPUT", -5: "SHP_ERR_DEVICE", -6: "SHP_ERR_KEYS"}
+
+SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches",
+           "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms",
+           "shp_last_error", "shp_engine_destroy", "shp_synth_fill"]
+
+
+class ShpConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("max_keys", ctypes.c_int32), ("max_batch", ctypes.c_int64),
+                ("max_matches", ctypes.c_int64), ("start_clock", ctypes.c_int64),
+                ("force_general", ctypes.c_int32), ("profile_kernels", ctypes.c_int32)]
+
+
+class ShpBatch(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("ts", ctypes.c_void_p), ("key", ctypes.c_void_p),
+                ("stream", ctypes.c_void_p), ("cols", ctypes.c_void_p), ("nulls", ctypes.c_void_p)]
+
+
+class ShpMatches(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_int64), ("num_states", ctypes.c_int32),
+                ("key", ctypes.c_void_p), ("ts", ctypes.c_void_p), ("type", ctypes.c_void_p),
+                ("pos", ctypes.c_void_p), ("ref_off", ctypes.c_void_p), ("slot_len", ctypes.c_void_p),
+                ("refs", ctypes.c_void_p)]
+
+
+class ShpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{SHP_ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run `python -m siddhi_amd.build` "
+                              f"(there is no CPU fallback for the state path)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.shp_engine_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(ShpConfig), ctypes.POINTER(ctypes.c_void_p)]
+        for f in ("shp_push_batch", "shp_push_batch_device"):
+            getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpBatch), ctypes.POINTER(ShpMatches)]
+        L.shp_fetch_matches.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpMatches)]
+        L.shp_advance_clock.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ShpMatches)]
+        L.shp_engine_num_states.argtypes = [ctypes.c_void_p]
+        L.shp_engine_path.argtypes = [ctypes.c_void_p]
+        L.shp_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        L.shp_last_kernel_ms.restype = ctypes.c_double
+        L.shp_last_error.argtypes = [ctypes.c_void_p]
+        L.shp_last_error.restype = ctypes.c_char_p
+        L.shp_engine_destroy.argtypes = [ctypes.c_void_p]
+        L.shp_synth_fill.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                     ctypes.c_int] + [ctypes.c_void_p] * 6
+        _lib = L
+    return _lib
+
+
+def _arr(ptr, n, dtype):
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype)
+    buf = (ctypes.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype, count=n).copy()
+
+
+def matches_to_numpy(mt: ShpMatches):
+    m, S = mt.m, mt.num_states
+    slot_len = _arr(mt.slot_len, m * S, np.int16).reshape(m, S).astype(np.int32)
+    nrefs = int(slot_len.sum())
+    return {
+        "key": _arr(mt.key, m, np.int32), "ts": _arr(mt.ts, m, np.int64), "type": _arr(mt.type, m, np.int8),
+        "pos": _arr(mt.pos, m, np.int64), "slot_len": slot_len, "refs": _arr(mt.refs, nrefs, np.int64),
+    }
+
+
+class HipEngine:
+    """One engine per query (libsiddhi_hip.so). Same interface as the test oracle."""
+
+    def __init__(self, program_json: str, start_clock: int = 0, max_keys: int = 1 << 16,
+                 max_batch: int = 1 << 20, max_matches: int = 0, device: int = 0, force_general: bool = False,
+                 profile_kernels: bool = False):
+        L = lib()
+        cfg = ShpConfig(device, max_keys, max_batch, max_matches, int(start_clock), int(force_general),
+                        int(profile_kernels))
+        h = ctypes.c_void_p()
+        rc = L.shp_engine_create(program_json.encode(), ctypes.byref(cfg), ctypes.byref(h))
+        if rc != 0:
+            raise ShpError(rc, "shp_engine_create failed (see stderr)")
+        self.h = h
+        self.S = L.shp_engine_num_states(h)
+        self.max_batch = max_batch
+        self._pending = None
+
+    @property
+    def path(self):
+        return lib().shp_engine_path(self.h)
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ShpError(rc, lib().shp_last_error(self.h).decode())
+
+    def push(self, ts, key, stream, cols, nulls):
+        L = lib()
+        n = len(ts)
+        out_all = []
+        for lo in range(0, max(n, 1), self.max_batch):
+            hi = min(n, lo + self.max_batch)
+            if hi <= lo:
+                break
+            t = np.ascontiguousarray(ts[lo:hi], np.int64)
+            k = np.ascontiguousarray(key[lo:hi], np.int32)
+            s = np.ascontiguousarray(stream[lo:hi], np.int32)
+            cs = [np.ascontiguousarray(c[lo:hi]) for c in cols]
+            ns = [None if m is None else np.ascontiguousarray(m[lo:hi], np.uint8) for m in nulls]
+            colp = (ctypes.c_void_p * max(1, len(cs)))(*[c.ctypes.data for c in cs])
+            nulp = (ctypes.c_void_p * max(1, len(ns)))(*[0 if m is None else m.ctypes.data for m in ns])
+            b = ShpBatch(hi - lo, t.ctypes.data, k.ctypes.data, s.ctypes.data,
+                         ctypes.cast(colp, ctypes.c_void_p), ctypes.cast(nulp, ctypes.c_void_p))
+            mt = ShpMatches()
+            self._check(L.shp_push_batch(self.h, ctypes.byref(b), ctypes.byref(mt)))
+            out_all.append(matches_to_numpy(mt))
+        self._pending = _concat(out_all, self._pending, self.S)
+
+    def advance(self, now):
+        mt = ShpMatches()
+        self._check(lib().shp_advance_clock(self.h, int(now), ctypes.byref(mt)))
+        self._pending = _concat([matches_to_numpy(mt)], self._pending, self.S)
+
+    def fetch(self):
+        out = self._pending if self._pending is not None else _concat([], None, self.S)
+        self._pending = None
+        return out
+
+    def kernel_ms(self, which="total"):
+        return lib().shp_last_kernel_ms(self.h, which.encode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().shp_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _concat(parts, prev, S):
+    parts = ([prev] if prev is not None else []) + list(parts)
+    if not parts:
+        return {"key": np.zeros(0, np.int32), "ts": np.zeros(0, np.int64), "type": np.zeros(0, np.int8),
+                "pos": np.zeros(0, np.int64), "slot_len": np.zeros((0, S), np.int32),
+                "refs": np.zeros(0, np.int64)}
+    return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}

@@ -1,0 +1,133 @@
+"""GPU parity: libsiddhi_hip.so (HIP, gfx950) against the oracle, bit-exact per key.
+
+* every in-scope transcribed reference known-answer test, through the general NFA
+  lanes and through the engine's default path selection;
+* synthetic §8d streams for every config shape (C1..C5, plus the C3 `every <1:5>`
+  variant), general lanes and the specialised 2-state kernel, whole and split batches;
+* device generator == numpy generator; error behaviour of the boundary.
+"""
+import numpy as np
+import pytest
+
+from diff_util import compare, per_key, program_for, run, small_stream
+from golden_runner import load_fixtures, run_fixture
+from oracle.oracle import OracleEngine
+from test_oracle_golden import OUT_OF_SCOPE
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = [f for f in load_fixtures() if f["name"] not in OUT_OF_SCOPE]
+
+
+def hip(force_general, max_keys=256, max_batch=1 << 16, **kw):
+    from siddhi_amd.native import HipEngine
+
+    def make(pj, start):
+        return HipEngine(pj, start, max_keys=max_keys, max_batch=max_batch, force_general=force_general, **kw)
+    return make
+
+
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["name"] for f in FIXTURES])
+def test_golden_general_lanes(fx):
+    ok, msg, _ = run_fixture(fx, hip(True))
+    assert ok, f'{fx["source"]}: {msg}'
+
+
+FAST_FIXTURES = []
+for _f in FIXTURES:
+    try:
+        from siddhi_amd.query.compiler import compile_app
+        _, _qs, _ = compile_app(_f["app"])
+        if len(_qs) == 1:
+            FAST_FIXTURES.append(_f)
+    except Exception:
+        pass
+
+
+@pytest.mark.parametrize("fx", FAST_FIXTURES, ids=[f["name"] for f in FAST_FIXTURES])
+def test_golden_default_path(fx):
+    ok, msg, _ = run_fixture(fx, hip(False))
+    assert ok, f'{fx["source"]}: {msg}'
+
+
+CASES = [
+    ("c1", 1, 20000, 1),
+    ("c2", 2, 50000, 64),
+    ("c3", 3, 40000, 64),
+    ("c3b", "3b", 40000, 64),
+    ("c4", 4, 60000, 200),
+    ("c5", 5, 50000, 64),
+]
+
+
+@pytest.mark.parametrize("name,q,n,keys", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("general", [True, False], ids=["general", "default"])
+@pytest.mark.parametrize("batch", [None, 9973], ids=["whole", "split"])
+def test_synthetic_matches_oracle(name, q, n, keys, general, batch):
+    cq = program_for(q)
+    g = small_stream(q, n, keys)
+    a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    eng = hip(general, max_keys=keys, max_batch=batch or n)(cq.program_json(), 0)
+    if q in (2, 5, 1) and not general:
+        assert eng.path == 1, "2-state every/within shape should select the specialised kernel"
+    b = per_key(run(eng, cq, g, batch))
+    msg = compare(a, b)
+    assert msg is None, msg
+    if q != 3:
+        assert sum(len(v) for v in a.values()) > 0
+
+
+def test_c2_10k_keys_fast_path_vs_oracle():
+    """C2 shape at its real key count (10k keys), 2M events, specialised kernel vs oracle."""
+    cq = program_for(2)
+    g = small_stream(2, 2_000_000, 10_000)
+    a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    eng = hip(False, max_keys=10_000, max_batch=1 << 21)(cq.program_json(), 0)
+    assert eng.path == 1
+    b = per_key(run(eng, cq, g, 700_001))
+    assert compare(a, b) is None
+    assert sum(len(v) for v in a.values()) > 100_000
+
+
+def test_device_generator_matches_numpy():
+    import torch
+    from siddhi_amd import native, synth
+    n = 100_003
+    for cfg in (2, 4):
+        spec = synth.CONFIGS[cfg]
+        ts = torch.empty(n, dtype=torch.int64, device="cuda")
+        key = torch.empty(n, dtype=torch.int32, device="cuda")
+        price = torch.empty(n, dtype=torch.float32, device="cuda")
+        vol = torch.empty(n, dtype=torch.int64, device="cuda")
+        st = torch.empty(n, dtype=torch.int32, device="cuda")
+        rc = native.lib().shp_synth_fill(cfg, 12345, n, spec.keys, spec.n_streams, int(spec.dense),
+                                         ts.data_ptr(), key.data_ptr(), price.data_ptr(), vol.data_ptr(),
+                                         st.data_ptr(), None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        ref = synth.generate(spec, 12345, n)
+        assert (ts.cpu().numpy() == ref["ts"]).all()
+        assert (key.cpu().numpy() == ref["key"]).all()
+        assert (price.cpu().numpy().view(np.uint32) == ref["price"].view(np.uint32)).all()
+        assert (vol.cpu().numpy() == ref["volume"]).all()
+        assert (st.cpu().numpy() == ref["stream"]).all()
+
+
+def test_key_out_of_range_fails_loudly():
+    from siddhi_amd.native import HipEngine, ShpError
+    cq = program_for(2)
+    eng = HipEngine(cq.program_json(), 0, max_keys=8, max_batch=1024)
+    g = small_stream(2, 100, 64)
+    with pytest.raises(ShpError, match="SHP_ERR_KEYS"):
+        run(eng, cq, g)
+
+
+def test_decreasing_ts_on_fast_path_fails_loudly():
+    from siddhi_amd.native import HipEngine, ShpError
+    cq = program_for(2)
+    eng = HipEngine(cq.program_json(), 0, max_keys=4, max_batch=1024)
+    assert eng.path == 1
+    g = small_stream(2, 200, 4)
+    g["ts"] = g["ts"][::-1].copy()
+    with pytest.raises(ShpError, match="SHP_ERR_UNSUPPORTED"):
+        run(eng, cq, g)
