@@ -97,6 +97,10 @@ int shp_engine_path(const shp_engine* e);
  * siddhi_amd/synth.py). Any output pointer may be NULL. hip_stream: a hipStream_t or NULL. */
 int shp_synth_fill(int config, int64_t start, int64_t count, int64_t keys, int n_streams, int dense,
                    int64_t* ts, int32_t* key, float* price, int64_t* volume, int32_t* stream, void* hip_stream);
+/* Bench/test utilities: device memory without a second HIP runtime in the process. */
+void* shp_dev_alloc(int64_t bytes);
+int shp_dev_free(void* p);
+int shp_dev_to_host(void* dst, const void* src, int64_t bytes);
 /* Device time (ms) of the last push measured with HIP events on the engine stream:
  * which = "total" | "partition" | "nfa" | a kernel name (needs cfg.profile_kernels), e.g.
  * "radix_sort", "nfa_lanes", "fast_search", "fast_emit". */

@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libsiddhi_hip.so")
 SRC = os.path.join(HERE, "csrc")
-DEPS = ["engine.hip", "synth.hip", "nfa_lane.h", "fastpath.h", "prog.h", "compile.h", "jsonv.h"]
+DEPS = ["engine.hip", "synth.hip", "nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h"]
 
 
 def _stale() -> bool:

@@ -392,6 +392,61 @@ class ProgramCompiler {
     }
   }
 
+  bool fastOperand(const JV& e, FOperand& o) {
+    const std::string& op = e.get("op").sv;
+    o = FOperand{};
+    if (op == "const") {
+      o.kind = 0;
+      o.tag = tagOf(e.get("type").sv);
+      const JV& v = e.get("v");
+      switch (o.tag) {
+        case T_FLOAT: { float f = (float)v.d(); uint32_t u; memcpy(&u, &f, 4); o.imm = u; break; }
+        case T_DOUBLE: { double d = v.d(); memcpy(&o.imm, &d, 8); break; }
+        case T_BOOL: o.imm = v.t == JV::BOOLEAN ? v.bv : v.i() != 0; break;
+        case T_NULL: return false;
+        default: o.imm = v.i(); break;
+      }
+      return true;
+    }
+    if (op == "var") {
+      int idx = (int)e.get("index").i();
+      int stt = (int)e.get("state").i();
+      if (!(idx == 0 || idx == -1) || stt < 0 || stt > 1) return false;
+      o.kind = 1;
+      o.state = (int8_t)stt;
+      int col = (int)e.get("col").i();
+      o.pos = P.colPos[col];
+      o.tag = P.colTag[col];
+      return true;
+    }
+    return false;
+  }
+  bool fastTerm(const JV& e, FTerm& t) {
+    if (e.get("op").sv != "cmp") return false;
+    static const char* names[] = {"gt", "ge", "lt", "le", "eq", "ne"};
+    t = FTerm{};
+    for (int i = 0; i < 6; i++)
+      if (e.get("cmp").sv == names[i]) t.cmp = (int8_t)i;
+    if (!fastOperand(e.get("a"), t.a) || !fastOperand(e.get("b"), t.b)) return false;
+    t.ptype = (int8_t)promote(t.a.tag, t.b.tag);
+    return t.ptype != T_NULL;
+  }
+  bool fastPred(const JV& f, FPred& p) {
+    p = FPred{};
+    if (f.t == JV::NIL) return true;
+    const std::string& op = f.get("op").sv;
+    if (op == "cmp") {
+      p.n = 1;
+      return fastTerm(f, p.t[0]);
+    }
+    if (op == "and" || op == "or") {
+      p.n = 2;
+      p.combine = op == "or";
+      return fastTerm(f.get("a"), p.t[0]) && fastTerm(f.get("b"), p.t[1]);
+    }
+    return false;
+  }
+
   // every e1=S[f1] -> e2=S[f2] within W  (SURVEY.md Appendix A.7 closed form)
   void detectFast(const JV& root) {
     fast.ok = 0;
@@ -404,6 +459,8 @@ class ProgramCompiler {
     if (a.get("x").get("state").i() != 0 || b.get("state").i() != 1) return;
     if (P.pre[0].stream != P.pre[1].stream) return;
     if (P.ncol > 2) return;
+    const JV& st = root.get("states");
+    if (!fastPred(st[0].get("filter"), fast.f1) || !fastPred(st[1].get("filter"), fast.f2)) return;
     fast.ok = 1;
     fast.stream = P.pre[0].stream;
     fast.within = P.within;

@@ -93,12 +93,33 @@ struct DevProg {
   Instr code[MAXCODE];
 };
 
+// Register-only predicate for the specialised kernel: up to two comparisons joined by
+// AND/OR, each operand a constant or an attribute of slot 0 (candidate e1) / slot 1 (e2).
+struct FOperand {
+  int8_t kind;   // 0 const, 1 var
+  int8_t state;  // 0 or 1
+  int8_t pos;    // value position within the event's predicate columns (0/1)
+  int8_t tag;    // value tag
+  int32_t pad;
+  int64_t imm;
+};
+struct FTerm {
+  int8_t cmp, ptype, pad[6];
+  FOperand a, b;
+};
+struct FPred {
+  int32_t n;        // 0: no filter (always true), 1 or 2 terms
+  int32_t combine;  // 0 AND, 1 OR
+  FTerm t[2];
+};
+
 // Recognised shape for the specialised kernel (2-state `every e1=S[f1] -> e2=S[f2] within W`,
-// same stream, both states plain stream states).
+// same stream, both states plain stream states, filters expressible as FPred).
 struct FastShape {
   int32_t ok;
   int32_t stream;
   int64_t within;
+  FPred f1, f2;
 };
 
 }  // namespace shp

@@ -78,3 +78,13 @@ extern "C" int shp_synth_fill(int config, int64_t start, int64_t count, int64_t 
                                                        volume, stream);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+
+// Bench/test utilities: device buffers without a second HIP runtime in the process.
+extern "C" void* shp_dev_alloc(int64_t bytes) {
+  void* p = nullptr;
+  return hipMalloc(&p, bytes > 0 ? bytes : 1) == hipSuccess ? p : nullptr;
+}
+extern "C" int shp_dev_free(void* p) { return hipFree(p) == hipSuccess ? 0 : -5; }
+extern "C" int shp_dev_to_host(void* dst, const void* src, int64_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -5;
+}

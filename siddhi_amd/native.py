@@ -19,7 +19,8 @@ SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACIT
 
 SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches",
            "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms",
-           "shp_last_error", "shp_engine_destroy", "shp_synth_fill"]
+           "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
+           "shp_dev_to_host"]
 
 
 class ShpConfig(ctypes.Structure):
@@ -67,6 +68,10 @@ def lib():
         L.shp_engine_destroy.argtypes = [ctypes.c_void_p]
         L.shp_synth_fill.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                      ctypes.c_int] + [ctypes.c_void_p] * 6
+        L.shp_dev_alloc.restype = ctypes.c_void_p
+        L.shp_dev_alloc.argtypes = [ctypes.c_int64]
+        L.shp_dev_free.argtypes = [ctypes.c_void_p]
+        L.shp_dev_to_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         _lib = L
     return _lib
 

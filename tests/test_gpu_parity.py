@@ -90,27 +90,31 @@ def test_c2_10k_keys_fast_path_vs_oracle():
 
 
 def test_device_generator_matches_numpy():
-    import torch
+    """shp_synth_fill (HIP) is bit-identical to siddhi_amd.synth (numpy PCG32)."""
     from siddhi_amd import native, synth
+    L = native.lib()
     n = 100_003
     for cfg in (2, 4):
         spec = synth.CONFIGS[cfg]
-        ts = torch.empty(n, dtype=torch.int64, device="cuda")
-        key = torch.empty(n, dtype=torch.int32, device="cuda")
-        price = torch.empty(n, dtype=torch.float32, device="cuda")
-        vol = torch.empty(n, dtype=torch.int64, device="cuda")
-        st = torch.empty(n, dtype=torch.int32, device="cuda")
-        rc = native.lib().shp_synth_fill(cfg, 12345, n, spec.keys, spec.n_streams, int(spec.dense),
-                                         ts.data_ptr(), key.data_ptr(), price.data_ptr(), vol.data_ptr(),
-                                         st.data_ptr(), None)
-        assert rc == 0
-        torch.cuda.synchronize()
+        bufs = {k: L.shp_dev_alloc(n * sz) for k, sz in
+                (("ts", 8), ("key", 4), ("price", 4), ("volume", 8), ("stream", 4))}
+        try:
+            rc = L.shp_synth_fill(cfg, 12345, n, spec.keys, spec.n_streams, int(spec.dense), bufs["ts"],
+                                  bufs["key"], bufs["price"], bufs["volume"], bufs["stream"], None)
+            assert rc == 0
+            got = {}
+            for k, dt in (("ts", np.int64), ("key", np.int32), ("price", np.float32), ("volume", np.int64),
+                          ("stream", np.int32)):
+                a = np.empty(n, dt)
+                assert L.shp_dev_to_host(a.ctypes.data, bufs[k], a.nbytes) == 0
+                got[k] = a
+        finally:
+            for p in bufs.values():
+                L.shp_dev_free(p)
         ref = synth.generate(spec, 12345, n)
-        assert (ts.cpu().numpy() == ref["ts"]).all()
-        assert (key.cpu().numpy() == ref["key"]).all()
-        assert (price.cpu().numpy().view(np.uint32) == ref["price"].view(np.uint32)).all()
-        assert (vol.cpu().numpy() == ref["volume"]).all()
-        assert (st.cpu().numpy() == ref["stream"]).all()
+        for k in ("ts", "key", "volume", "stream"):
+            assert (got[k] == ref[k]).all(), k
+        assert (got["price"].view(np.uint32) == ref["price"].view(np.uint32)).all()
 
 
 def test_key_out_of_range_fails_loudly():
