@@ -27,7 +27,11 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 BYTES_PER_EVENT = 16    # ts 8 + key 4 + price 4
-BYTES_PER_MATCH = 16    # 2 x u32 idx + i64 ts
+BYTES_PER_MATCH = 16    # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
+KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_solve", "sw_expand",
+           "radix_sort", "clock_scan", "key_hist", "key_scan", "sort_keys", "iota", "clamp_clock",
+           "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry", "nfa_lanes")
+PATHS = {2: "sweep (owner partition + LDS sweep)", 1: "scan kernels over a key-sorted batch", 0: "general NFA lanes"}
 
 
 def parse():
@@ -39,7 +43,8 @@ def parse():
     ap.add_argument("--keys", type=int, default=10_000)
     ap.add_argument("--cpu-sample", type=int, default=2_500_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--general", action="store_true", help="force the general NFA lanes")
+    ap.add_argument("--path", choices=["auto", "general", "scan"], default="auto",
+                    help="auto = sweep path (default); scan = round-1 scan kernels; general = NFA lanes")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
     return ap.parse_args()
 
@@ -64,8 +69,10 @@ def main():
     cq = qs[0]
     N, K, G = a.events, a.keys, world
     cap = int(N * 1.08) + 4096 if G > 1 else N
+    force = {"auto": 0, "general": 1, "scan": 2}[a.path]
     eng = native.HipEngine(cq.program_json(), 0, max_keys=K, max_batch=cap, max_matches=cap,
-                           device=local, force_general=a.general, profile_kernels=True)
+                           device=local, force_general=force, profile_kernels=True,
+                           match_layout=native.LAYOUT_PAIRS if force == 0 else native.LAYOUT_FULL)
     L = native.lib()
     steps = a.warmup + a.steps
 
@@ -81,7 +88,6 @@ def main():
         return ts, key, price
 
     batches = [gen(s) for s in range(steps)]
-    stream0 = torch.zeros(cap, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
 
     def exchange(ts, key, price):
@@ -109,8 +115,8 @@ def main():
             torch.cuda.current_stream().synchronize()  # engine runs on its own HIP stream
         n = ts.numel()
         colp = (ctypes.c_void_p * 1)(price.data_ptr())
-        b = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), stream0.data_ptr(), ctypes.cast(colp, ctypes.c_void_p),
-                            None)
+        # one input stream: the stream column is NULL (= every event on stream 0)
+        b = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), None, ctypes.cast(colp, ctypes.c_void_p), None)
         mt = native.ShpMatches()
         rc = L.shp_push_batch_device(eng.h, ctypes.byref(b), ctypes.byref(mt))
         if rc != 0:
@@ -129,9 +135,7 @@ def main():
         n, m = step(i)
         ev_local += n
         m_local += m
-        for name in ("radix_sort", "clock_scan", "key_hist", "key_scan", "sort_keys", "iota", "clamp_clock",
-                     "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry",
-                     "nfa_lanes"):
+        for name in KERNELS:
             kernel_ms[name] = kernel_ms.get(name, 0.0) + eng.kernel_ms(name)
     torch.cuda.synchronize()
     if dist:
@@ -185,7 +189,7 @@ def main():
                 "events_per_gpu_per_step": N,
                 "keys": K,
                 "parallelism": f"key-sharded x{G}" + (" (RCCL all-to-all by key owner)" if G > 1 else ""),
-                "engine_path": "specialised 2-state kernel" if eng.path == 1 else "general NFA lanes",
+                "engine_path": PATHS.get(eng.path, str(eng.path)),
                 "matches_per_s": m_total / elapsed,
                 "matches_per_step_gpu0": m_per_launch,
                 "p50_batch_ms": elapsed / a.steps * 1e3,

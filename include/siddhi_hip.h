@@ -8,7 +8,7 @@
  * and fed through StreamJunction.Receiver.receive(...)
  *   modules/siddhi-core/src/main/java/io/siddhi/core/stream/StreamJunction.java:443-456
  * by the Pattern/Sequence{Single,Multi}ProcessStreamReceivers
- *   modules/siddhi-core/src/main/java/io/siddhi/core/query/input/stream/state/receiver/*.java
+ *   modules/siddhi-core/src/main/java/io/siddhi/core/query/input/stream/state/receiver/ (all)
  * and emits one StateEvent per match into QuerySelector.process
  *   modules/siddhi-core/src/main/java/io/siddhi/core/query/selector/QuerySelector.java:76-99.
  * The entry points below replace, respectively:
@@ -49,9 +49,17 @@ typedef struct shp_config {
   int64_t max_batch;       /* largest n accepted by one push */
   int64_t max_matches;     /* match-record capacity per push */
   int64_t start_clock;     /* event-time clock at start() (0 in playback mode) */
-  int32_t force_general;   /* 1: never use the specialised 2-state kernel */
+  int32_t force_general;   /* 1: general NFA lanes only; 2: no sweep path (scan kernel or lanes) */
   int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
+  int32_t match_layout;    /* SHP_LAYOUT_FULL (0) or SHP_LAYOUT_PAIRS (1, sweep path only) */
 } shp_config;
+
+/* Match layouts. FULL: every field of shp_matches is valid. PAIRS (2-state sweep path,
+ * device pushes): only `refs` is written, as m pairs (e1 seq, e2 seq); the other fields are
+ * implied: ref_off[i] = 2i, slot_len = {1, 1}, pos = ts-event = refs[2i+1], type CURRENT,
+ * key/ts = those of event refs[2i+1] in the pushed batch. shp_fetch_matches expands them. */
+#define SHP_LAYOUT_FULL 0
+#define SHP_LAYOUT_PAIRS 1
 
 /* One batch of events in SoA form. Column c follows program["columns"][c]:
  * int->int32, long->int64, float->float32, double->float64, bool->uint8,
@@ -60,7 +68,7 @@ typedef struct shp_batch {
   int64_t n;
   const int64_t* ts;
   const int32_t* key;      /* partition key id per event (0 when not partitioned) */
-  const int32_t* stream;   /* stream index per event (program["streams"] order) */
+  const int32_t* stream;   /* stream index per event (program["streams"] order); NULL = all 0 */
   const void* const* cols;
   const uint8_t* const* nulls;
 } shp_batch;
@@ -79,6 +87,7 @@ typedef struct shp_matches {
   const int64_t* ref_off;
   const int16_t* slot_len;
   const int64_t* refs;
+  int32_t layout;          /* SHP_LAYOUT_FULL or SHP_LAYOUT_PAIRS (see above) */
 } shp_matches;
 
 int shp_engine_create(const char* nfa_program_json, const shp_config* cfg, shp_engine** out);
@@ -90,7 +99,8 @@ int shp_push_batch_device(shp_engine* e, const shp_batch* in, shp_matches* out);
 int shp_fetch_matches(shp_engine* e, shp_matches* out);
 int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out);
 int shp_engine_num_states(const shp_engine* e);
-/* Which kernel the engine runs: 1 = specialised 2-state scan, 0 = general NFA lanes. */
+/* Which kernels the engine runs: 2 = sweep (owner partition + LDS sweep), 1 = specialised 2-state
+ * scan kernel, 0 = general NFA lanes. */
 int shp_engine_path(const shp_engine* e);
 /* Bench/test utility (not part of the reference boundary): fill device buffers with events
  * start..start+count-1 of the SURVEY.md §8d synthetic stream (PCG32, bit-identical to

@@ -26,6 +26,7 @@
 #include "compile.h"
 #include "fastpath.h"
 #include "nfa_lane.h"
+#include "sweep.h"
 
 using namespace shp;
 
@@ -113,8 +114,12 @@ struct shp_engine {
   shp_config cfg{};
   LaneLayout Y{};
   char* arena = nullptr;
-  int fast = 0;
+  int fast = 0;   // 1: specialised scan kernels (fastpath.h), 2: sweep (sweep.h)
   FastState fs{};
+  SweepState sw{};
+  bool expanded = true;  // sweep matches materialised as full records
+  BatchView lastB{};
+  const int32_t* lastKey = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   std::string err;
@@ -185,6 +190,7 @@ struct shp_engine {
     F(d_mtype);
     F(d_mslot);
     fs.release();
+    sw.release();
     kt.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -222,7 +228,14 @@ struct shp_engine {
     HIP_OK(hipMemcpy(dprog, &comp.P, sizeof(DevProg), hipMemcpyHostToDevice));
     clock = cfg.start_clock;
     while ((1ll << key_bits) <= cfg.max_keys) key_bits++;  // + one sentinel key for clock-only events
-    fast = comp.fast.ok && !cfg.force_general;
+    fast = comp.fast.ok && cfg.force_general != 1;
+    int32_t nown = 0;
+    std::vector<uint32_t> kmap;
+    if (fast && cfg.force_general == 0 && SweepState::shape_ok(comp.P, comp.fast) &&
+        SweepState::build_map(cfg.max_keys, nown, kmap))
+      fast = 2;
+    if (cfg.match_layout == SHP_LAYOUT_PAIRS && fast != 2)
+      throw CompileError(-2, "match_layout PAIRS needs the sweep path");
     kt.enabled = cfg.profile_kernels != 0;
     cap = cfg.max_batch + 1;
     alloc(d_ts, cap);
@@ -258,9 +271,15 @@ struct shp_engine {
     HIP_OK(rocprim::exclusive_scan(nullptr, b3, d_kcnt, d_kbeg, 0u, (size_t)cfg.max_keys, rocprim::plus<uint32_t>(),
                                    stream));
     tmp_bytes = std::max(b1, std::max(b2, b3));
-    if (fast) tmp_bytes = std::max(tmp_bytes, fs.scratch_bytes(cap, cfg.max_keys, stream));
+    if (fast == 1) tmp_bytes = std::max(tmp_bytes, fs.scratch_bytes(cap, cfg.max_keys, stream));
     HIP_OK(hipMalloc(&d_tmp, tmp_bytes));
-    if (fast) {
+    if (fast == 2) {
+      sw.create(comp.P, comp.fast, cfg.max_keys, cap, nown, kmap, stream);
+#ifdef SHP_SW_STAMPS
+      HIP_OK(hipMalloc((void**)&sw.D.stamps, (size_t)nown * 8 * sizeof(unsigned long long)));
+      HIP_OK(hipMemset(sw.D.stamps, 0, (size_t)nown * 8 * sizeof(unsigned long long)));
+#endif
+    } else if (fast == 1) {
       fs.create(comp.P, comp.fast, cfg.max_keys, cap, mcap, stream);
     } else {
       Y.build(cfg.max_keys);
@@ -277,37 +296,15 @@ struct shp_engine {
     const int64_t* x_ts = in ? in->ts : d_ts;
     const int32_t* x_key = in ? (P.partitioned ? in->key : d_key) : d_key;
     const int32_t* x_stream = in ? in->stream : d_stream;
-    if (in && !P.partitioned) HIP_OK(hipMemsetAsync(d_key, 0, n * 4, stream));
+    if (in && !P.partitioned && fast != 2) HIP_OK(hipMemsetAsync(d_key, 0, n * 4, stream));
+    if (!x_stream && fast != 2) {  // NULL stream column: every event on stream 0
+      HIP_OK(hipMemsetAsync(d_stream, 0, n * 4, stream));
+      x_stream = d_stream;
+    }
     HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), stream));
     HIP_OK(hipMemsetAsync(d_mcount, 0, 2 * sizeof(unsigned long long), stream));
     kt.begin_push();
     HIP_OK(hipEventRecord(ev0, stream));
-    int gb = (int)std::min<int64_t>((n + 255) / 256, 2048);
-    if (gb < 1) gb = 1;
-    // 1. clock
-    size_t tb = tmp_bytes;
-    kt.mark("clock_scan", stream);
-    HIP_OK(rocprim::inclusive_scan(d_tmp, tb, x_ts, d_rmax, (size_t)n, rocprim::maximum<int64_t>(), stream));
-    kt.mark("clamp_clock", stream);
-    k_clamp_clock<<<gb, 256, 0, stream>>>(d_rmax, n, clock);
-    // 2. partition by key (stable)
-    HIP_OK(hipMemsetAsync(d_kcnt, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
-    kt.mark("key_hist", stream);
-    k_key_hist<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_kcnt, cfg.max_keys, P.partitioned, d_err);
-    tb = tmp_bytes;
-    kt.mark("key_scan", stream);
-    HIP_OK(rocprim::exclusive_scan(d_tmp, tb, d_kcnt, d_kbeg, 0u, (size_t)cfg.max_keys, rocprim::plus<uint32_t>(),
-                                   stream));
-    kt.mark("sort_keys", stream);
-    k_sort_keys<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_skey, P.partitioned, (uint32_t)cfg.max_keys);
-    kt.mark("iota", stream);
-    k_iota<<<gb, 256, 0, stream>>>(d_idx, n);
-    tb = tmp_bytes;
-    kt.mark("radix_sort", stream);
-    HIP_OK(rocprim::radix_sort_pairs(d_tmp, tb, d_skey, d_skey2, d_idx, d_perm, (size_t)n, 0, key_bits + 1, stream));
-    kt.mark(nullptr, stream);
-    HIP_OK(hipEventRecord(ev1, stream));
-    // 3. NFA
     BatchView B{};
     B.n = n;
     B.seq0 = seq;
@@ -322,13 +319,55 @@ struct shp_engine {
       B.nulls[c] = in ? (in->nulls ? in->nulls[c] : nullptr) : d_nulls[c];
     }
     MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs};
-    if (fast) {
-      fs.run(P, B, O, d_perm, d_kbeg, d_kcnt, cfg.max_keys, d_tmp, tmp_bytes, d_err, stream, d_skey2, dprog, kt);
+    int64_t tsmax = INT64_MIN;
+    if (fast == 2) {
+      // sweep: no clock scan, no global sort (the engine clock is the running max of ts)
+      HIP_OK(hipEventRecord(ev1, stream));
+      if (!clock_only) sw.run(B, x_key, O, d_err, stream, kt);
+      lastB = B;
+      lastKey = x_key;
+      expanded = false;
+      if (cfg.match_layout == SHP_LAYOUT_FULL) {
+        sw.expand(B, x_key, O, stream, kt);
+        expanded = true;
+      }
+      HIP_OK(hipMemcpyAsync(&tsmax, sw.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
     } else {
-      int L = cfg.max_keys;
-      kt.mark("nfa_lanes", stream);
-      k_nfa_lanes<<<(L + 63) / 64, 64, 0, stream>>>(dprog, Y, arena, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+      int gb = (int)std::min<int64_t>((n + 255) / 256, 2048);
+      if (gb < 1) gb = 1;
+      // 1. clock
+      size_t tb = tmp_bytes;
+      kt.mark("clock_scan", stream);
+      HIP_OK(rocprim::inclusive_scan(d_tmp, tb, x_ts, d_rmax, (size_t)n, rocprim::maximum<int64_t>(), stream));
+      kt.mark("clamp_clock", stream);
+      k_clamp_clock<<<gb, 256, 0, stream>>>(d_rmax, n, clock);
+      // 2. partition by key (stable)
+      HIP_OK(hipMemsetAsync(d_kcnt, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
+      kt.mark("key_hist", stream);
+      k_key_hist<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_kcnt, cfg.max_keys, P.partitioned, d_err);
+      tb = tmp_bytes;
+      kt.mark("key_scan", stream);
+      HIP_OK(rocprim::exclusive_scan(d_tmp, tb, d_kcnt, d_kbeg, 0u, (size_t)cfg.max_keys, rocprim::plus<uint32_t>(),
+                                     stream));
+      kt.mark("sort_keys", stream);
+      k_sort_keys<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_skey, P.partitioned, (uint32_t)cfg.max_keys);
+      kt.mark("iota", stream);
+      k_iota<<<gb, 256, 0, stream>>>(d_idx, n);
+      tb = tmp_bytes;
+      kt.mark("radix_sort", stream);
+      HIP_OK(rocprim::radix_sort_pairs(d_tmp, tb, d_skey, d_skey2, d_idx, d_perm, (size_t)n, 0, key_bits + 1, stream));
       kt.mark(nullptr, stream);
+      HIP_OK(hipEventRecord(ev1, stream));
+      // 3. NFA
+      if (fast == 1) {
+        fs.run(P, B, O, d_perm, d_kbeg, d_kcnt, cfg.max_keys, d_tmp, tmp_bytes, d_err, stream, d_skey2, dprog, kt);
+      } else {
+        int L = cfg.max_keys;
+        kt.mark("nfa_lanes", stream);
+        k_nfa_lanes<<<(L + 63) / 64, 64, 0, stream>>>(dprog, Y, arena, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+        kt.mark(nullptr, stream);
+      }
+      if (n > 0) HIP_OK(hipMemcpyAsync(&tsmax, d_rmax + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
     }
     HIP_OK(hipEventRecord(ev2, stream));
     HIP_OK(hipGetLastError());
@@ -344,17 +383,27 @@ struct shp_engine {
     last_ms_nfa = b;
     last_ms_total = a + b;
     kt.collect();
-    // carry the clock: last rmax
-    if (n > 0) HIP_OK(hipMemcpy(&clock, d_rmax + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost));
+    // carry the clock (running max of ts, playback)
+    if (tsmax != INT64_MIN && tsmax > clock) clock = tsmax;
     if (!clock_only) seq += n;
-    last_m = (int64_t)cnt[0];
+    last_m = std::min<int64_t>((int64_t)cnt[0], mcap);
     if (herr) {
-      if (herr & (1 << 20)) return fail(SHP_ERR_KEYS, "partition key id >= max_keys");
+      if (herr & SWE_KEYS) return fail(SHP_ERR_KEYS, "partition key id >= max_keys");
       if (herr & E_OUT) return fail(SHP_ERR_OUTPUT, "match buffer too small for this batch (max_matches)");
-      if (herr & (1 << 21)) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state fast path");
+      if (herr & SWE_MONO) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state fast path");
+      if (herr & SWE_RANGE) return fail(SHP_ERR_UNSUPPORTED, "timestamps span more than 2^49 ms on the sweep path");
       return fail(SHP_ERR_CAPACITY, "per-key table capacity exceeded (code " + std::to_string(herr) + ")");
     }
     return SHP_OK;
+  }
+
+  // sweep path, PAIRS layout: materialise the full records of the last push on demand
+  void ensure_expanded() {
+    if (fast != 2 || expanded) return;
+    MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs};
+    sw.expand(lastB, lastKey, O, stream, kt);
+    HIP_OK(hipStreamSynchronize(stream));
+    expanded = true;
   }
 
   int fail(int code, const std::string& m) {
@@ -368,7 +417,8 @@ struct shp_engine {
     HIP_OK(hipMemcpyAsync(d_ts, in->ts, n * 8, kind, stream));
     if (P.partitioned) HIP_OK(hipMemcpyAsync(d_key, in->key, n * 4, kind, stream));
     else HIP_OK(hipMemsetAsync(d_key, 0, n * 4, stream));
-    HIP_OK(hipMemcpyAsync(d_stream, in->stream, n * 4, kind, stream));
+    if (in->stream) HIP_OK(hipMemcpyAsync(d_stream, in->stream, n * 4, kind, stream));
+    else HIP_OK(hipMemsetAsync(d_stream, 0, n * 4, stream));
     for (int c = 0; c < P.ncol; c++) {
       HIP_OK(hipMemcpyAsync(d_cols[c], in->cols[c], n * colBytes(P.colTag[c]), kind, stream));
       if (in->nulls && in->nulls[c]) HIP_OK(hipMemcpyAsync(d_nulls[c], in->nulls[c], n, kind, stream));
@@ -377,6 +427,7 @@ struct shp_engine {
   }
 
   void fill_device(shp_matches* out) {
+    out->layout = expanded ? SHP_LAYOUT_FULL : SHP_LAYOUT_PAIRS;
     out->m = last_m;
     out->num_states = comp.P.nstates;
     out->key = d_mkey;
@@ -390,6 +441,8 @@ struct shp_engine {
 
   // copy to host and order by (pos, per-lane order) so callbacks follow reference emission order
   void fetch(shp_matches* out) {
+    ensure_expanded();
+    out->layout = SHP_LAYOUT_FULL;
     int64_t m = last_m;
     int S = comp.P.nstates;
     std::vector<int32_t> k(m);
@@ -540,6 +593,7 @@ int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out) {
     e->stage(&b, hipMemcpyHostToDevice);
     int rc = e->run(1, true);
     if (rc != SHP_OK) return rc;
+    if (e->fast == 2 && now > e->clock) e->clock = now;
     e->fetch(out);
     return SHP_OK;
   });
@@ -556,6 +610,15 @@ double shp_last_kernel_ms(const shp_engine* e, const char* which) {
   if (w == "total") return e->last_ms_total;
   return e->kt.get(w);
 }
+
+#ifdef SHP_SW_STAMPS
+// diagnostic build only: per-owner solve phase cycles of the last push (nown * 8)
+int shp_debug_sw_stamps(shp_engine* e, unsigned long long* host, int64_t n) {
+  if (!e || e->fast != 2 || !e->sw.D.stamps) return SHP_ERR_ARG;
+  int64_t k = std::min<int64_t>(n, (int64_t)e->sw.D.nown * 8);
+  return hipMemcpy(host, e->sw.D.stamps, k * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)(k / 8) : SHP_ERR_DEVICE;
+}
+#endif
 
 const char* shp_last_error(const shp_engine* e) { return e ? e->err.c_str() : "null engine"; }
 

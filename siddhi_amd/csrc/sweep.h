@@ -1,0 +1,1058 @@
+// siddhi-hip: the "sweep" path — the 2-state `every e1=S[f1] -> e2=S[f2] within W`
+// query as two HBM passes (partition, then an LDS-resident per-owner sweep).
+//
+// Semantics (StreamPreStateProcessor.processAndReturn/expireEvents
+// :326-403 and the last-state-first order of PatternMultiProcessStreamReceiver :32-39):
+// per partition key, with non-decreasing timestamps, every event i with f1(i) opens
+// candidate i; candidate i closes at the first later event j of the key with
+// ts_j - ts_i <= W and f2(i, j), and expires at the first later event with ts_j - ts_i > W.
+// Matches are emitted in (j, i) order per key.  Candidates are independent of each other.
+//
+// Layout and passes:
+//   keys are hashed onto NOWN "owners" (host-built map key -> owner | local key << 16,
+//   <= SW_LK local keys per owner).
+//   k_sw_count    super-tile x owner histogram            reads key (+stream)      4 B/event
+//   exclusive scan of the NOWN x NST counts (owner-major)  -> stable owner regions
+//   k_sw_scatter  stable multisplit by owner (wave ballot ranks, no atomics), writes a
+//                 16-byte record {ts|local key, batch index, value} per event
+//                                                          reads 16 B, writes 16 B
+//   k_sw_solve    one workgroup per owner walks its region in chunks of SWS_CHUNK records:
+//                 carried open candidates + chunk -> stable split by local key in LDS ->
+//                 per-candidate forward scan -> per-closer counts -> block scan ->
+//                 (i, j) pairs written in (key, j, i) order -> open candidates carried.
+//                                                          reads 16 B, writes 16 B/match
+// Per-key emission order is exact; across keys the order is unspecified (as the ABI says).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <rocprim/rocprim.hpp>
+#include <cstring>
+#include <utility>
+#include <stdexcept>
+#include <vector>
+
+#include "fast_core.h"
+#include "fastpath.h"
+#include "nfa_lane.h"
+#include "prog.h"
+
+namespace shp {
+
+constexpr int SW_THREADS = 256;
+constexpr int SW_WAVES = SW_THREADS / 64;
+constexpr int SW_LK = 255;          // local keys per owner; bin 255 = "no item"
+constexpr int SW_MAXOWN = 2048;     // owners (partition bins)
+// partition
+constexpr int SWP_ROUND = 4096;
+constexpr int SWP_SEG = SWP_ROUND / SW_WAVES;
+constexpr int SWP_SUB = SWP_SEG / 64;
+// solve
+constexpr int SWS_CHUNK = 2048;
+constexpr int SWS_CCAP = 512;  // carried open candidates per owner
+constexpr int SWS_EMAX = SWS_CHUNK + SWS_CCAP;
+constexpr int SWS_SEG = SWS_EMAX / SW_WAVES;
+constexpr int SWS_SUB = SWS_SEG / 64;
+constexpr int SW_PROBE = 8;  // positions every candidate probes without a loop
+
+// error bits (engine.hip maps them to status codes)
+constexpr int SWE_KEYS = 1 << 20;   // key id outside [0, max_keys)
+constexpr int SWE_MONO = 1 << 21;   // ts decreases within a key
+constexpr int SWE_RANGE = 1 << 23;  // ts outside base +- 2^49 ms
+
+// 16-byte record.  kt: [63:56] local key (0xFF = none), [55] carried, [54] null,
+// [49:0] ts - base + 2^49.  ref: batch index (events) or carry slot (carried).
+struct __attribute__((aligned(16))) SwRec {
+  uint64_t kt;
+  uint32_t ref;
+  uint32_t v;
+};
+
+constexpr uint64_t SW_TSBIAS = 1ull << 49;
+constexpr uint64_t SW_TSMASK = (1ull << 50) - 1;
+constexpr uint64_t SW_CARRIED = 1ull << 55;
+constexpr uint64_t SW_NULL = 1ull << 54;
+
+__device__ __forceinline__ uint32_t sw_lk(uint64_t kt) { return (uint32_t)(kt >> 56); }
+__device__ __forceinline__ int64_t sw_ts(uint64_t kt) { return (int64_t)(kt & SW_TSMASK) - (int64_t)SW_TSBIAS; }
+__device__ __forceinline__ uint64_t sw_kt(uint32_t lk, int64_t rel, uint64_t flags) {
+  return ((uint64_t)lk << 56) | flags | ((uint64_t)(rel + (int64_t)SW_TSBIAS) & SW_TSMASK);
+}
+__device__ __forceinline__ bool sw_rel_ok(int64_t rel) {
+  return rel >= -(int64_t)SW_TSBIAS && rel < (int64_t)SW_TSBIAS;
+}
+
+struct SwTerm {
+  int32_t mask;  // outcomes that make the term true: 1 A<B, 2 A==B, 4 A>B, 8 unordered (NaN)
+  int8_t ak, bk; // operand kind: 0 const, 1 e1.v, 2 e2.v
+  int8_t flt;    // int column promoted to float: round through float
+  int8_t pad;
+  double ac, bc;
+};
+struct SwPred {
+  int32_t n, combine;  // terms (0: no filter), 0 AND / 1 OR
+  SwTerm t[2];
+};
+
+// Diagnostic build only (-DSHP_SW_STAMPS): per-owner cycle counts of the solve phases.
+#ifdef SHP_SW_STAMPS
+#define SW_STAMP(k)                          \
+  do {                                       \
+    __syncthreads();                         \
+    if (tid == 0) {                          \
+      uint64_t t_ = clock64();               \
+      st_acc[k] += t_ - st_prev;             \
+      st_prev = t_;                          \
+    }                                        \
+  } while (0)
+#else
+#define SW_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
+struct SweepDev {
+  SwPred f1, f2;
+  int64_t within;
+  int32_t vtag;  // tag of the predicate column, T_NULL when the query reads none
+  int32_t fstream;
+  int32_t nown, own_bits, nst, maxkeys;
+  int32_t lk_bits;       // bits of the largest local key id
+  int64_t st_len;
+  const uint32_t* kmap;  // key -> owner | local key << 16
+  uint32_t* cnt;         // nown * nst + 1: counts, scanned into off
+  uint32_t* off;
+  SwRec* recs;           // batch capacity
+  // per-owner carry across pushes
+  int32_t* c_n;          // nown
+  int64_t* c_ts;         // nown * SWS_CCAP, absolute ts
+  int64_t* c_seq;
+  uint32_t* c_v;
+  uint8_t* c_lk;
+  uint8_t* c_null;
+  int64_t* lastts;       // nown * SW_LK, absolute ts, INT64_MIN when unseen
+  int64_t* tsmax;        // running max of ts (engine clock)
+  unsigned long long* stamps;  // diagnostic build: nown * 8 phase cycle counts (else unused)
+};
+
+// Predicate terms lowered for the sweep (host, SweepState::lower): with one 4-byte column, every
+// operand of a compare is a constant, e1.v or e2.v, and Java's binary numeric promotion
+// (JLS 5.6.2, as CompareConditionExpressionExecutor*Float/Int/... apply it) is exact in double
+// once an int operand promoted to float has been rounded to float first.  A term is therefore
+// (op, A, B) over doubles; string ids compare by equality only (java_cmp's default branch).
+__device__ __forceinline__ bool sw_term(const SwTerm t, double c1f, double c1i, bool n1, double c2f, double c2i,
+                                        bool n2) {
+  const double c1 = t.flt ? c1f : c1i, c2 = t.flt ? c2f : c2i;
+  const double c12a = t.ak == 1 ? c1 : c2, c12b = t.bk == 1 ? c1 : c2;
+  const double A = t.ak == 0 ? t.ac : c12a;
+  const double B = t.bk == 0 ? t.bc : c12b;
+  const bool nul = (t.ak == 1 && n1) || (t.ak == 2 && n2) || (t.bk == 1 && n1) || (t.bk == 2 && n2);
+  // branch-free IEEE compare: gt {4}, ge {2,4}, lt {1}, le {1,2}, eq {2}, ne {1,4,8}
+  const int o3 = (A < B ? 1 : 0) | (A == B ? 2 : 0) | (A > B ? 4 : 0);
+  const bool r = ((o3 | (o3 == 0 ? 8 : 0)) & t.mask) != 0;
+  return !nul && r;  // CompareConditionExpressionExecutor: a null operand -> false
+}
+// NT: number of terms (template, so the probe loop is straight-line code); AND/OR without
+// short-circuit (terms have no side effects; And/OrConditionExpressionExecutor give the same value)
+template <int NT>
+__device__ __forceinline__ bool sw_pred(const SwPred& p, double c1f, double c1i, bool n1, double c2f, double c2i,
+                                        bool n2) {
+  if constexpr (NT == 0) {
+    return true;
+  } else if constexpr (NT == 1) {
+    return sw_term(p.t[0], c1f, c1i, n1, c2f, c2i, n2);
+  } else {
+    const bool a = sw_term(p.t[0], c1f, c1i, n1, c2f, c2i, n2);
+    const bool b = sw_term(p.t[1], c1f, c1i, n1, c2f, c2i, n2);
+    return p.combine ? (a || b) : (a && b);
+  }
+}
+// f2 in canonical form (SweepState::lower): every term is `e2.v OP B` with B a constant or e1.v,
+// so B is resolved once per candidate and a probe costs one compare per term.  CT is the type
+// the compares run in: 0 double (always exact, see SwTerm), 1 float (float column, constants
+// exactly representable), 2 int32 (int / string-id column, integral constants in range) —
+// chosen on the host where it gives the same answer as the promoted Java compare.
+template <int CT> struct SwTy { using T = double; };
+template <> struct SwTy<1> { using T = float; };
+template <> struct SwTy<2> { using T = int32_t; };
+
+template <int CT>
+struct SwCand {
+  typename SwTy<CT>::T b[2];
+  bool bn[2];
+};
+template <class T>
+__device__ __forceinline__ bool sw_cmp(int32_t mask, T A, T B) {
+  const bool lt = A < B, eq = A == B, gt = A > B;
+  const bool un = !(lt || eq || gt);
+  return (lt & ((mask & 1) != 0)) | (eq & ((mask & 2) != 0)) | (gt & ((mask & 4) != 0)) | (un & ((mask & 8) != 0));
+}
+template <int CT>
+__device__ __forceinline__ typename SwTy<CT>::T sw_val(uint32_t v, double f, double i, bool flt) {
+  if constexpr (CT == 1) return __uint_as_float(v);
+  else if constexpr (CT == 2) return (int32_t)v;
+  else return flt ? f : i;
+}
+template <int NT, int CT>
+__device__ __forceinline__ SwCand<CT> sw_cand(const SwPred& p, uint32_t av, double af, double ai, bool an) {
+  SwCand<CT> c{};
+#pragma unroll
+  for (int t = 0; t < NT; t++) {
+    const SwTerm& x = p.t[t];
+    c.b[t] = x.bk == 0 ? (typename SwTy<CT>::T)x.bc : sw_val<CT>(av, af, ai, x.flt);
+    c.bn[t] = x.bk == 1 && an;
+  }
+  return c;
+}
+template <int NT, int CT>
+__device__ __forceinline__ bool sw_close(const SwPred& p, const SwCand<CT>& c, uint32_t ev, double ef, double ei,
+                                         bool en) {
+  if constexpr (NT == 0) {
+    return true;
+  } else if constexpr (NT == 1) {
+    return !en & !c.bn[0] & sw_cmp(p.t[0].mask, sw_val<CT>(ev, ef, ei, p.t[0].flt), c.b[0]);
+  } else {
+    const bool a = !en & !c.bn[0] & sw_cmp(p.t[0].mask, sw_val<CT>(ev, ef, ei, p.t[0].flt), c.b[0]);
+    const bool b = !en & !c.bn[1] & sw_cmp(p.t[1].mask, sw_val<CT>(ev, ef, ei, p.t[1].flt), c.b[1]);
+    return p.combine ? (a | b) : (a & b);
+  }
+}
+
+// the column value as the two promoted doubles (float path / exact int path)
+__device__ __forceinline__ void sw_conv(uint32_t v, bool isfloat, double& f, double& i) {
+  if (isfloat) {
+    f = i = (double)__uint_as_float(v);
+  } else {
+    const int32_t x = (int32_t)v;
+    f = (double)(float)x;
+    i = (double)x;
+  }
+}
+
+__device__ __forceinline__ uint64_t sw_match_peers(uint32_t bin, int bits, bool valid) {
+  uint64_t peers = __ballot(valid);
+  for (int b = 0; b < bits; b++) {
+    bool bit = (bin >> b) & 1u;
+    uint64_t m = __ballot(bit);
+    peers &= bit ? m : ~m;
+  }
+  return peers;
+}
+
+__device__ __forceinline__ uint64_t sw_lanemask_lt() {
+  uint32_t lane = __lane_id();
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// exclusive block scan of one value per thread (SW_THREADS threads); wtot: SW_WAVES words of LDS
+__device__ __forceinline__ uint32_t sw_block_scan(uint32_t v, uint32_t* wtot, uint32_t& total) {
+  uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) wtot[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < SW_WAVES; i++) {
+    uint32_t t = wtot[i];
+    pre += (uint32_t)i < w ? t : 0u;
+    tot += t;
+  }
+  total = tot;
+  __syncthreads();
+  return pre + x - v;
+}
+
+// ------------------------------------------------------------------ pass 1: count
+__global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B, const int32_t* __restrict__ key,
+                                                         int* err) {
+  __shared__ uint32_t h[SW_MAXOWN];
+  const int st = blockIdx.x;
+  for (int b = threadIdx.x; b < D.nown; b += SW_THREADS) h[b] = 0;
+  __syncthreads();
+  const int64_t lo = (int64_t)st * D.st_len, hi = min(B.n, lo + D.st_len);
+  int e = 0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += SW_THREADS) {
+    int s = B.stream ? B.stream[i] : 0;
+    if (s < 0) continue;
+    int32_t k = B.partitioned ? key[i] : 0;
+    if (k < 0 || k >= D.maxkeys) {
+      e |= SWE_KEYS;
+      continue;
+    }
+    if (s != D.fstream) continue;
+    atomicAdd(&h[D.kmap[k] & 0xffffu], 1u);
+  }
+  if (e) atomicOr(err, e);
+  __syncthreads();
+  for (int b = threadIdx.x; b < D.nown; b += SW_THREADS) D.cnt[(int64_t)b * D.nst + st] = h[b];
+  if (st == 0 && threadIdx.x == 0) D.cnt[(int64_t)D.nown * D.nst] = 0;
+}
+
+// ------------------------------------------------------------------ pass 2: stable scatter by owner
+__global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView B, const int32_t* __restrict__ key,
+                                                           int* err) {
+  __shared__ uint32_t wcnt[SW_WAVES][SW_MAXOWN];  // per-wave counts, then write cursors
+  __shared__ uint32_t grun[SW_MAXOWN];
+  const int st = blockIdx.x;
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  const uint64_t lt = sw_lanemask_lt();
+  for (int b = threadIdx.x; b < D.nown; b += SW_THREADS) grun[b] = D.off[(int64_t)b * D.nst + st];
+  const int64_t lo = (int64_t)st * D.st_len, hi = min(B.n, lo + D.st_len);
+  const int64_t base = B.n > 0 ? B.ts[0] : 0;
+  const uint32_t* vcol = (const uint32_t*)B.cols[0];
+  const uint8_t* ncol = B.nulls[0];
+  int e = 0;
+  int64_t tmax = INT64_MIN;
+  for (int64_t r0 = lo; r0 < hi; r0 += SWP_ROUND) {
+    for (int b = lane; b < D.nown; b += 64) wcnt[w][b] = 0;
+    __syncthreads();
+    SwRec rec[SWP_SUB];
+    uint32_t own[SWP_SUB];
+    uint32_t rk[SWP_SUB];
+#pragma unroll
+    for (int s = 0; s < SWP_SUB; s++) {
+      int64_t i = r0 + (int64_t)w * SWP_SEG + s * 64 + lane;
+      bool valid = i < hi;
+      uint32_t o = 0, lk = 0;
+      if (valid) {
+        int sid = B.stream ? B.stream[i] : 0;
+        int32_t k = B.partitioned ? key[i] : 0;
+        valid = sid == D.fstream && k >= 0 && k < D.maxkeys;
+        if (valid) {
+          uint32_t km = D.kmap[k];
+          o = km & 0xffffu;
+          lk = km >> 16;
+          int64_t t = B.ts[i];
+          tmax = max(tmax, t);
+          int64_t rel = t - base;
+          if (!sw_rel_ok(rel)) e |= SWE_RANGE;
+          bool nul = ncol && ncol[i];
+          rec[s].kt = sw_kt(lk, rel, nul ? SW_NULL : 0ull);
+          rec[s].ref = (uint32_t)i;
+          rec[s].v = vcol ? vcol[i] : 0u;
+        }
+      }
+      uint64_t peers = sw_match_peers(o, D.own_bits, valid);
+      uint32_t before = 0;
+      if (valid) before = wcnt[w][o];
+      rk[s] = before + (uint32_t)__popcll(peers & lt);
+      if (valid && (peers & lt) == 0) wcnt[w][o] = before + (uint32_t)__popcll(peers);
+      own[s] = valid ? o : 0xffffffffu;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < D.nown; b += SW_THREADS) {
+      uint32_t g = grun[b];
+#pragma unroll
+      for (int ww = 0; ww < SW_WAVES; ww++) {
+        uint32_t c = wcnt[ww][b];
+        wcnt[ww][b] = g;
+        g += c;
+      }
+      grun[b] = g;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < SWP_SUB; s++)
+      if (own[s] != 0xffffffffu) D.recs[wcnt[w][own[s]] + rk[s]] = rec[s];
+    __syncthreads();
+  }
+  if (e) atomicOr(err, e);
+  // running max of ts (the engine clock after the push)
+  for (int d = 32; d > 0; d >>= 1) tmax = max(tmax, (int64_t)__shfl_xor((long long)tmax, d, 64));
+  if (lane == 0 && tmax != INT64_MIN) atomicMax((long long*)D.tsmax, (long long)tmax);
+}
+
+// ------------------------------------------------------------------ pass 3: per-owner sweep
+// One 512-thread workgroup per owner walks the owner's region (arrival order) in chunks of
+// SWS_CHUNK records.  Per chunk, all in LDS:
+//   rank     records (prefetched into registers during the previous chunk) are ranked by local
+//            key with wave ballots; carried open candidates are already in key order
+//   place    sorted position p -> (ts relative to the chunk base, value), key|flags, ref
+//   probe    every candidate tests the next SW_PROBE events of its key unconditionally
+//            (straight-line code); a loop finishes the rare longer scans
+//   emit     each closing event finds its candidates (backward probe of m), a block scan gives
+//            the output offsets, (e1 seq, e2 seq) pairs are written in (key, j, i) order
+//   carry    still-open candidates (key order) become the next chunk's carry
+#define SWM(p) S.m_[8 + (p)]
+constexpr int SWS_THREADS = 512;
+constexpr int SWS_WAVES = SWS_THREADS / 64;
+constexpr int SWS_RPT = SWS_CHUNK / SWS_THREADS;  // records per thread
+constexpr int SWS_PER = (SWS_EMAX + SWS_THREADS - 1) / SWS_THREADS;
+constexpr uint32_t SW_LKF_CAR = 1u << 8, SW_LKF_NULL = 1u << 9, SW_LKF_NONE = 0xFFu;
+constexpr int32_t SW_TS_FLOOR = -(1 << 30) - 1;  // carried ts below this are clamped (all expired)
+constexpr int64_t SW_TS_SPAN = 1ll << 29;        // |event ts - chunk base| bound
+
+struct SwSolveSmem {
+  int2 tv[SWS_EMAX + SW_PROBE];       // (ts - chunk base, value) by sorted position, then sentinels
+  uint16_t lkf[SWS_EMAX + SW_PROBE];  // local key | carried | null
+  uint32_t ref[SWS_EMAX];             // batch index, or carry slot (carried)
+  uint32_t cnt2[SWS_EMAX / 2 + 1];    // closes per position, two 16-bit counters per word
+  int16_t m_[8 + SWS_EMAX + 8];       // m(p) = m_[8 + p]: >=0 closing position, -1 expired, -2 open,
+                                      // -3 not a candidate (8 guard entries each side)
+  uint16_t wc[SWS_WAVES][SW_LK + 1];  // per-wave record counts per key, then write cursors
+  uint32_t binoff[SW_LK + 2];
+  uint32_t ncar[SW_LK + 1];           // carried candidates per key
+  uint16_t cstart[SW_LK + 1], fe[SW_LK + 1];  // carry index / sorted position of a key's first event
+  uint64_t ckt[2][SWS_CCAP];          // carry: key | null | ts50 (batch-relative)
+  uint32_t cv[2][SWS_CCAP];
+  int64_t cseq[2][SWS_CCAP];
+  int64_t lastts[SW_LK];              // batch-relative ts of the key's latest event (INT64_MIN unseen)
+  uint32_t wtot[SWS_WAVES];
+  unsigned long long gbase;
+};
+
+template <int NW>
+__device__ __forceinline__ uint32_t sw_block_scan_n(uint32_t v, uint32_t* wtot, uint32_t& total) {
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) wtot[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; i++) {
+    const uint32_t t = wtot[i];
+    pre += (uint32_t)i < w ? t : 0u;
+    tot += t;
+  }
+  total = tot;
+  __syncthreads();
+  return pre + x - v;
+}
+
+template <int NT1, int NT2, int CT>
+__global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView B, MatchOut O, int* err) {
+  __shared__ SwSolveSmem S;
+  const int o = blockIdx.x;
+  const uint32_t tid0 = threadIdx.x;
+  const uint32_t tid = tid0, lane = __lane_id(), w = tid >> 6;
+  const uint64_t lt = sw_lanemask_lt();
+  const int64_t rb = D.off[(int64_t)o * D.nst], re = D.off[(int64_t)(o + 1) * D.nst];
+  if (rb == re) return;  // no events for this owner: carry and last ts unchanged
+  const int64_t base = B.ts[0];
+  const int32_t W = (int32_t)D.within;  // < 2^29 (SweepState::shape_ok)
+  const SwPred f1 = D.f1, f2 = D.f2;
+  const bool vnull = D.vtag == T_NULL;
+  const bool vflt = D.vtag == T_FLOAT;
+  const int lkbits = D.lk_bits;
+  int e = 0;
+  // carry and last ts from the previous push
+  int nc = D.c_n[o];
+  for (int i = tid; i <= SW_LK; i += SWS_THREADS) S.ncar[i] = 0;
+  if (tid < 8) S.m_[tid] = -3;
+  __syncthreads();
+  for (int i = tid; i < nc; i += SWS_THREADS) {
+    const int64_t c = (int64_t)o * SWS_CCAP + i;
+    const int64_t rel = D.c_ts[c] - base;
+    if (!sw_rel_ok(rel)) e |= SWE_RANGE;
+    S.ckt[0][i] = sw_kt(D.c_lk[c], rel, D.c_null[c] ? SW_NULL : 0ull);
+    S.cv[0][i] = D.c_v[c];
+    S.cseq[0][i] = D.c_seq[c];
+    atomicAdd(&S.ncar[D.c_lk[c]], 1u);
+  }
+  for (int i = tid; i < SW_LK; i += SWS_THREADS) {
+    const int64_t t = D.lastts[(int64_t)o * SW_LK + i];
+    S.lastts[i] = t == INT64_MIN ? INT64_MIN : t - base;
+  }
+  int cur = 0;
+  // prefetch chunk 0: record j of a chunk = w * (64 * SWS_RPT) + s * 64 + lane
+  SwRec pf[SWS_RPT];
+#pragma unroll
+  for (int s = 0; s < SWS_RPT; s++) {
+    const int64_t j = rb + (int64_t)w * (64 * SWS_RPT) + s * 64 + lane;
+    if (j < re) pf[s] = D.recs[j];
+  }
+  uint64_t tbk = D.recs[rb].kt;
+  __syncthreads();
+#ifdef SHP_SW_STAMPS
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_prev = clock64();
+  unsigned long long dbg_steps = 0, dbg_cands = 0, dbg_chunks = 0, dbg_nc = 0;
+  __shared__ unsigned long long dbg_sum[2];
+  if (tid == 0) dbg_sum[0] = dbg_sum[1] = 0;
+#endif
+  for (int64_t cb = rb; cb < re; cb += SWS_CHUNK) {
+    uint32_t tid_o = tid0;
+    asm volatile("" : "+v"(tid_o));  // keep per-thread LDS addresses out of loop-invariant registers
+    const uint32_t tid = tid_o, lane = tid_o & 63u, w = __builtin_amdgcn_readfirstlane(tid_o >> 6);
+    const int nchunk = (int)min((int64_t)SWS_CHUNK, re - cb);
+    const int E = nc + nchunk;
+    const int64_t tb = sw_ts(tbk);  // chunk base: batch-relative ts of the chunk's first record
+#ifdef SHP_SW_STAMPS
+    dbg_chunks++;
+    dbg_nc += nc;
+#endif
+    // 1. rank the chunk's records by local key (stable: wave-major, then sub-round, then lane)
+    for (int b = lane; b <= SW_LK; b += 64) S.wc[w][b] = 0;
+    __syncthreads();
+    uint32_t rk[SWS_RPT], bin[SWS_RPT];
+    const uint32_t nonebin = lkbits >= 8 ? SW_LKF_NONE : (1u << lkbits);
+    const int rbits = lkbits >= 8 ? 8 : lkbits + 1;
+#pragma unroll
+    for (int s = 0; s < SWS_RPT; s++) {
+      const int j = (int)w * (64 * SWS_RPT) + s * 64 + (int)lane;
+      const uint32_t bn = j < nchunk ? sw_lk(pf[s].kt) : nonebin;
+      bin[s] = bn;
+      const uint64_t peers = sw_match_peers(bn, rbits, true);
+      const uint32_t before = S.wc[w][bn];
+      rk[s] = before + (uint32_t)__popcll(peers & lt);
+      if ((peers & lt) == 0) S.wc[w][bn] = (uint16_t)(before + (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    {  // key offsets (carried first within each key), per-wave write cursors
+      const uint32_t b = tid;
+      uint32_t c[SWS_WAVES], t = 0, nk = 0;
+      if (b <= (uint32_t)SW_LK && b != nonebin) {
+        nk = S.ncar[b];
+#pragma unroll
+        for (int ww = 0; ww < SWS_WAVES; ww++) {
+          c[ww] = S.wc[ww][b];
+          t += c[ww];
+        }
+      }
+      uint32_t total;
+      const uint32_t pre = sw_block_scan_n<SWS_WAVES>(((t + nk) << 16) | nk, S.wtot, total);
+      if (b <= (uint32_t)SW_LK && b != nonebin) {
+        uint32_t g = (pre >> 16) + nk;
+        S.binoff[b] = pre >> 16;
+        S.cstart[b] = (uint16_t)(pre & 0xffffu);
+        S.fe[b] = (uint16_t)((pre >> 16) + nk);
+#pragma unroll
+        for (int ww = 0; ww < SWS_WAVES; ww++) {
+          S.wc[ww][b] = (uint16_t)g;
+          g += c[ww];
+        }
+      }
+      if (b <= (uint32_t)SW_LK && b == nonebin) {
+        S.binoff[b] = pre >> 16;
+        S.cstart[b] = (uint16_t)(pre & 0xffffu);
+        S.fe[b] = (uint16_t)(pre >> 16);
+      }
+      if (tid == 0) S.binoff[SW_LK + 1] = total >> 16;
+    }
+    __syncthreads();
+    // 2. place records and carried candidates by sorted position
+#pragma unroll
+    for (int s = 0; s < SWS_RPT; s++) {
+      if (bin[s] == nonebin) continue;
+      const uint32_t p = S.wc[w][bin[s]] + rk[s];
+      const int64_t rel = sw_ts(pf[s].kt) - tb;
+      if (rel >= SW_TS_SPAN || rel <= -SW_TS_SPAN) e |= SWE_RANGE;
+      S.tv[p] = make_int2((int32_t)rel, (int32_t)pf[s].v);
+      S.lkf[p] = (uint16_t)(bin[s] | ((pf[s].kt & SW_NULL) ? SW_LKF_NULL : 0u));
+      S.ref[p] = pf[s].ref;
+    }
+    for (int x = tid; x < nc; x += SWS_THREADS) {
+      const uint64_t kt = S.ckt[cur][x];
+      const uint32_t lk = sw_lk(kt);
+      const uint32_t p = S.binoff[lk] + (uint32_t)x - S.cstart[lk];
+      const int64_t rel = sw_ts(kt) - tb;
+      const int64_t crel = rel < SW_TS_FLOOR ? SW_TS_FLOOR : (rel > (1ll << 30) ? (1ll << 30) : rel);
+      S.tv[p] = make_int2((int32_t)crel, (int32_t)S.cv[cur][x]);
+      S.lkf[p] = (uint16_t)(lk | SW_LKF_CAR | ((kt & SW_NULL) ? SW_LKF_NULL : 0u));
+      S.ref[p] = (uint32_t)x;
+    }
+    if (tid < SW_PROBE) {
+      S.tv[E + tid] = make_int2(0, 0);
+      S.lkf[E + tid] = (uint16_t)SW_LKF_NONE;
+    }
+    for (int i = tid; i <= SWS_EMAX / 2; i += SWS_THREADS) S.cnt2[i] = 0;
+    // prefetch the next chunk while this one is solved
+    {
+      const int64_t nb = cb + SWS_CHUNK;
+#pragma unroll
+      for (int s = 0; s < SWS_RPT; s++) {
+        const int64_t j = nb + (int64_t)w * (64 * SWS_RPT) + s * 64 + lane;
+        if (j < re) pf[s] = D.recs[j];
+      }
+      if (nb < re) tbk = D.recs[nb].kt;
+    }
+    __syncthreads();
+    SW_STAMP(0);
+    // 3. probe: every candidate looks for its closing event among the next events of its key
+    for (int k = 0; k < SWS_PER; k++) {
+      const int p = (int)tid + k * SWS_THREADS;
+      if (p >= E) break;
+      const uint32_t f = S.lkf[p];
+      const int2 a = S.tv[p];
+      const bool car = (f & SW_LKF_CAR) != 0;
+      const bool an = vnull || (f & SW_LKF_NULL) != 0;
+      double af = 0, ai = 0;
+      sw_conv((uint32_t)a.y, vflt, af, ai);
+      const bool cand = car || sw_pred<NT1>(f1, af, ai, an, 0.0, 0.0, true);
+      const uint32_t lk = f & 0xFFu;
+      const int end = (int)S.binoff[lk + 1];
+      const int q0 = max(p + 1, (int)S.fe[lk]);  // carried candidates are not events
+      const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
+      int res = cand ? -4 : -3;  // -4: unresolved
+      int2 b[SW_PROBE];
+      uint32_t bf[SW_PROBE];
+#pragma unroll
+      for (int d = 0; d < SW_PROBE; d++) {
+        b[d] = S.tv[q0 + d];
+        bf[d] = S.lkf[q0 + d];
+      }
+#pragma unroll
+      for (int d = 0; d < SW_PROBE; d++) {
+        double ef = 0, ei = 0;
+        if constexpr (CT == 0) sw_conv((uint32_t)b[d].y, vflt, ef, ei);
+        const bool inrun = q0 + d < end;
+        const bool expired = b[d].x - a.x > W;
+        const bool hit = sw_close<NT2, CT>(f2, cbv, (uint32_t)b[d].y, ef, ei, vnull || (bf[d] & SW_LKF_NULL) != 0);
+        const int r = !inrun ? -2 : (expired ? -1 : (hit ? q0 + d : -4));
+        res = res == -4 ? r : res;
+      }
+#ifdef SHP_SW_STAMPS
+      if (cand) dbg_cands++;
+#endif
+      if (res == -4) {
+        res = -2;
+        for (int q = q0 + SW_PROBE; q < end; q++) {
+#ifdef SHP_SW_STAMPS
+          dbg_steps++;
+#endif
+          const int2 c = S.tv[q];
+          if (c.x - a.x > W) {
+            res = -1;
+            break;
+          }
+          double cf = 0, ci = 0;
+          if constexpr (CT == 0) sw_conv((uint32_t)c.y, vflt, cf, ci);
+          if (sw_close<NT2, CT>(f2, cbv, (uint32_t)c.y, cf, ci, vnull || (S.lkf[q] & SW_LKF_NULL) != 0)) {
+            res = q;
+            break;
+          }
+        }
+      }
+      SWM(p) = (int16_t)res;
+      if (res >= 0) atomicAdd(&S.cnt2[res >> 1], 1u << ((res & 1) * 16));
+    }
+    if (tid < 8) SWM(E + tid) = -3;
+    __syncthreads();
+    SW_STAMP(1);
+    // 4. closes per event (counted by the probe), output offsets, then the pairs: each closing
+    //    event collects its candidates backwards (they sit within the window before it)
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < SWS_PER; k++) {
+      const int q = (int)tid * SWS_PER + k;
+      tot += q < E ? (S.cnt2[q >> 1] >> ((q & 1) * 16)) & 0xffffu : 0u;
+    }
+    for (int i = tid; i <= SW_LK; i += SWS_THREADS) S.ncar[i] = 0;  // recounted by the carry step
+    uint32_t total;
+    uint32_t off = sw_block_scan_n<SWS_WAVES>(tot, S.wtot, total);
+    if (tid == 0) {
+      const unsigned long long g = total ? atomicAdd(O.count, (unsigned long long)total) : 0ull;
+      if (g + total > (unsigned long long)O.cap) e |= E_OUT;
+      S.gbase = g;
+    }
+    __syncthreads();
+    SW_STAMP(2);
+    {
+      const unsigned long long gb = S.gbase;
+      for (int k = 0; k < SWS_PER; k++) {
+        const int q = (int)tid * SWS_PER + k;
+        const uint32_t c = q < E ? (S.cnt2[q >> 1] >> ((q & 1) * 16)) & 0xffffu : 0u;
+        if (c) {
+          const uint64_t dst = gb + off;
+          const int64_t sq = B.seq0 + S.ref[q];
+          int16_t mm[SW_PROBE];
+#pragma unroll
+          for (int d = 0; d < SW_PROBE; d++) mm[d] = SWM(q - 1 - d);  // guards below position 0
+          uint32_t found = 0;
+#pragma unroll
+          for (int d = 0; d < SW_PROBE; d++) {
+            if (mm[d] == q) {
+              const int p = q - 1 - d;
+              const uint32_t r = S.ref[p];
+              const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
+              const uint64_t slot = dst + (c - 1 - found);
+              if (slot < (uint64_t)O.cap) {
+                longlong2 pr;
+                pr.x = si;
+                pr.y = sq;
+                *(longlong2*)(O.refs + 2 * slot) = pr;
+              }
+              found++;
+            }
+          }
+          for (int p = q - 1 - SW_PROBE; p >= 0 && found < c; p--) {
+            if (SWM(p) != q) continue;
+            const uint32_t r = S.ref[p];
+            const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
+            const uint64_t slot = dst + (c - 1 - found);
+            if (slot < (uint64_t)O.cap) {
+              longlong2 pr;
+              pr.x = si;
+              pr.y = sq;
+              *(longlong2*)(O.refs + 2 * slot) = pr;
+            }
+            found++;
+          }
+        }
+        off += c;
+      }
+    }
+    SW_STAMP(3);
+    // 5. per-key timestamp order (first event against the key's last ts, the rest against their
+    //    predecessor) and the key's latest ts
+    for (int k = 0; k < SWS_PER; k++) {
+      const int p = (int)tid + k * SWS_THREADS;
+      if (p >= E) break;
+      const uint32_t f = S.lkf[p];
+      if (f & SW_LKF_CAR) continue;
+      const uint32_t lk = f & 0xFFu;
+      const int32_t t = S.tv[p].x;
+      if (p > (int)S.fe[lk]) {
+        if (t < S.tv[p - 1].x) e |= SWE_MONO;
+      } else {
+        const int64_t prev = S.lastts[lk];
+        if (prev != INT64_MIN && tb + t < prev) e |= SWE_MONO;
+      }
+    }
+    __syncthreads();
+    for (int k = 0; k < SWS_PER; k++) {
+      const int p = (int)tid + k * SWS_THREADS;
+      if (p >= E) break;
+      const uint32_t f = S.lkf[p];
+      const uint32_t lk = f & 0xFFu;
+      if (!(f & SW_LKF_CAR) && p + 1 == (int)S.binoff[lk + 1]) S.lastts[lk] = tb + S.tv[p].x;
+    }
+    SW_STAMP(4);
+    // 6. still-open candidates become the carry (sorted order = key, then i)
+    {
+      uint32_t open = 0;
+#pragma unroll
+      for (int k = 0; k < SWS_PER; k++) {
+        const int p = (int)tid * SWS_PER + k;
+        open += (p < E && SWM(p) == -2) ? 1u : 0u;
+      }
+      uint32_t ntot;
+      uint32_t pre = sw_block_scan_n<SWS_WAVES>(open, S.wtot, ntot);
+      const int nx = cur ^ 1;
+#pragma unroll
+      for (int k = 0; k < SWS_PER; k++) {
+        const int p = (int)tid * SWS_PER + k;
+        if (p < E && SWM(p) == -2) {
+          if (pre < (uint32_t)SWS_CCAP) {
+            const uint32_t f = S.lkf[p];
+            const uint32_t r = S.ref[p];
+            const uint32_t lk = f & 0xFFu;
+            if (f & SW_LKF_CAR) {
+              S.ckt[nx][pre] = S.ckt[cur][r];
+              S.cv[nx][pre] = S.cv[cur][r];
+              S.cseq[nx][pre] = S.cseq[cur][r];
+            } else {
+              S.ckt[nx][pre] = sw_kt(lk, tb + S.tv[p].x, (f & SW_LKF_NULL) ? SW_NULL : 0ull);
+              S.cv[nx][pre] = (uint32_t)S.tv[p].y;
+              S.cseq[nx][pre] = B.seq0 + r;
+            }
+            atomicAdd(&S.ncar[lk], 1u);
+          }
+          pre++;
+        }
+      }
+      if (ntot > (uint32_t)SWS_CCAP) {
+        e |= E_LIST;
+        ntot = SWS_CCAP;
+      }
+      nc = (int)ntot;
+      cur = nx;
+    }
+    __syncthreads();
+    SW_STAMP(5);
+    SW_STAMP(6);
+    SW_STAMP(7);
+  }
+#ifdef SHP_SW_STAMPS
+  atomicAdd(&dbg_sum[0], dbg_steps);
+  atomicAdd(&dbg_sum[1], dbg_cands);
+  __syncthreads();
+  if (tid == 0 && D.stamps) {
+    for (int k = 0; k < 6; k++) D.stamps[(int64_t)o * 8 + k] = st_acc[k];
+    D.stamps[(int64_t)o * 8 + 7] = (dbg_sum[0] << 24) | (dbg_sum[1] & 0xffffff);
+    D.stamps[(int64_t)o * 8 + 6] = (dbg_chunks << 40) | (dbg_nc & 0xffffffffffull);
+  }
+#endif
+  // write back carry and last ts
+  for (int i = tid; i < nc; i += SWS_THREADS) {
+    const int64_t c = (int64_t)o * SWS_CCAP + i;
+    const uint64_t kt = S.ckt[cur][i];
+    D.c_ts[c] = base + sw_ts(kt);
+    D.c_seq[c] = S.cseq[cur][i];
+    D.c_v[c] = S.cv[cur][i];
+    D.c_lk[c] = (uint8_t)sw_lk(kt);
+    D.c_null[c] = (kt & SW_NULL) ? 1 : 0;
+  }
+  for (int i = tid; i < SW_LK; i += SWS_THREADS) {
+    const int64_t t = S.lastts[i];
+    D.lastts[(int64_t)o * SW_LK + i] = t == INT64_MIN ? INT64_MIN : base + t;
+  }
+  if (tid == 0) D.c_n[o] = nc;
+  if (e) atomicOr(err, e);
+}
+
+// full match records from the (i, j) pairs (shp_push_batch / shp_fetch_matches)
+__global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchOut O) {
+  const int64_t m = min((int64_t)*O.count, O.cap);
+  if (blockIdx.x == 0 && threadIdx.x == 0) O.count[1] = 2ull * (unsigned long long)m;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t j = O.refs[2 * i + 1];
+    int64_t g = j - B.seq0;
+    O.key[i] = B.partitioned ? key[g] : 0;
+    O.ts[i] = B.ts[g];
+    O.type[i] = 0;
+    O.pos[i] = j;
+    O.ref_off[i] = 2 * i;
+    O.slot_len[i * MAXS] = 1;
+    O.slot_len[i * MAXS + 1] = 1;
+  }
+}
+
+__global__ void k_sw_init(SweepDev D) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < D.nown) D.c_n[i] = 0;
+  if (i < (int64_t)D.nown * SW_LK) D.lastts[i] = INT64_MIN;
+  if (i == 0) *D.tsmax = INT64_MIN;
+}
+
+}  // namespace shp
+
+// ------------------------------------------------------------------ host side
+namespace shp {
+
+struct SweepState {
+  SweepDev D{};
+  int ct = 0;  // compare type of the probe loop (see SwCand)
+  int64_t st_len = 65536;
+  int32_t nst_max = 1;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+
+  static uint32_t hash32(uint32_t x) {  // murmur3 finaliser
+    x ^= x >> 16;
+    x *= 0x85ebca6bu;
+    x ^= x >> 13;
+    x *= 0xc2b2ae35u;
+    x ^= x >> 16;
+    return x;
+  }
+
+  // Is the program a sweep shape? One 4-byte predicate column (int / float / string id) or none,
+  // filters over slot 0/1 attributes of that column only, lowerable to SwPred.
+  static bool shape_ok(const DevProg& P, const FastShape& f) {
+    if (!f.ok || P.ncol > 1) return false;
+    if (P.ncol == 1 && !(P.colTag[0] == T_INT || P.colTag[0] == T_FLOAT || P.colTag[0] == T_STR)) return false;
+    SwPred a, b;
+    int8_t vt = P.ncol == 1 ? P.colTag[0] : T_NULL;
+    return lower(f.f1, vt, a) && lower(f.f2, vt, b) && canonical_e2(b);
+  }
+
+  static bool lower_operand(const FOperand& o, int8_t ptype, int8_t vtag, int8_t& kind, double& c) {
+    kind = 0;
+    c = 0;
+    if (o.kind == 1) {
+      if (o.pos != 0 || vtag == T_NULL) return false;
+      kind = (int8_t)(o.state + 1);
+      return o.state == 0 || o.state == 1;
+    }
+    switch (o.tag) {
+      case T_INT: {
+        int32_t x = (int32_t)o.imm;
+        c = ptype == T_FLOAT ? (double)(float)x : (double)x;
+        return true;
+      }
+      case T_LONG: {
+        // exact against 32-bit column values whatever the rounding, unless equal-compared
+        // beyond 2^53 (left to the scan path)
+        if (o.imm > (1ll << 53) || o.imm < -(1ll << 53)) return false;
+        c = ptype == T_FLOAT ? (double)(float)o.imm : (double)o.imm;
+        return true;
+      }
+      case T_FLOAT: {
+        uint32_t u = (uint32_t)o.imm;
+        float f;
+        memcpy(&f, &u, 4);
+        c = (double)f;
+        return true;
+      }
+      case T_DOUBLE: memcpy(&c, &o.imm, 8); return true;
+      case T_STR: c = (double)(int32_t)o.imm; return true;
+      default: return false;
+    }
+  }
+
+  // narrowest compare type that is exact for every term of the canonical f2 (see SwCand)
+  static int compare_type(const SwPred& p, int8_t vtag) {
+    bool f = vtag == T_FLOAT, i = vtag == T_INT || vtag == T_STR;
+    for (int k = 0; k < p.n; k++) {
+      const SwTerm& t = p.t[k];
+      if (t.bk == 0) {
+        double c = t.bc;
+        if (f && !(c != c) && (double)(float)c != c) f = false;
+        if (i && !(c == (double)(int32_t)c && c >= -2147483648.0 && c <= 2147483647.0)) i = false;
+      }
+      if (t.flt) i = false;
+    }
+    return f ? 1 : (i ? 2 : 0);
+  }
+
+  // rewrite every term of f2 as `e2.v OP B` (B const or e1.v), mirroring the operator on a swap
+  static bool canonical_e2(SwPred& p) {
+    for (int i = 0; i < p.n; i++) {
+      SwTerm& t = p.t[i];
+      if (t.ak != 2 && t.bk == 2) {
+        std::swap(t.ak, t.bk);
+        std::swap(t.ac, t.bc);
+        t.mask = (t.mask & 0xA) | ((t.mask & 1) << 2) | ((t.mask & 4) >> 2);  // lt <-> gt
+      }
+      if (t.ak != 2 || t.bk == 2) return false;
+    }
+    return true;
+  }
+
+  static bool lower(const FPred& p, int8_t vtag, SwPred& out) {
+    out = SwPred{};
+    out.n = p.n;
+    out.combine = p.combine;
+    for (int i = 0; i < p.n; i++) {
+      const FTerm& t = p.t[i];
+      SwTerm& o = out.t[i];
+      if (t.ptype == T_BOOL || t.ptype == T_NULL) return false;
+      if (t.a.kind == 0 && t.b.kind == 0) return false;
+      static const int32_t masks[6] = {4, 6, 1, 3, 2, 13};  // gt ge lt le eq ne
+      // string ids (java_cmp's default branch): == for eq, != for every other operator
+      o.mask = t.ptype == T_STR ? (t.cmp == 4 ? 2 : 13) : masks[t.cmp < 6 ? t.cmp : 5];
+      o.flt = vtag == T_INT && t.ptype == T_FLOAT;
+      if (!lower_operand(t.a, t.ptype, vtag, o.ak, o.ac) || !lower_operand(t.b, t.ptype, vtag, o.bk, o.bc))
+        return false;
+    }
+    return true;
+  }
+
+  // host key map: key -> owner | local key << 16; false when keys cannot be spread under the caps
+  static bool build_map(int32_t max_keys, int32_t& nown, std::vector<uint32_t>& kmap) {
+    nown = 1;
+    while (nown < SW_MAXOWN && (int64_t)nown * 10 < max_keys) nown *= 2;
+    for (;;) {
+      std::vector<int32_t> nloc(nown, 0);
+      kmap.assign(max_keys, 0);
+      int32_t mx = 0;
+      int bits = 0;
+      while ((1 << bits) < nown) bits++;
+      for (int32_t k = 0; k < max_keys; k++) {
+        // Fibonacci hashing: consecutive ids, and any arithmetic progression of ids (the keys
+        // one rank of a key-sharded job sees), spread evenly over the owners
+        uint32_t o = bits == 0 ? 0u : ((uint32_t)k * 2654435769u) >> (32 - bits);
+        int32_t lk = nloc[o]++;
+        mx = std::max(mx, lk + 1);
+        kmap[k] = o | ((uint32_t)lk << 16);
+      }
+      if (mx <= SW_LK) return true;
+      if (nown >= SW_MAXOWN) return false;
+      nown *= 2;
+    }
+  }
+
+  template <class T>
+  static void al(T*& p, int64_t n) {
+    if (hipMalloc((void**)&p, std::max<int64_t>(n, 1) * sizeof(T)) != hipSuccess)
+      throw std::runtime_error("hipMalloc failed (sweep path)");
+  }
+
+  void create(const DevProg& P, const FastShape& f, int32_t max_keys, int64_t cap, int32_t nown,
+              const std::vector<uint32_t>& kmap, hipStream_t s) {
+    D.vtag = P.ncol == 1 ? P.colTag[0] : T_NULL;
+    if (!lower(f.f1, (int8_t)D.vtag, D.f1) || !lower(f.f2, (int8_t)D.vtag, D.f2) || !canonical_e2(D.f2))
+      throw std::runtime_error("sweep: predicate not lowerable");
+    D.within = f.within;
+    D.fstream = f.stream;
+    ct = compare_type(D.f2, (int8_t)D.vtag);
+    D.nown = nown;
+    D.own_bits = 0;
+    while ((1 << D.own_bits) < nown) D.own_bits++;
+    D.maxkeys = max_keys;
+    {
+      uint32_t mx = 0;
+      for (uint32_t km : kmap) mx = std::max(mx, km >> 16);
+      D.lk_bits = 0;
+      while ((1u << D.lk_bits) <= mx) D.lk_bits++;
+    }
+    nst_max = (int32_t)std::max<int64_t>(1, (cap + st_len - 1) / st_len);
+    D.st_len = st_len;
+    uint32_t* km = nullptr;
+    al(km, max_keys);
+    if (hipMemcpy(km, kmap.data(), (size_t)max_keys * 4, hipMemcpyHostToDevice) != hipSuccess)
+      throw std::runtime_error("hipMemcpy failed (sweep key map)");
+    D.kmap = km;
+    int64_t nc = (int64_t)nown * nst_max + 1;
+    al(D.cnt, nc);
+    al(D.off, nc);
+    al(D.recs, cap);
+    al(D.c_n, nown);
+    al(D.c_ts, (int64_t)nown * SWS_CCAP);
+    al(D.c_seq, (int64_t)nown * SWS_CCAP);
+    al(D.c_v, (int64_t)nown * SWS_CCAP);
+    al(D.c_lk, (int64_t)nown * SWS_CCAP);
+    al(D.c_null, (int64_t)nown * SWS_CCAP);
+    al(D.lastts, (int64_t)nown * SW_LK);
+    al(D.tsmax, 1);
+    (void)rocprim::exclusive_scan(nullptr, tmp_bytes, D.cnt, D.off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s);
+    if (hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)) != hipSuccess)
+      throw std::runtime_error("hipMalloc failed (sweep scan scratch)");
+    int64_t ninit = std::max<int64_t>(nown, (int64_t)nown * SW_LK);
+    k_sw_init<<<(unsigned)((ninit + 255) / 256), 256, 0, s>>>(D);
+  }
+
+  void release() {
+    void* ps[] = {(void*)D.kmap, D.cnt, D.off, D.recs, D.c_n, D.c_ts, D.c_seq, D.c_v, D.c_lk, D.c_null,
+                  D.lastts, D.tsmax, tmp};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+    D = SweepDev{};
+    tmp = nullptr;
+  }
+
+  // the three passes over one batch; matches (i, j) go to O.refs in per-key emission order
+  void run(const BatchView& B, const int32_t* key, const MatchOut& O, int* err, hipStream_t s, KTimer& kt) {
+    if (B.n <= 0) return;
+    D.nst = (int32_t)((B.n + st_len - 1) / st_len);
+    size_t nc = (size_t)D.nown * D.nst + 1;
+    kt.mark("sw_count", s);
+    k_sw_count<<<D.nst, SW_THREADS, 0, s>>>(D, B, key, err);
+    kt.mark("sw_scan", s);
+    size_t tb = tmp_bytes;
+    (void)rocprim::exclusive_scan(tmp, tb, D.cnt, D.off, 0u, nc, rocprim::plus<uint32_t>(), s);
+    kt.mark("sw_scatter", s);
+    k_sw_scatter<<<D.nst, SW_THREADS, 0, s>>>(D, B, key, err);
+    kt.mark("sw_solve", s);
+    switch ((D.f1.n * 3 + D.f2.n) * 3 + ct) {
+#define SW_CASE(a, b, c) \
+  case (a * 3 + b) * 3 + c: k_sw_solve<a, b, c><<<D.nown, SWS_THREADS, 0, s>>>(D, B, O, err); break;
+#define SW_CASES(a, b) SW_CASE(a, b, 0) SW_CASE(a, b, 1) SW_CASE(a, b, 2)
+      SW_CASES(0, 0) SW_CASES(0, 1) SW_CASES(0, 2) SW_CASES(1, 0) SW_CASES(1, 1) SW_CASES(1, 2)
+      SW_CASES(2, 0) SW_CASES(2, 1) SW_CASES(2, 2)
+#undef SW_CASES
+#undef SW_CASE
+      default: break;
+    }
+    kt.mark(nullptr, s);
+  }
+
+  void expand(const BatchView& B, const int32_t* key, const MatchOut& O, hipStream_t s, KTimer& kt) {
+    kt.mark("sw_expand", s);
+    k_sw_expand<<<2048, 256, 0, s>>>(B, key, O);
+    kt.mark(nullptr, s);
+  }
+};
+
+}  // namespace shp

@@ -12,6 +12,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libsiddhi_hip.so")
+# diagnostics only (tools/sweep_probe.py): load the stamps build instead of the product library
+if os.environ.get("SIDDHI_HIP_DIAG_LIB"):
+    LIB_PATH = os.environ["SIDDHI_HIP_DIAG_LIB"]
 _lib = None
 
 SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACITY",
@@ -26,7 +29,10 @@ SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_
 class ShpConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("max_keys", ctypes.c_int32), ("max_batch", ctypes.c_int64),
                 ("max_matches", ctypes.c_int64), ("start_clock", ctypes.c_int64),
-                ("force_general", ctypes.c_int32), ("profile_kernels", ctypes.c_int32)]
+                ("force_general", ctypes.c_int32), ("profile_kernels", ctypes.c_int32),
+                ("match_layout", ctypes.c_int32)]
+
+LAYOUT_FULL, LAYOUT_PAIRS = 0, 1
 
 
 class ShpBatch(ctypes.Structure):
@@ -38,7 +44,7 @@ class ShpMatches(ctypes.Structure):
     _fields_ = [("m", ctypes.c_int64), ("num_states", ctypes.c_int32),
                 ("key", ctypes.c_void_p), ("ts", ctypes.c_void_p), ("type", ctypes.c_void_p),
                 ("pos", ctypes.c_void_p), ("ref_off", ctypes.c_void_p), ("slot_len", ctypes.c_void_p),
-                ("refs", ctypes.c_void_p)]
+                ("refs", ctypes.c_void_p), ("layout", ctypes.c_int32)]
 
 
 class ShpError(RuntimeError):
@@ -97,11 +103,12 @@ class HipEngine:
     """One engine per query (libsiddhi_hip.so). Same interface as the test oracle."""
 
     def __init__(self, program_json: str, start_clock: int = 0, max_keys: int = 1 << 16,
-                 max_batch: int = 1 << 20, max_matches: int = 0, device: int = 0, force_general: bool = False,
-                 profile_kernels: bool = False):
+                 max_batch: int = 1 << 20, max_matches: int = 0, device: int = 0, force_general: int = 0,
+                 profile_kernels: bool = False, match_layout: int = LAYOUT_FULL):
+        """force_general: 0 auto path, 1 general NFA lanes only, 2 no sweep path."""
         L = lib()
         cfg = ShpConfig(device, max_keys, max_batch, max_matches, int(start_clock), int(force_general),
-                        int(profile_kernels))
+                        int(profile_kernels), int(match_layout))
         h = ctypes.c_void_p()
         rc = L.shp_engine_create(program_json.encode(), ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:

@@ -31,12 +31,42 @@ def test_library_exports_every_declared_symbol():
     assert sorted(native.SYMBOLS) == declared_symbols()
 
 
-def test_config_struct_layout_matches_header():
-    # shp_config: int32 device, int32 max_keys, int64 max_batch, int64 max_matches, int64 start_clock,
-    # int32 force_general, int32 profile_kernels
-    assert ctypes.sizeof(native.ShpConfig) == 40
-    assert ctypes.sizeof(native.ShpBatch) == 48
-    assert ctypes.sizeof(native.ShpMatches) == 72
+def _c_layout():
+    """sizeof/offsetof of the ABI structs as the C compiler lays them out from the header."""
+    import subprocess
+    import tempfile
+    fields = {"shp_config": [f[0] for f in native.ShpConfig._fields_],
+              "shp_batch": [f[0] for f in native.ShpBatch._fields_],
+              "shp_matches": [f[0] for f in native.ShpMatches._fields_]}
+    body = []
+    for st, fs in fields.items():
+        body.append(f'printf("{st} %zu", sizeof({st}));')
+        for f in fs:
+            body.append(f'printf(" %zu", offsetof({st}, {f}));')
+        body.append('printf("\\n");')
+    src = ("#include <stdio.h>\n#include <stddef.h>\n#include \"siddhi_hip.h\"\nint main(void){"
+           + "".join(body) + "return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "l")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", exe, c])
+        out = subprocess.check_output([exe]).decode().split("\n")
+    res = {}
+    for line in out:
+        if line.strip():
+            parts = line.split()
+            res[parts[0]] = [int(x) for x in parts[1:]]
+    return res
+
+
+def test_struct_layouts_match_header():
+    lay = _c_layout()
+    for name, cls in (("shp_config", native.ShpConfig), ("shp_batch", native.ShpBatch),
+                      ("shp_matches", native.ShpMatches)):
+        size, *offs = lay[name]
+        assert ctypes.sizeof(cls) == size, name
+        assert [getattr(cls, f[0]).offset for f in cls._fields_] == offs, name
 
 
 def test_program_compiler_rejects_out_of_scope():

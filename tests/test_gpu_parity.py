@@ -61,15 +61,16 @@ CASES = [
 
 
 @pytest.mark.parametrize("name,q,n,keys", CASES, ids=[c[0] for c in CASES])
-@pytest.mark.parametrize("general", [True, False], ids=["general", "default"])
+@pytest.mark.parametrize("general", [1, 2, 0], ids=["general", "scan", "default"])
 @pytest.mark.parametrize("batch", [None, 9973], ids=["whole", "split"])
 def test_synthetic_matches_oracle(name, q, n, keys, general, batch):
     cq = program_for(q)
     g = small_stream(q, n, keys)
     a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
     eng = hip(general, max_keys=keys, max_batch=batch or n)(cq.program_json(), 0)
-    if q in (2, 5, 1) and not general:
-        assert eng.path == 1, "2-state every/within shape should select the specialised kernel"
+    if q in (2, 5, 1):
+        want = {1: 0, 2: 1, 0: 2}[general]
+        assert eng.path == want, "2-state every/within shape: sweep by default, scan kernel when asked"
     b = per_key(run(eng, cq, g, batch))
     msg = compare(a, b)
     assert msg is None, msg
@@ -82,10 +83,11 @@ def test_c2_10k_keys_fast_path_vs_oracle():
     cq = program_for(2)
     g = small_stream(2, 2_000_000, 10_000)
     a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
-    eng = hip(False, max_keys=10_000, max_batch=1 << 21)(cq.program_json(), 0)
-    assert eng.path == 1
-    b = per_key(run(eng, cq, g, 700_001))
-    assert compare(a, b) is None
+    for force, path in ((0, 2), (2, 1)):
+        eng = hip(force, max_keys=10_000, max_batch=1 << 21)(cq.program_json(), 0)
+        assert eng.path == path
+        b = per_key(run(eng, cq, g, 700_001))
+        assert compare(a, b) is None
     assert sum(len(v) for v in a.values()) > 100_000
 
 
@@ -130,7 +132,7 @@ def test_decreasing_ts_on_fast_path_fails_loudly():
     from siddhi_amd.native import HipEngine, ShpError
     cq = program_for(2)
     eng = HipEngine(cq.program_json(), 0, max_keys=4, max_batch=1024)
-    assert eng.path == 1
+    assert eng.path == 2
     g = small_stream(2, 200, 4)
     g["ts"] = g["ts"][::-1].copy()
     with pytest.raises(ShpError, match="SHP_ERR_UNSUPPORTED"):
