@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include <rocprim/rocprim.hpp>
+#include <cmath>
 #include <cstring>
 #include <utility>
 #include <stdexcept>
@@ -44,7 +45,7 @@ constexpr int SW_WAVES = SW_THREADS / 64;
 constexpr int SW_LK = 255;          // local keys per owner; bin 255 = "no item"
 constexpr int SW_MAXOWN = 2048;     // owners (partition bins)
 // partition
-constexpr int SWP_ROUND = 4096;
+constexpr int SWP_ROUND = 2048;
 constexpr int SWP_SEG = SWP_ROUND / SW_WAVES;
 constexpr int SWP_SUB = SWP_SEG / 64;
 // solve
@@ -118,6 +119,7 @@ struct SweepDev {
   int32_t fstream;
   int32_t nown, own_bits, nst, maxkeys;
   int32_t lk_bits;       // bits of the largest local key id
+  int32_t maybe_null;    // some pushed batch carried a null bitmap (sticky; the carry may hold nulls)
   int64_t st_len;
   const uint32_t* kmap;  // key -> owner | local key << 16
   uint32_t* cnt;         // nown * nst + 1: counts, scanned into off
@@ -218,6 +220,20 @@ __device__ __forceinline__ bool sw_close(const SwPred& p, const SwCand<CT>& c, u
   }
 }
 
+// f1 in canonical form: every term is `e1.v OP constant` (typed compares as for f2)
+template <int NT, int CT>
+__device__ __forceinline__ bool sw_open(const SwPred& p, uint32_t v, bool n) {
+  if constexpr (NT == 0) {
+    return true;
+  } else if constexpr (NT == 1) {
+    return !n & sw_cmp(p.t[0].mask, sw_val<CT>(v, 0.0, 0.0, false), (typename SwTy<CT>::T)p.t[0].bc);
+  } else {
+    const bool a = !n & sw_cmp(p.t[0].mask, sw_val<CT>(v, 0.0, 0.0, false), (typename SwTy<CT>::T)p.t[0].bc);
+    const bool b = !n & sw_cmp(p.t[1].mask, sw_val<CT>(v, 0.0, 0.0, false), (typename SwTy<CT>::T)p.t[1].bc);
+    return p.combine ? (a | b) : (a & b);
+  }
+}
+
 // the column value as the two promoted doubles (float path / exact int path)
 __device__ __forceinline__ void sw_conv(uint32_t v, bool isfloat, double& f, double& i) {
   if (isfloat) {
@@ -276,16 +292,33 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B
   __syncthreads();
   const int64_t lo = (int64_t)st * D.st_len, hi = min(B.n, lo + D.st_len);
   int e = 0;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += SW_THREADS) {
-    int s = B.stream ? B.stream[i] : 0;
-    if (s < 0) continue;
-    int32_t k = B.partitioned ? key[i] : 0;
-    if (k < 0 || k >= D.maxkeys) {
-      e |= SWE_KEYS;
-      continue;
+  constexpr int U = 8;  // loads of U events in flight per thread before the dependent key-map reads
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (int64_t)SW_THREADS * U) {
+    int32_t kk[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = i0 + (int64_t)u * SW_THREADS;
+      int32_t k = -1;
+      if (i < hi) {
+        const int s = B.stream ? B.stream[i] : 0;
+        if (s >= 0) {
+          k = B.partitioned ? key[i] : 0;
+          if (k < 0 || k >= D.maxkeys) {
+            e |= SWE_KEYS;
+            k = -1;
+          } else if (s != D.fstream) {
+            k = -1;
+          }
+        }
+      }
+      kk[u] = k;
     }
-    if (s != D.fstream) continue;
-    atomicAdd(&h[D.kmap[k] & 0xffffu], 1u);
+    uint32_t km[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) km[u] = kk[u] >= 0 ? D.kmap[kk[u]] : 0u;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (kk[u] >= 0) atomicAdd(&h[km[u] & 0xffffu], 1u);
   }
   if (e) atomicOr(err, e);
   __syncthreads();
@@ -314,28 +347,37 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
     SwRec rec[SWP_SUB];
     uint32_t own[SWP_SUB];
     uint32_t rk[SWP_SUB];
+    // all loads of the round first (independent, so they are in flight together), then the
+    // key-map lookups, then the ranking
+    int32_t kk[SWP_SUB];
 #pragma unroll
     for (int s = 0; s < SWP_SUB; s++) {
-      int64_t i = r0 + (int64_t)w * SWP_SEG + s * 64 + lane;
-      bool valid = i < hi;
-      uint32_t o = 0, lk = 0;
+      const int64_t i = r0 + (int64_t)w * SWP_SEG + s * 64 + lane;
+      int32_t k = -1;
+      if (i < hi) {
+        const int sid = B.stream ? B.stream[i] : 0;
+        k = B.partitioned ? key[i] : 0;
+        if (sid != D.fstream || k >= D.maxkeys) k = -1;
+        rec[s].ref = (uint32_t)i;
+        rec[s].kt = (uint64_t)B.ts[i];
+        rec[s].v = vcol ? vcol[i] : 0u;
+        if (k >= 0 && ncol && ncol[i]) k |= 0x40000000;  // null flag rides in the key for now
+      }
+      kk[s] = k;
+    }
+    uint32_t km[SWP_SUB];
+#pragma unroll
+    for (int s = 0; s < SWP_SUB; s++) km[s] = kk[s] >= 0 ? D.kmap[kk[s] & 0x3fffffff] : 0u;
+#pragma unroll
+    for (int s = 0; s < SWP_SUB; s++) {
+      const bool valid = kk[s] >= 0;
+      const uint32_t o = valid ? km[s] & 0xffffu : 0u;
       if (valid) {
-        int sid = B.stream ? B.stream[i] : 0;
-        int32_t k = B.partitioned ? key[i] : 0;
-        valid = sid == D.fstream && k >= 0 && k < D.maxkeys;
-        if (valid) {
-          uint32_t km = D.kmap[k];
-          o = km & 0xffffu;
-          lk = km >> 16;
-          int64_t t = B.ts[i];
-          tmax = max(tmax, t);
-          int64_t rel = t - base;
-          if (!sw_rel_ok(rel)) e |= SWE_RANGE;
-          bool nul = ncol && ncol[i];
-          rec[s].kt = sw_kt(lk, rel, nul ? SW_NULL : 0ull);
-          rec[s].ref = (uint32_t)i;
-          rec[s].v = vcol ? vcol[i] : 0u;
-        }
+        const int64_t t = (int64_t)rec[s].kt;
+        tmax = max(tmax, t);
+        const int64_t rel = t - base;
+        if (!sw_rel_ok(rel)) e |= SWE_RANGE;
+        rec[s].kt = sw_kt(km[s] >> 16, rel, (kk[s] & 0x40000000) ? SW_NULL : 0ull);
       }
       uint64_t peers = sw_match_peers(o, D.own_bits, valid);
       uint32_t before = 0;
@@ -443,6 +485,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
   const SwPred f1 = D.f1, f2 = D.f2;
   const bool vnull = D.vtag == T_NULL;
   const bool vflt = D.vtag == T_FLOAT;
+  const bool maybe_null = D.maybe_null != 0;
   const int lkbits = D.lk_bits;
   int e = 0;
   // carry and last ts from the previous push
@@ -587,8 +630,13 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       const bool car = (f & SW_LKF_CAR) != 0;
       const bool an = vnull || (f & SW_LKF_NULL) != 0;
       double af = 0, ai = 0;
-      sw_conv((uint32_t)a.y, vflt, af, ai);
-      const bool cand = car || sw_pred<NT1>(f1, af, ai, an, 0.0, 0.0, true);
+      bool cand;
+      if constexpr (CT == 0) {
+        sw_conv((uint32_t)a.y, vflt, af, ai);
+        cand = car || sw_pred<NT1>(f1, af, ai, an, 0.0, 0.0, true);
+      } else {
+        cand = car || sw_open<NT1, CT>(f1, (uint32_t)a.y, an);
+      }
       const uint32_t lk = f & 0xFFu;
       const int end = (int)S.binoff[lk + 1];
       const int q0 = max(p + 1, (int)S.fe[lk]);  // carried candidates are not events
@@ -599,7 +647,11 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
 #pragma unroll
       for (int d = 0; d < SW_PROBE; d++) {
         b[d] = S.tv[q0 + d];
-        bf[d] = S.lkf[q0 + d];
+        bf[d] = 0;
+      }
+      if (maybe_null) {
+#pragma unroll
+        for (int d = 0; d < SW_PROBE; d++) bf[d] = S.lkf[q0 + d];
       }
 #pragma unroll
       for (int d = 0; d < SW_PROBE; d++) {
@@ -627,7 +679,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
           }
           double cf = 0, ci = 0;
           if constexpr (CT == 0) sw_conv((uint32_t)c.y, vflt, cf, ci);
-          if (sw_close<NT2, CT>(f2, cbv, (uint32_t)c.y, cf, ci, vnull || (S.lkf[q] & SW_LKF_NULL) != 0)) {
+          if (sw_close<NT2, CT>(f2, cbv, (uint32_t)c.y, cf, ci, vnull || (maybe_null && (S.lkf[q] & SW_LKF_NULL) != 0))) {
             res = q;
             break;
           }
@@ -659,47 +711,42 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     SW_STAMP(2);
     {
       const unsigned long long gb = S.gbase;
+      const int q0 = (int)tid * SWS_PER;
+      int16_t mw[SWS_PER + SW_PROBE];  // m(q0 - SW_PROBE .. q0 + SWS_PER - 1); guards below 0
+#pragma unroll
+      for (int i = 0; i < SWS_PER + SW_PROBE; i++) mw[i] = SWM(q0 - SW_PROBE + i);
+      uint64_t dst = gb + off;
+#pragma unroll
       for (int k = 0; k < SWS_PER; k++) {
-        const int q = (int)tid * SWS_PER + k;
+        const int q = q0 + k;
         const uint32_t c = q < E ? (S.cnt2[q >> 1] >> ((q & 1) * 16)) & 0xffffu : 0u;
         if (c) {
-          const uint64_t dst = gb + off;
           const int64_t sq = B.seq0 + S.ref[q];
-          int16_t mm[SW_PROBE];
+          // candidates within SW_PROBE positions before q: bit d-1 set when m(q - d) == q
+          uint32_t near = 0;
 #pragma unroll
-          for (int d = 0; d < SW_PROBE; d++) mm[d] = SWM(q - 1 - d);  // guards below position 0
+          for (int d = 1; d <= SW_PROBE; d++) near |= (mw[k + SW_PROBE - d] == q ? 1u : 0u) << (d - 1);
           uint32_t found = 0;
-#pragma unroll
-          for (int d = 0; d < SW_PROBE; d++) {
-            if (mm[d] == q) {
-              const int p = q - 1 - d;
-              const uint32_t r = S.ref[p];
-              const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
-              const uint64_t slot = dst + (c - 1 - found);
-              if (slot < (uint64_t)O.cap) {
-                longlong2 pr;
-                pr.x = si;
-                pr.y = sq;
-                *(longlong2*)(O.refs + 2 * slot) = pr;
-              }
-              found++;
-            }
+          while (near) {
+            const int d = __ffs(near);  // nearest first = largest i first
+            near &= near - 1;
+            const int p = q - d;
+            const uint32_t r = S.ref[p];
+            const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
+            const uint64_t slot = dst + (c - 1 - found);
+            if (slot < (uint64_t)O.cap) *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
+            found++;
           }
           for (int p = q - 1 - SW_PROBE; p >= 0 && found < c; p--) {
             if (SWM(p) != q) continue;
             const uint32_t r = S.ref[p];
             const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
             const uint64_t slot = dst + (c - 1 - found);
-            if (slot < (uint64_t)O.cap) {
-              longlong2 pr;
-              pr.x = si;
-              pr.y = sq;
-              *(longlong2*)(O.refs + 2 * slot) = pr;
-            }
+            if (slot < (uint64_t)O.cap) *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
             found++;
           }
         }
-        off += c;
+        dst += c;
       }
     }
     SW_STAMP(3);
@@ -899,11 +946,25 @@ struct SweepState {
       if (t.bk == 0) {
         double c = t.bc;
         if (f && !(c != c) && (double)(float)c != c) f = false;
-        if (i && !(c == (double)(int32_t)c && c >= -2147483648.0 && c <= 2147483647.0)) i = false;
+        if (i && !(c >= -2147483648.0 && c <= 2147483647.0 && c == std::floor(c))) i = false;
       }
       if (t.flt) i = false;
     }
     return f ? 1 : (i ? 2 : 0);
+  }
+
+  // f1 as `e1.v OP constant` terms (needed for the typed compare paths)
+  static bool canonical_e1(SwPred& p) {
+    for (int i = 0; i < p.n; i++) {
+      SwTerm& t = p.t[i];
+      if (t.ak == 0 && t.bk == 1) {
+        std::swap(t.ak, t.bk);
+        std::swap(t.ac, t.bc);
+        t.mask = (t.mask & 0xA) | ((t.mask & 1) << 2) | ((t.mask & 4) >> 2);
+      }
+      if (!(t.ak == 1 && t.bk == 0)) return false;
+    }
+    return true;
   }
 
   // rewrite every term of f2 as `e2.v OP B` (B const or e1.v), mirroring the operator on a swap
@@ -976,7 +1037,16 @@ struct SweepState {
       throw std::runtime_error("sweep: predicate not lowerable");
     D.within = f.within;
     D.fstream = f.stream;
-    ct = compare_type(D.f2, (int8_t)D.vtag);
+    {
+      SwPred c1 = D.f1;
+      if (canonical_e1(c1)) {
+        D.f1 = c1;
+        int a = compare_type(D.f1, (int8_t)D.vtag), b = compare_type(D.f2, (int8_t)D.vtag);
+        ct = a == b ? a : 0;
+      } else {
+        ct = 0;  // f1 evaluated by the generic double path
+      }
+    }
     D.nown = nown;
     D.own_bits = 0;
     while ((1 << D.own_bits) < nown) D.own_bits++;
@@ -1025,6 +1095,7 @@ struct SweepState {
   // the three passes over one batch; matches (i, j) go to O.refs in per-key emission order
   void run(const BatchView& B, const int32_t* key, const MatchOut& O, int* err, hipStream_t s, KTimer& kt) {
     if (B.n <= 0) return;
+    if (B.nulls[0]) D.maybe_null = 1;
     D.nst = (int32_t)((B.n + st_len - 1) / st_len);
     size_t nc = (size_t)D.nown * D.nst + 1;
     kt.mark("sw_count", s);

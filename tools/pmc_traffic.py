@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""HBM traffic per kernel launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+gfx950 correction (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): FETCH_SIZE counts
+half the bytes of a wide coalesced streaming read, so reads are doubled:
+    hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024      (FETCH_SIZE / WRITE_SIZE in KB)
+Usage: pmc_traffic.py <fetch_dir> <write_dir>  -> JSON on stdout (bench.py reads it as --pmc)
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+
+def short(name: str) -> str:
+    n = name.replace("(anonymous namespace)::", "")
+    m = re.search(r"k_(\w+?)(?:<[^(]*)?\(", n)
+    return m.group(1) if m else n[:60]
+
+
+def per_kernel(d: str, counter: str):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    acc = {}
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = short(r["Kernel_Name"])
+            s = acc.setdefault(k, [0.0, set()])
+            s[0] += float(r["Counter_Value"])
+            s[1].add(r["Dispatch_Id"])
+    return {k: v[0] / max(1, len(v[1])) for k, v in acc.items()}
+
+
+def main():
+    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+    write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    out = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
+                     "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 read correction)",
+           "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(k, 0.0), write.get(k, 0.0)
+        out["kernels"][k] = {"fetch_kb": f, "write_kb": w, "hbm_bytes_per_launch": (2 * f + w) * 1024}
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()
