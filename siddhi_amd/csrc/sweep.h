@@ -49,12 +49,14 @@ constexpr int SWP_ROUND = 2048;
 constexpr int SWP_SEG = SWP_ROUND / SW_WAVES;
 constexpr int SWP_SUB = SWP_SEG / 64;
 // solve
-constexpr int SWS_CHUNK = 2048;
+constexpr int SWS_CHUNK = 1984;  // records per chunk: with ~<64 carried, E <= 2048 = 4 per thread
 constexpr int SWS_CCAP = 512;  // carried open candidates per owner
 constexpr int SWS_EMAX = SWS_CHUNK + SWS_CCAP;
 constexpr int SWS_SEG = SWS_EMAX / SW_WAVES;
 constexpr int SWS_SUB = SWS_SEG / 64;
-constexpr int SW_PROBE = 8;  // positions every candidate probes without a loop
+constexpr int SW_PROBE = 8;  // probe window (emit back-search, sentinel padding)
+constexpr int SW_P1 = 4;     // first-round probes per position
+constexpr int SW_P2 = 8;     // probes per worklist round
 
 // error bits (engine.hip maps them to status codes)
 constexpr int SWE_KEYS = 1 << 20;   // key id outside [0, max_keys)
@@ -423,15 +425,46 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
 #define SWM(p) S.m_[8 + (p)]
 constexpr int SWS_THREADS = 512;
 constexpr int SWS_WAVES = SWS_THREADS / 64;
-constexpr int SWS_RPT = SWS_CHUNK / SWS_THREADS;  // records per thread
+constexpr int SWS_RPT = (SWS_CHUNK + SWS_THREADS - 1) / SWS_THREADS;  // prefetch slots per thread
 constexpr int SWS_PER = (SWS_EMAX + SWS_THREADS - 1) / SWS_THREADS;
 constexpr uint32_t SW_LKF_CAR = 1u << 8, SW_LKF_NULL = 1u << 9, SW_LKF_NONE = 0xFFu;
 constexpr int32_t SW_TS_FLOOR = -(1 << 30) - 1;  // carried ts below this are clamped (all expired)
 constexpr int64_t SW_TS_SPAN = 1ll << 29;        // |event ts - chunk base| bound
 
+// One straight-line batch of P probes for a candidate (ts a_ts, resolved values cbv) starting at
+// sorted position qb of its key run ending at `end`: -2 run ended (open), -1 expired, q closing
+// event, -4 unresolved.  `res` carries an earlier resolution through unchanged.
+template <int NT2, int CT, int P>
+__device__ __forceinline__ int sw_probe(const int2* tv, const uint16_t* lkf, int qb, int end, int32_t a_ts, int32_t W,
+                                        const SwPred& f2, const SwCand<CT>& cbv, bool vflt, bool vnull, bool maybe_null,
+                                        int res) {
+  int2 b[P];
+  uint32_t bf[P];
+#pragma unroll
+  for (int d = 0; d < P; d++) {
+    b[d] = tv[qb + d];
+    bf[d] = 0;
+  }
+  if (maybe_null) {
+#pragma unroll
+    for (int d = 0; d < P; d++) bf[d] = lkf[qb + d];
+  }
+#pragma unroll
+  for (int d = 0; d < P; d++) {
+    double ef = 0, ei = 0;
+    if constexpr (CT == 0) sw_conv((uint32_t)b[d].y, vflt, ef, ei);
+    const bool inrun = qb + d < end;
+    const bool expired = b[d].x - a_ts > W;
+    const bool hit = sw_close<NT2, CT>(f2, cbv, (uint32_t)b[d].y, ef, ei, vnull || (bf[d] & SW_LKF_NULL) != 0);
+    const int r = !inrun ? -2 : (expired ? -1 : (hit ? qb + d : -4));
+    res = res == -4 ? r : res;
+  }
+  return res;
+}
+
 struct SwSolveSmem {
-  int2 tv[SWS_EMAX + SW_PROBE];       // (ts - chunk base, value) by sorted position, then sentinels
-  uint16_t lkf[SWS_EMAX + SW_PROBE];  // local key | carried | null
+  int2 tv[SWS_EMAX + 2 * SW_PROBE];   // (ts - chunk base, value) by sorted position, then sentinels
+  uint16_t lkf[SWS_EMAX + 2 * SW_PROBE];  // local key | carried | null
   uint32_t ref[SWS_EMAX];             // batch index, or carry slot (carried)
   uint32_t cnt2[SWS_EMAX / 2 + 1];    // closes per position, two 16-bit counters per word
   int16_t m_[8 + SWS_EMAX + 8];       // m(p) = m_[8 + p]: >=0 closing position, -1 expired, -2 open,
@@ -446,6 +479,8 @@ struct SwSolveSmem {
   int64_t lastts[SW_LK];              // batch-relative ts of the key's latest event (INT64_MIN unseen)
   uint32_t wtot[SWS_WAVES];
   unsigned long long gbase;
+  uint16_t wl[SWS_EMAX];              // probe worklist (unresolved candidates)
+  uint32_t wln;
 };
 
 template <int NW>
@@ -511,8 +546,9 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
   SwRec pf[SWS_RPT];
 #pragma unroll
   for (int s = 0; s < SWS_RPT; s++) {
-    const int64_t j = rb + (int64_t)w * (64 * SWS_RPT) + s * 64 + lane;
-    if (j < re) pf[s] = D.recs[j];
+    const int jj = (int)w * (64 * SWS_RPT) + s * 64 + (int)lane;
+    const int64_t j = rb + jj;
+    if (jj < SWS_CHUNK && j < re) pf[s] = D.recs[j];
   }
   uint64_t tbk = D.recs[rb].kt;
   __syncthreads();
@@ -604,7 +640,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       S.lkf[p] = (uint16_t)(lk | SW_LKF_CAR | ((kt & SW_NULL) ? SW_LKF_NULL : 0u));
       S.ref[p] = (uint32_t)x;
     }
-    if (tid < SW_PROBE) {
+    if (tid < 2 * SW_PROBE) {
       S.tv[E + tid] = make_int2(0, 0);
       S.lkf[E + tid] = (uint16_t)SW_LKF_NONE;
     }
@@ -614,14 +650,20 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       const int64_t nb = cb + SWS_CHUNK;
 #pragma unroll
       for (int s = 0; s < SWS_RPT; s++) {
-        const int64_t j = nb + (int64_t)w * (64 * SWS_RPT) + s * 64 + lane;
-        if (j < re) pf[s] = D.recs[j];
+        const int jj = (int)w * (64 * SWS_RPT) + s * 64 + (int)lane;
+        const int64_t j = nb + jj;
+        if (jj < SWS_CHUNK && j < re) pf[s] = D.recs[j];
       }
       if (nb < re) tbk = D.recs[nb].kt;
     }
     __syncthreads();
     SW_STAMP(0);
-    // 3. probe: every candidate looks for its closing event among the next events of its key
+    // 3. probe.  Round 1: every position tests whether it is a candidate and probes the first
+    //    SW_P1 events of its key (straight-line code, no per-lane loop).  Candidates still
+    //    unresolved go to a worklist; each later round gives every worklist entry SW_P2 more
+    //    events, so lanes stay busy on the few long scans instead of idling in divergent loops.
+    if (tid == 0) S.wln = 0;
+    __syncthreads();
     for (int k = 0; k < SWS_PER; k++) {
       const int p = (int)tid + k * SWS_THREADS;
       if (p >= E) break;
@@ -642,67 +684,78 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       const int q0 = max(p + 1, (int)S.fe[lk]);  // carried candidates are not events
       const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
       int res = cand ? -4 : -3;  // -4: unresolved
-      int2 b[SW_PROBE];
-      uint32_t bf[SW_PROBE];
-#pragma unroll
-      for (int d = 0; d < SW_PROBE; d++) {
-        b[d] = S.tv[q0 + d];
-        bf[d] = 0;
-      }
-      if (maybe_null) {
-#pragma unroll
-        for (int d = 0; d < SW_PROBE; d++) bf[d] = S.lkf[q0 + d];
-      }
-#pragma unroll
-      for (int d = 0; d < SW_PROBE; d++) {
-        double ef = 0, ei = 0;
-        if constexpr (CT == 0) sw_conv((uint32_t)b[d].y, vflt, ef, ei);
-        const bool inrun = q0 + d < end;
-        const bool expired = b[d].x - a.x > W;
-        const bool hit = sw_close<NT2, CT>(f2, cbv, (uint32_t)b[d].y, ef, ei, vnull || (bf[d] & SW_LKF_NULL) != 0);
-        const int r = !inrun ? -2 : (expired ? -1 : (hit ? q0 + d : -4));
-        res = res == -4 ? r : res;
-      }
-#ifdef SHP_SW_STAMPS
-      if (cand) dbg_cands++;
-#endif
+      res = sw_probe<NT2, CT, SW_P1>(S.tv, S.lkf, q0, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, res);
       if (res == -4) {
-        res = -2;
-        for (int q = q0 + SW_PROBE; q < end; q++) {
-#ifdef SHP_SW_STAMPS
-          dbg_steps++;
-#endif
-          const int2 c = S.tv[q];
-          if (c.x - a.x > W) {
-            res = -1;
-            break;
-          }
-          double cf = 0, ci = 0;
-          if constexpr (CT == 0) sw_conv((uint32_t)c.y, vflt, cf, ci);
-          if (sw_close<NT2, CT>(f2, cbv, (uint32_t)c.y, cf, ci, vnull || (maybe_null && (S.lkf[q] & SW_LKF_NULL) != 0))) {
-            res = q;
-            break;
-          }
+        const uint32_t i = atomicAdd(&S.wln, 1u);
+        S.wl[i] = (uint16_t)p;
+      } else {
+        SWM(p) = (int16_t)res;
+        if (res >= 0) atomicAdd(&S.cnt2[res >> 1], 1u << ((res & 1) * 16));
+      }
+    }
+    __syncthreads();
+    for (int round = 0;; round++) {
+      const uint32_t nw = S.wln;
+      if (nw == 0) break;  // uniform: every thread read the same count after the barrier
+      uint32_t item[SWS_PER];
+#pragma unroll
+      for (int k = 0; k < SWS_PER; k++) {
+        const uint32_t i = tid + (uint32_t)k * SWS_THREADS;
+        item[k] = i < nw ? (uint32_t)S.wl[i] : 0xffffffffu;
+      }
+      __syncthreads();
+      if (tid == 0) S.wln = 0;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < SWS_PER; k++) {
+        if (item[k] == 0xffffffffu) continue;
+        const int p = (int)item[k];
+        const uint32_t f = S.lkf[p];
+        const int2 a = S.tv[p];
+        const bool an = vnull || (f & SW_LKF_NULL) != 0;
+        double af = 0, ai = 0;
+        if constexpr (CT == 0) sw_conv((uint32_t)a.y, vflt, af, ai);
+        const uint32_t lk = f & 0xFFu;
+        const int end = (int)S.binoff[lk + 1];
+        const int qn = max(p + 1, (int)S.fe[lk]) + SW_P1 + round * SW_P2;
+        const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
+        int res = sw_probe<NT2, CT, SW_P2>(S.tv, S.lkf, qn, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, -4);
+        if (res == -4 && qn + SW_P2 >= end) res = -2;  // key run exhausted: still open
+        if (res == -4) {
+          const uint32_t i = atomicAdd(&S.wln, 1u);
+          S.wl[i] = (uint16_t)p;
+        } else {
+          SWM(p) = (int16_t)res;
+          if (res >= 0) atomicAdd(&S.cnt2[res >> 1], 1u << ((res & 1) * 16));
         }
       }
-      SWM(p) = (int16_t)res;
-      if (res >= 0) atomicAdd(&S.cnt2[res >> 1], 1u << ((res & 1) * 16));
+      __syncthreads();
     }
     if (tid < 8) SWM(E + tid) = -3;
     __syncthreads();
     SW_STAMP(1);
-    // 4. closes per event (counted by the probe), output offsets, then the pairs: each closing
-    //    event collects its candidates backwards (they sit within the window before it)
-    uint32_t tot = 0;
+    // 4. closes per event (counted by the probe) -> exclusive output offsets (16-bit, in place of
+    //    the counts), then every matched candidate writes its own pair: its slot among the
+    //    candidates of its closing event q is fixed by how many later candidates q also closed
+    uint16_t* off16 = reinterpret_cast<uint16_t*>(S.cnt2);
+    uint32_t cq[SWS_PER], tot = 0;
 #pragma unroll
     for (int k = 0; k < SWS_PER; k++) {
       const int q = (int)tid * SWS_PER + k;
-      tot += q < E ? (S.cnt2[q >> 1] >> ((q & 1) * 16)) & 0xffffu : 0u;
+      cq[k] = q < E ? off16[q] : 0u;
+      tot += cq[k];
     }
     for (int i = tid; i <= SW_LK; i += SWS_THREADS) S.ncar[i] = 0;  // recounted by the carry step
     uint32_t total;
     uint32_t off = sw_block_scan_n<SWS_WAVES>(tot, S.wtot, total);
+#pragma unroll
+    for (int k = 0; k < SWS_PER; k++) {
+      const int q = (int)tid * SWS_PER + k;
+      if (q < E) off16[q] = (uint16_t)off;
+      off += cq[k];
+    }
     if (tid == 0) {
+      off16[E] = (uint16_t)total;
       const unsigned long long g = total ? atomicAdd(O.count, (unsigned long long)total) : 0ull;
       if (g + total > (unsigned long long)O.cap) e |= E_OUT;
       S.gbase = g;
@@ -711,42 +764,21 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     SW_STAMP(2);
     {
       const unsigned long long gb = S.gbase;
-      const int q0 = (int)tid * SWS_PER;
-      int16_t mw[SWS_PER + SW_PROBE];  // m(q0 - SW_PROBE .. q0 + SWS_PER - 1); guards below 0
-#pragma unroll
-      for (int i = 0; i < SWS_PER + SW_PROBE; i++) mw[i] = SWM(q0 - SW_PROBE + i);
-      uint64_t dst = gb + off;
-#pragma unroll
       for (int k = 0; k < SWS_PER; k++) {
-        const int q = q0 + k;
-        const uint32_t c = q < E ? (S.cnt2[q >> 1] >> ((q & 1) * 16)) & 0xffffu : 0u;
-        if (c) {
-          const int64_t sq = B.seq0 + S.ref[q];
-          // candidates within SW_PROBE positions before q: bit d-1 set when m(q - d) == q
-          uint32_t near = 0;
+        const int p = (int)tid + k * SWS_THREADS;
+        if (p >= E) break;
+        const int q = SWM(p);
+        if (q < 0) continue;
+        const uint32_t c = (uint32_t)off16[q + 1] - off16[q];
+        uint32_t later = 0;
 #pragma unroll
-          for (int d = 1; d <= SW_PROBE; d++) near |= (mw[k + SW_PROBE - d] == q ? 1u : 0u) << (d - 1);
-          uint32_t found = 0;
-          while (near) {
-            const int d = __ffs(near);  // nearest first = largest i first
-            near &= near - 1;
-            const int p = q - d;
-            const uint32_t r = S.ref[p];
-            const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
-            const uint64_t slot = dst + (c - 1 - found);
-            if (slot < (uint64_t)O.cap) *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
-            found++;
-          }
-          for (int p = q - 1 - SW_PROBE; p >= 0 && found < c; p--) {
-            if (SWM(p) != q) continue;
-            const uint32_t r = S.ref[p];
-            const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
-            const uint64_t slot = dst + (c - 1 - found);
-            if (slot < (uint64_t)O.cap) *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
-            found++;
-          }
-        }
-        dst += c;
+        for (int d = 1; d <= SW_PROBE; d++) later += (p + d < q && SWM(p + d) == q) ? 1u : 0u;
+        for (int p2 = p + SW_PROBE + 1; p2 < q; p2++) later += SWM(p2) == q ? 1u : 0u;
+        const uint32_t r = S.ref[p];
+        const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
+        const int64_t sq = B.seq0 + S.ref[q];
+        const uint64_t slot = gb + off16[q] + (c - 1 - later);
+        if (slot < (uint64_t)O.cap) *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
       }
     }
     SW_STAMP(3);
