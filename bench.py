@@ -17,6 +17,8 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+
+import numpy as np
 import json
 import os
 import sys
@@ -31,6 +33,15 @@ BYTES_PER_MATCH = 16    # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
 KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_solve", "sw_expand",
            "radix_sort", "clock_scan", "key_hist", "key_scan", "sort_keys", "iota", "clamp_clock",
            "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry", "nfa_lanes")
+WORKLOADS = {
+    "1": "C1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec (one key)",
+    "2": "C2: partition with (symbol of StockStream) every e1=StockStream[price>20] -> "
+         "e2=StockStream[price>e1.price] within 1 sec",
+    "3b": "C3': partition with (k of S) every e1=S[v>20]<1:5>, e2=S[v<e1[last].v]",
+    "4": "C4: partition every (e1=S1[price>20] and e2=S2[price>20]) -> not S3[price>e1.price] for 5 sec "
+         "within 10 sec",
+    "5": "C5: partition every e1 -> e2[price>e1.price] within 1 sec select symbol, avg(e2.price)",
+}
 PATHS = {2: "sweep (owner partition + LDS sweep)", 1: "scan kernels over a key-sorted batch", 0: "general NFA lanes"}
 
 
@@ -40,7 +51,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--events", type=int, default=100_000_000, help="events per GPU per step")
-    ap.add_argument("--keys", type=int, default=10_000)
+    ap.add_argument("--keys", type=int, default=0, help="keys (default: the config's, C2 = 10k)")
+    ap.add_argument("--config", default="2", help="SURVEY §8d config: 2 (headline), 1, 3b, 4, 5")
     ap.add_argument("--cpu-sample", type=int, default=2_500_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=["auto", "general", "scan"], default="auto",
@@ -62,17 +74,23 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from siddhi_amd import native, synth
+    from siddhi_amd import native, shard, synth
     from siddhi_amd.query.compiler import compile_app
 
-    _, qs, _ = compile_app(synth.QUERIES[2])
+    cfg_id = int(a.config) if a.config.isdigit() else a.config
+    spec = synth.CONFIGS[3 if cfg_id == "3b" else cfg_id]
+    _, qs, _ = compile_app(synth.QUERIES[cfg_id])
     cq = qs[0]
-    N, K, G = a.events, a.keys, world
+    assert all(c[1] == 1 and c[2] == "float" for c in cq.columns), "bench configs read price only"
+    N, G = a.events, world
+    K = a.keys if a.keys else spec.keys
+    K_local = -(-K // G)  # each rank's engine holds a dense dictionary of the keys it owns
     cap = int(N * 1.08) + 4096 if G > 1 else N
     force = {"auto": 0, "general": 1, "scan": 2}[a.path]
-    eng = native.HipEngine(cq.program_json(), 0, max_keys=K, max_batch=cap, max_matches=cap,
+    eng = native.HipEngine(cq.program_json(), 0, max_keys=K_local, max_batch=cap, max_matches=cap,
                            device=local, force_general=force, profile_kernels=True,
-                           match_layout=native.LAYOUT_PAIRS if force == 0 else native.LAYOUT_FULL)
+                           match_layout=native.LAYOUT_PAIRS if force == 0 and _sweep_shape(cq, local, K_local)
+                           else native.LAYOUT_FULL)
     L = native.lib()
     steps = a.warmup + a.steps
 
@@ -82,41 +100,34 @@ def main():
         ts = torch.empty(N, dtype=torch.int64, device="cuda")
         key = torch.empty(N, dtype=torch.int32, device="cuda")
         price = torch.empty(N, dtype=torch.float32, device="cuda")
-        rc = L.shp_synth_fill(2, start, N, K, 1, 0, ts.data_ptr(), key.data_ptr(), price.data_ptr(),
-                              None, None, None)
+        stream = torch.empty(N, dtype=torch.int32, device="cuda") if spec.n_streams > 1 else None
+        rc = L.shp_synth_fill(spec.config, start, N, K, spec.n_streams, int(spec.dense), ts.data_ptr(),
+                              key.data_ptr(), price.data_ptr(), None,
+                              stream.data_ptr() if stream is not None else None, None)
         assert rc == 0
-        return ts, key, price
+        return ts, key, price, stream
 
     batches = [gen(s) for s in range(steps)]
     torch.cuda.synchronize()
 
-    def exchange(ts, key, price):
-        """RCCL all-to-all of the SoA columns by key owner (key % G); order within a source kept."""
-        owner = key % G
-        order = torch.argsort(owner, stable=True)
-        send_counts = torch.bincount(owner, minlength=G)
-        recv_counts = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts)
-        sc = send_counts.tolist()
-        rc_ = recv_counts.tolist()
-        tot = sum(rc_)
-        out = []
-        for col in (ts, key, price):
-            src = col[order]
-            dst = torch.empty(tot, dtype=col.dtype, device=col.device)
-            dist.all_to_all_single(dst, src, rc_, sc)
-            out.append(dst)
-        return out
-
     def step(i):
-        ts, key, price = batches[i]
+        ts, key, price, stream = batches[i]
         if G > 1:
-            ts, key, price = exchange(ts, key, price)
-            torch.cuda.current_stream().synchronize()  # engine runs on its own HIP stream
+            cols = {"ts": ts, "key": key, "price": price}
+            if stream is not None:
+                cols["stream"] = stream
+            got = shard.exchange(cols, "key", G, dist)
+            ts, price, stream = got["ts"], got["price"], got.get("stream")
+            key = shard.local_key(got["key"], G).to(torch.int32)
+            torch.cuda.current_stream().synchronize()  # the engine runs on its own HIP stream
         n = ts.numel()
-        colp = (ctypes.c_void_p * 1)(price.data_ptr())
+        # one pointer per program column (cq.columns: (stream, attr, type)); every stream's
+        # predicate attribute is the synthetic price column
+        ncol = max(1, len(cq.columns))
+        colp = (ctypes.c_void_p * ncol)(*([price.data_ptr()] * ncol))
         # one input stream: the stream column is NULL (= every event on stream 0)
-        b = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), None, ctypes.cast(colp, ctypes.c_void_p), None)
+        b = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), stream.data_ptr() if stream is not None else None,
+                            ctypes.cast(colp, ctypes.c_void_p), None)
         mt = native.ShpMatches()
         rc = L.shp_push_batch_device(eng.h, ctypes.byref(b), ctypes.byref(mt))
         if rc != 0:
@@ -131,8 +142,11 @@ def main():
     kernel_ms = {}
     t0 = time.perf_counter()
     ev_local, m_local = 0, 0
+    lat = []
     for i in range(a.warmup, steps):
-        n, m = step(i)
+        ts0 = time.perf_counter()
+        n, m = step(i)  # synchronous: matches are counted on the host when it returns
+        lat.append((time.perf_counter() - ts0) * 1e3)
         ev_local += n
         m_local += m
         for name in KERNELS:
@@ -169,7 +183,7 @@ def main():
                 traffic = None
         cpu = None
         if not a.no_cpu_baseline and G == 1:
-            cpu = cpu_baseline(cq, a.cpu_sample, K)
+            cpu = cpu_baseline(cq, a.cpu_sample, K, spec.config)
         line = {
             "metric": "input events/sec, keyed pattern query, 1/2/4/8 MI355X; p99 batch latency",
             "value": value,
@@ -184,15 +198,15 @@ def main():
             "dtype": "f32 compare / int64 ts",
             "data": "synthetic (PCG32 stream of SURVEY.md §8d, generated in HBM)",
             "config": {
-                "workload": "C2: partition with (symbol of StockStream) every e1=StockStream[price>20] -> "
-                            "e2=StockStream[price>e1.price] within 1 sec; 10k keys",
+                "workload": WORKLOADS.get(str(cfg_id), f"C{cfg_id}") + f"; {K} keys",
                 "events_per_gpu_per_step": N,
                 "keys": K,
                 "parallelism": f"key-sharded x{G}" + (" (RCCL all-to-all by key owner)" if G > 1 else ""),
                 "engine_path": PATHS.get(eng.path, str(eng.path)),
                 "matches_per_s": m_total / elapsed,
                 "matches_per_step_gpu0": m_per_launch,
-                "p50_batch_ms": elapsed / a.steps * 1e3,
+                "p50_batch_ms": float(np.percentile(lat, 50)),
+                "p99_batch_ms": float(np.percentile(lat, 99)),
             },
             "roofline": {
                 "bound": "hbm",
@@ -212,18 +226,28 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(cq, sample, keys):
+def _sweep_shape(cq, device, keys):
+    """Does the engine pick the sweep path (and so allow the PAIRS layout) for this query?"""
+    from siddhi_amd import native
+    e = native.HipEngine(cq.program_json(), 0, max_keys=keys, max_batch=16, device=device)
+    try:
+        return e.path == 2
+    finally:
+        e.close()
+
+
+def cpu_baseline(cq, sample, keys, config=2):
     """Oracle (C++ restatement of the reference semantics), one thread, first `sample` C2 events."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from diff_util import run, small_stream
     from oracle.oracle import OracleEngine
-    g = small_stream(2, sample, keys)
+    g = small_stream(config, sample, keys)
     e = OracleEngine(cq.program_json(), 0)
     t = time.perf_counter()
     mb = run(e, cq, g)
     dt = time.perf_counter() - t
     return {"value": sample / dt, "unit": "events/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample} events of the C2 stream ({keys} keys), oracle/liboracle.so, "
+            "sample": f"first {sample} events of the C{config} stream ({keys} keys), oracle/liboracle.so, "
                       f"{len(mb['key'])} matches, {dt:.1f} s"}
 
 

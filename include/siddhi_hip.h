@@ -49,7 +49,8 @@ typedef struct shp_config {
   int64_t max_batch;       /* largest n accepted by one push */
   int64_t max_matches;     /* match-record capacity per push */
   int64_t start_clock;     /* event-time clock at start() (0 in playback mode) */
-  int32_t force_general;   /* 1: general NFA lanes only; 2: no sweep path (scan kernel or lanes) */
+  int32_t force_general;   /* 0 auto; 1 general NFA lanes only; 2 no sweep path (scan kernels or
+                              lanes); 3 sweep path whenever the shape allows (any key count) */
   int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
   int32_t match_layout;    /* SHP_LAYOUT_FULL (0) or SHP_LAYOUT_PAIRS (1, sweep path only) */
 } shp_config;

@@ -107,6 +107,8 @@ __global__ __launch_bounds__(64) void k_nfa_lanes(const DevProg* __restrict__ Pp
 }
 
 // ---------------------------------------------------------------- engine
+constexpr int32_t SWEEP_MIN_KEYS = 256;
+
 struct shp_engine {
   KTimer kt;
   ProgramCompiler comp;
@@ -231,7 +233,10 @@ struct shp_engine {
     fast = comp.fast.ok && cfg.force_general != 1;
     int32_t nown = 0;
     std::vector<uint32_t> kmap;
-    if (fast && cfg.force_general == 0 && SweepState::shape_ok(comp.P, comp.fast) &&
+    // the sweep needs enough keys to spread over workgroups (one owner region is sequential);
+    // below SWEEP_MIN_KEYS the scan kernels are parallel over candidates instead
+    const bool want_sweep = cfg.force_general == 3 || (cfg.force_general == 0 && cfg.max_keys >= SWEEP_MIN_KEYS);
+    if (fast && want_sweep && SweepState::shape_ok(comp.P, comp.fast) &&
         SweepState::build_map(cfg.max_keys, nown, kmap))
       fast = 2;
     if (cfg.match_layout == SHP_LAYOUT_PAIRS && fast != 2)

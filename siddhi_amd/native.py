@@ -105,7 +105,7 @@ class HipEngine:
     def __init__(self, program_json: str, start_clock: int = 0, max_keys: int = 1 << 16,
                  max_batch: int = 1 << 20, max_matches: int = 0, device: int = 0, force_general: int = 0,
                  profile_kernels: bool = False, match_layout: int = LAYOUT_FULL):
-        """force_general: 0 auto path, 1 general NFA lanes only, 2 no sweep path."""
+        """force_general: 0 auto path, 1 general NFA lanes only, 2 no sweep path, 3 sweep whenever possible."""
         L = lib()
         cfg = ShpConfig(device, max_keys, max_batch, max_matches, int(start_clock), int(force_general),
                         int(profile_kernels), int(match_layout))

@@ -61,7 +61,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("name,q,n,keys", CASES, ids=[c[0] for c in CASES])
-@pytest.mark.parametrize("general", [1, 2, 0], ids=["general", "scan", "default"])
+@pytest.mark.parametrize("general", [1, 2, 3, 0], ids=["general", "scan", "sweep", "default"])
 @pytest.mark.parametrize("batch", [None, 9973], ids=["whole", "split"])
 def test_synthetic_matches_oracle(name, q, n, keys, general, batch):
     cq = program_for(q)
@@ -69,8 +69,9 @@ def test_synthetic_matches_oracle(name, q, n, keys, general, batch):
     a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
     eng = hip(general, max_keys=keys, max_batch=batch or n)(cq.program_json(), 0)
     if q in (2, 5, 1):
-        want = {1: 0, 2: 1, 0: 2}[general]
-        assert eng.path == want, "2-state every/within shape: sweep by default, scan kernel when asked"
+        auto = 2 if keys >= 256 else 1  # SWEEP_MIN_KEYS
+        want = {1: 0, 2: 1, 3: 2, 0: auto}[general]
+        assert eng.path == want, "2-state every/within shape: sweep (>= 256 keys) or scan kernels"
     b = per_key(run(eng, cq, g, batch))
     msg = compare(a, b)
     assert msg is None, msg
@@ -131,7 +132,7 @@ def test_key_out_of_range_fails_loudly():
 def test_decreasing_ts_on_fast_path_fails_loudly():
     from siddhi_amd.native import HipEngine, ShpError
     cq = program_for(2)
-    eng = HipEngine(cq.program_json(), 0, max_keys=4, max_batch=1024)
+    eng = HipEngine(cq.program_json(), 0, max_keys=4, max_batch=1024, force_general=3)
     assert eng.path == 2
     g = small_stream(2, 200, 4)
     g["ts"] = g["ts"][::-1].copy()
