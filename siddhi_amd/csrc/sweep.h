@@ -551,6 +551,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     if (jj < SWS_CHUNK && j < re) pf[s] = D.recs[j];
   }
   uint64_t tbk = D.recs[rb].kt;
+  for (int i = tid; i < SWS_WAVES * (SW_LK + 1); i += SWS_THREADS) (&S.wc[0][0])[i] = 0;
   __syncthreads();
 #ifdef SHP_SW_STAMPS
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -570,9 +571,8 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     dbg_chunks++;
     dbg_nc += nc;
 #endif
-    // 1. rank the chunk's records by local key (stable: wave-major, then sub-round, then lane)
-    for (int b = lane; b <= SW_LK; b += 64) S.wc[w][b] = 0;
-    __syncthreads();
+    // 1. rank the chunk's records by local key (stable: wave-major, then sub-round, then lane);
+    //    S.wc was zeroed during the previous chunk's probe (or before the first chunk)
     uint32_t rk[SWS_RPT], bin[SWS_RPT];
     const uint32_t nonebin = lkbits >= 8 ? SW_LKF_NONE : (1u << lkbits);
     const int rbits = lkbits >= 8 ? 8 : lkbits + 1;
@@ -645,6 +645,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       S.lkf[E + tid] = (uint16_t)SW_LKF_NONE;
     }
     for (int i = tid; i <= SWS_EMAX / 2; i += SWS_THREADS) S.cnt2[i] = 0;
+    if (tid == 0) S.wln = 0;
     // prefetch the next chunk while this one is solved
     {
       const int64_t nb = cb + SWS_CHUNK;
@@ -662,8 +663,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     //    SW_P1 events of its key (straight-line code, no per-lane loop).  Candidates still
     //    unresolved go to a worklist; each later round gives every worklist entry SW_P2 more
     //    events, so lanes stay busy on the few long scans instead of idling in divergent loops.
-    if (tid == 0) S.wln = 0;
-    __syncthreads();
+    for (int i = tid; i < SWS_WAVES * (SW_LK + 1); i += SWS_THREADS) (&S.wc[0][0])[i] = 0;  // next rank
     for (int k = 0; k < SWS_PER; k++) {
       const int p = (int)tid + k * SWS_THREADS;
       if (p >= E) break;
@@ -681,7 +681,15 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       }
       const uint32_t lk = f & 0xFFu;
       const int end = (int)S.binoff[lk + 1];
-      const int q0 = max(p + 1, (int)S.fe[lk]);  // carried candidates are not events
+      const int fe = (int)S.fe[lk];
+      const int q0 = max(p + 1, fe);  // carried candidates are not events
+      if (!car) {  // per-key timestamp order: the next event, and the key's last ts for its first
+        if (p + 1 < end && S.tv[p + 1].x < a.x) e |= SWE_MONO;
+        if (p == fe) {
+          const int64_t prev = S.lastts[lk];
+          if (prev != INT64_MIN && tb + a.x < prev) e |= SWE_MONO;
+        }
+      }
       const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
       int res = cand ? -4 : -3;  // -4: unresolved
       res = sw_probe<NT2, CT, SW_P1>(S.tv, S.lkf, q0, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, res);
@@ -782,30 +790,6 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       }
     }
     SW_STAMP(3);
-    // 5. per-key timestamp order (first event against the key's last ts, the rest against their
-    //    predecessor) and the key's latest ts
-    for (int k = 0; k < SWS_PER; k++) {
-      const int p = (int)tid + k * SWS_THREADS;
-      if (p >= E) break;
-      const uint32_t f = S.lkf[p];
-      if (f & SW_LKF_CAR) continue;
-      const uint32_t lk = f & 0xFFu;
-      const int32_t t = S.tv[p].x;
-      if (p > (int)S.fe[lk]) {
-        if (t < S.tv[p - 1].x) e |= SWE_MONO;
-      } else {
-        const int64_t prev = S.lastts[lk];
-        if (prev != INT64_MIN && tb + t < prev) e |= SWE_MONO;
-      }
-    }
-    __syncthreads();
-    for (int k = 0; k < SWS_PER; k++) {
-      const int p = (int)tid + k * SWS_THREADS;
-      if (p >= E) break;
-      const uint32_t f = S.lkf[p];
-      const uint32_t lk = f & 0xFFu;
-      if (!(f & SW_LKF_CAR) && p + 1 == (int)S.binoff[lk + 1]) S.lastts[lk] = tb + S.tv[p].x;
-    }
     SW_STAMP(4);
     // 6. still-open candidates become the carry (sorted order = key, then i)
     {
@@ -821,6 +805,11 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
 #pragma unroll
       for (int k = 0; k < SWS_PER; k++) {
         const int p = (int)tid * SWS_PER + k;
+        if (p < E) {  // the key's latest ts (its last event in the chunk)
+          const uint32_t f = S.lkf[p];
+          const uint32_t lk = f & 0xFFu;
+          if (!(f & SW_LKF_CAR) && p + 1 == (int)S.binoff[lk + 1]) S.lastts[lk] = tb + S.tv[p].x;
+        }
         if (p < E && SWM(p) == -2) {
           if (pre < (uint32_t)SWS_CCAP) {
             const uint32_t f = S.lkf[p];
