@@ -18,6 +18,7 @@
  *                       and the playback clock (core/stream/input/InputHandler.java:59-70)
  *   shp_advance_clock   TimestampGeneratorImpl.setCurrentTimestamp (core/util/timestamp/
  *                       TimestampGeneratorImpl.java:105-121) with no event (timer flush)
+ *   shp_snapshot/restore State.snapshot / State.restore of the query's state (SnapshotService)
  *   shp_engine_destroy  SiddhiAppRuntime.shutdown for the query
  * Errors are status codes (no exceptions cross the ABI); shp_last_error() gives text.
  * A single engine is not re-entrant (the reference serialises a query with
@@ -99,6 +100,13 @@ int shp_push_batch_device(shp_engine* e, const shp_batch* in, shp_matches* out);
 /* Copy the matches of the last shp_push_batch_device to host memory. */
 int shp_fetch_matches(shp_engine* e, shp_matches* out);
 int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out);
+/* Per-key state of the engine (partial matches, carried candidates, timers, clock, sequence
+ * numbers) as an opaque blob (engine-owned, valid until the next snapshot or destroy), and its
+ * restore into an engine created from the same program with the same path and max_keys.
+ * Replaces State.snapshot()/restore() (core/util/snapshot/state/State.java:25-36) as driven by
+ * SnapshotService (core/util/snapshot/SnapshotService.java:90-188) for the query. */
+int shp_snapshot(shp_engine* e, void** buf, size_t* len);
+int shp_restore(shp_engine* e, const void* buf, size_t len);
 int shp_engine_num_states(const shp_engine* e);
 /* Which kernels the engine runs: 2 = sweep (owner partition + LDS sweep), 1 = specialised 2-state
  * scan kernel, 0 = general NFA lanes. */

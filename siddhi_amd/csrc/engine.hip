@@ -220,6 +220,7 @@ struct shp_engine {
     if (cfg.max_batch < 1) cfg.max_batch = 1 << 16;
     if (cfg.max_matches < 1) cfg.max_matches = std::max<int64_t>(cfg.max_batch, 1 << 16);
     comp.compile(json);
+    program = json;
     if (!comp.P.partitioned) cfg.max_keys = 1;
     HIP_OK(hipSetDevice(cfg.device));
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -399,6 +400,108 @@ struct shp_engine {
       if (herr & SWE_RANGE) return fail(SHP_ERR_UNSUPPORTED, "timestamps span more than 2^49 ms on the sweep path");
       return fail(SHP_ERR_CAPACITY, "per-key table capacity exceeded (code " + std::to_string(herr) + ")");
     }
+    return SHP_OK;
+  }
+
+  // ---- snapshot / restore (State.snapshot/restore, core/util/snapshot/state/State.java:25-36):
+  // the device buffers that carry per-key state across pushes, for the engine's path
+  struct Section {
+    void* p;
+    size_t bytes;
+  };
+  std::vector<Section> state_sections() {
+    std::vector<Section> v;
+    const int64_t nk = cfg.max_keys;
+    if (fast == 2) {
+      const SweepDev& D = sw.D;
+      const int64_t no = D.nown, cc = (int64_t)no * SWS_CCAP;
+      v = {{D.c_n, (size_t)no * 4}, {D.c_ts, (size_t)cc * 8}, {D.c_seq, (size_t)cc * 8}, {D.c_v, (size_t)cc * 4},
+           {D.c_lk, (size_t)cc}, {D.c_null, (size_t)cc}, {D.lastts, (size_t)no * SW_LK * 8}, {D.tsmax, 8}};
+    } else if (fast == 1) {
+      const FastDev& F = fs.F;
+      v = {{F.c_seq, (size_t)nk * FCC * 8}, {F.c_ts, (size_t)nk * FCC * 8}, {F.c_val, (size_t)nk * FCC * 16},
+           {F.c_null, (size_t)nk * FCC * 2}, {F.c_n, (size_t)nk * 4}, {F.c_match, (size_t)nk * FCC * 4},
+           {F.last_ts, (size_t)nk * 8}, {F.first_open, (size_t)nk * 4}};
+    } else {
+      v = {{arena, (size_t)Y.bytes}};
+    }
+    return v;
+  }
+
+  static uint64_t fnv1a(const std::string& t) {
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : t) h = (h ^ c) * 1099511628211ull;
+    return h;
+  }
+
+  std::vector<char> snap;
+  std::string program;
+  struct SnapHeader {
+    char magic[8];
+    int32_t version, path;
+    int64_t max_keys, seq, clock, sections, payload;
+    uint64_t program_hash;
+    int32_t maybe_null, pad;
+  };
+
+  void snapshot(void** buf, size_t* len) {
+    HIP_OK(hipStreamSynchronize(stream));
+    auto secs = state_sections();
+    size_t payload = 0;
+    for (auto& x : secs) payload += 8 + x.bytes;
+    snap.assign(sizeof(SnapHeader) + payload, 0);
+    SnapHeader h{};
+    memcpy(h.magic, "SHPSNAP1", 8);
+    h.version = 1;
+    h.path = fast;
+    h.max_keys = cfg.max_keys;
+    h.seq = seq;
+    h.clock = clock;
+    h.sections = (int64_t)secs.size();
+    h.payload = (int64_t)payload;
+    h.program_hash = fnv1a(program);
+    h.maybe_null = fast == 2 ? sw.D.maybe_null : 0;
+    memcpy(snap.data(), &h, sizeof h);
+    char* q = snap.data() + sizeof h;
+    for (auto& x : secs) {
+      uint64_t b = x.bytes;
+      memcpy(q, &b, 8);
+      q += 8;
+      HIP_OK(hipMemcpy(q, x.p, x.bytes, hipMemcpyDeviceToHost));
+      q += x.bytes;
+    }
+    *buf = snap.data();
+    *len = snap.size();
+  }
+
+  int restore(const void* buf, size_t len) {
+    SnapHeader h;
+    if (!buf || len < sizeof h) return fail(SHP_ERR_ARG, "snapshot too short");
+    memcpy(&h, buf, sizeof h);
+    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 1) return fail(SHP_ERR_ARG, "not a snapshot");
+    if (h.path != fast || h.max_keys != cfg.max_keys || h.program_hash != fnv1a(program))
+      return fail(SHP_ERR_ARG, "snapshot is of a different query, path or key capacity");
+    auto secs = state_sections();
+    if ((size_t)h.sections != secs.size() || sizeof h + (size_t)h.payload != len)
+      return fail(SHP_ERR_ARG, "snapshot layout mismatch");
+    const char* q = (const char*)buf + sizeof h;
+    for (auto& x : secs) {
+      uint64_t b;
+      memcpy(&b, q, 8);
+      q += 8;
+      if (b != x.bytes) return fail(SHP_ERR_ARG, "snapshot section size mismatch");
+      q += b;
+    }
+    q = (const char*)buf + sizeof h;
+    HIP_OK(hipStreamSynchronize(stream));
+    for (auto& x : secs) {
+      q += 8;
+      HIP_OK(hipMemcpy(x.p, q, x.bytes, hipMemcpyHostToDevice));
+      q += x.bytes;
+    }
+    seq = h.seq;
+    clock = h.clock;
+    if (fast == 2) sw.D.maybe_null = h.maybe_null;
     return SHP_OK;
   }
 
@@ -624,6 +727,19 @@ int shp_debug_sw_stamps(shp_engine* e, unsigned long long* host, int64_t n) {
   return hipMemcpy(host, e->sw.D.stamps, k * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)(k / 8) : SHP_ERR_DEVICE;
 }
 #endif
+
+int shp_snapshot(shp_engine* e, void** buf, size_t* len) {
+  if (!e || !buf || !len) return SHP_ERR_ARG;
+  return guarded(e, [&]() {
+    e->snapshot(buf, len);
+    return SHP_OK;
+  });
+}
+
+int shp_restore(shp_engine* e, const void* buf, size_t len) {
+  if (!e) return SHP_ERR_ARG;
+  return guarded(e, [&]() { return e->restore(buf, len); });
+}
 
 const char* shp_last_error(const shp_engine* e) { return e ? e->err.c_str() : "null engine"; }
 

@@ -23,7 +23,7 @@ SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACIT
 SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches",
            "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
-           "shp_dev_to_host"]
+           "shp_dev_to_host", "shp_snapshot", "shp_restore"]
 
 
 class ShpConfig(ctypes.Structure):
@@ -78,6 +78,8 @@ def lib():
         L.shp_dev_alloc.argtypes = [ctypes.c_int64]
         L.shp_dev_free.argtypes = [ctypes.c_void_p]
         L.shp_dev_to_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        L.shp_snapshot.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
+        L.shp_restore.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -157,6 +159,17 @@ class HipEngine:
         out = self._pending if self._pending is not None else _concat([], None, self.S)
         self._pending = None
         return out
+
+    def snapshot(self) -> bytes:
+        """Engine state as bytes (shp_snapshot)."""
+        buf, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(lib().shp_snapshot(self.h, ctypes.byref(buf), ctypes.byref(n)))
+        return ctypes.string_at(buf, n.value)
+
+    def restore(self, blob: bytes):
+        """Load a snapshot taken from an engine of the same query (shp_restore)."""
+        b = ctypes.create_string_buffer(blob, len(blob))
+        self._check(lib().shp_restore(self.h, b, len(blob)))
 
     def kernel_ms(self, which="total"):
         return lib().shp_last_kernel_ms(self.h, which.encode())

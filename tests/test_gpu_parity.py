@@ -138,3 +138,35 @@ def test_decreasing_ts_on_fast_path_fails_loudly():
     g["ts"] = g["ts"][::-1].copy()
     with pytest.raises(ShpError, match="SHP_ERR_UNSUPPORTED"):
         run(eng, cq, g)
+
+
+@pytest.mark.parametrize("q,keys,general", [(2, 300, 0), (2, 64, 2), (2, 64, 1), ("3b", 64, 0), (4, 200, 0),
+                                            (5, 300, 0)],
+                         ids=["c2-sweep", "c2-scan", "c2-lanes", "c3b-lanes", "c4-lanes", "c5-sweep"])
+def test_snapshot_restore_continues_exactly(q, keys, general):
+    """shp_snapshot mid-stream, shp_restore into a fresh engine, continue: the oracle's matches."""
+    cq = program_for(q)
+    g = small_stream(q, 40000, keys)
+    ref = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    half = {k: v[:20000] for k, v in g.items()}
+    rest = {k: v[20000:] for k, v in g.items()}
+    a = hip(general, max_keys=keys, max_batch=1 << 15)(cq.program_json(), 0)
+    first = run(a, cq, half)
+    blob = a.snapshot()
+    b = hip(general, max_keys=keys, max_batch=1 << 15)(cq.program_json(), 0)
+    b.restore(blob)
+    second = run(b, cq, rest)
+    from siddhi_amd.native import _concat
+    got = per_key(_concat([first, second], None, a.S))
+    assert compare(ref, got) is None
+    assert sum(len(v) for v in ref.values()) > 0
+
+
+def test_restore_rejects_other_query():
+    from siddhi_amd.native import HipEngine, ShpError
+    a = HipEngine(program_for(2).program_json(), 0, max_keys=300, max_batch=1024)
+    b = HipEngine(program_for("3b").program_json(), 0, max_keys=300, max_batch=1024)
+    with pytest.raises(ShpError, match="SHP_ERR_ARG"):
+        b.restore(a.snapshot())
+    with pytest.raises(ShpError, match="SHP_ERR_ARG"):
+        b.restore(b"garbage")
