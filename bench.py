@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=["auto", "general", "scan"], default="auto",
                     help="auto = sweep path (default); scan = round-1 scan kernels; general = NFA lanes")
+    ap.add_argument("--same-device", action="store_true",
+                    help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, collectives over gloo")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
     return ap.parse_args()
 
@@ -68,11 +70,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.same_device:  # rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0
+        local = 0
     torch.cuda.set_device(local)
     dist = None
+    backend = "gloo" if a.same_device else "nccl"  # nccl = RCCL over xGMI on ROCm
+    coll_dev = "cpu" if backend == "gloo" else "cuda"
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from siddhi_amd import native, shard, synth
     from siddhi_amd.query.compiler import compile_app
@@ -107,25 +116,28 @@ def main():
         assert rc == 0
         return ts, key, price, stream
 
-    batches = [gen(s) for s in range(steps)]
+    batches = [gen(s) for s in range(steps + (1 if G > 1 else 0))]
     torch.cuda.synchronize()
+    xch = shard.DeviceExchange(N, G, dist, torch.device("cuda", local), spec.n_streams > 1,
+                               cpu_collectives=backend == "gloo") if G > 1 else None
+    pending = {}
 
     def step(i):
+        """One batch through the hot path.  N>1: batch i was exchanged by key owner while step i-1
+        ran (one RCCL all-to-all of packed records, overlapped with the engine); the exchange of
+        batch i+1 is started here, before this batch's push."""
         ts, key, price, stream = batches[i]
         if G > 1:
-            cols = {"ts": ts, "key": key, "price": price}
-            if stream is not None:
-                cols["stream"] = stream
-            got = shard.exchange(cols, "key", G, dist)
-            ts, price, stream = got["ts"], got["price"], got.get("stream")
-            key = shard.local_key(got["key"], G).to(torch.int32)
+            p = pending.pop(i) if i in pending else xch.start(ts, key, price, stream)
+            ts, key, price, stream = xch.finish(p)
             torch.cuda.current_stream().synchronize()  # the engine runs on its own HIP stream
+            if i + 1 < len(batches):
+                pending[i + 1] = xch.start(*batches[i + 1])
         n = ts.numel()
         # one pointer per program column (cq.columns: (stream, attr, type)); every stream's
         # predicate attribute is the synthetic price column
         ncol = max(1, len(cq.columns))
         colp = (ctypes.c_void_p * ncol)(*([price.data_ptr()] * ncol))
-        # one input stream: the stream column is NULL (= every event on stream 0)
         b = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), stream.data_ptr() if stream is not None else None,
                             ctypes.cast(colp, ctypes.c_void_p), None)
         mt = native.ShpMatches()
@@ -157,10 +169,10 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        cnt = torch.tensor([ev_local, m_local], dtype=torch.int64, device="cuda")
+        cnt = torch.tensor([ev_local, m_local], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(cnt)
         ev_total, m_total = int(cnt[0]), int(cnt[1])
     else:
@@ -201,7 +213,8 @@ def main():
                 "workload": WORKLOADS.get(str(cfg_id), f"C{cfg_id}") + f"; {K} keys",
                 "events_per_gpu_per_step": N,
                 "keys": K,
-                "parallelism": f"key-sharded x{G}" + (" (RCCL all-to-all by key owner)" if G > 1 else ""),
+                "parallelism": f"key-sharded x{G}" + (" (one RCCL all-to-all of packed records per batch, "
+                                                      "overlapped with the previous batch)" if G > 1 else ""),
                 "engine_path": PATHS.get(eng.path, str(eng.path)),
                 "matches_per_s": m_total / elapsed,
                 "matches_per_step_gpu0": m_per_launch,

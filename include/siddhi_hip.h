@@ -116,6 +116,15 @@ int shp_engine_path(const shp_engine* e);
  * siddhi_amd/synth.py). Any output pointer may be NULL. hip_stream: a hipStream_t or NULL. */
 int shp_synth_fill(int config, int64_t start, int64_t count, int64_t keys, int n_streams, int dense,
                    int64_t* ts, int32_t* key, float* price, int64_t* volume, int32_t* stream, void* hip_stream);
+/* Multi-GPU exchange utilities (not part of the reference boundary; siddhi_amd/shard.py):
+ * stable split of a device batch by destination rank key % G into packed 16-byte records
+ * {ts, stream << 24 | key / G, value} grouped by rank (counts[g] on the host), and the unpack of
+ * received records into the engine's SoA columns. */
+int64_t shp_shard_workspace_bytes(int64_t n, int G);
+int shp_shard_partition(int64_t n, const int64_t* ts, const int32_t* key, const void* value, const int32_t* stream,
+                        int G, void* out, int64_t* counts, void* ws, void* hip_stream);
+int shp_shard_unpack(int64_t m, const void* in, int64_t* ts, int32_t* key, void* value, int32_t* stream,
+                     void* hip_stream);
 /* Bench/test utilities: device memory without a second HIP runtime in the process. */
 void* shp_dev_alloc(int64_t bytes);
 int shp_dev_free(void* p);

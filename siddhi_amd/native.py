@@ -23,7 +23,8 @@ SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACIT
 SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches",
            "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
-           "shp_dev_to_host", "shp_snapshot", "shp_restore"]
+           "shp_dev_to_host", "shp_snapshot", "shp_restore", "shp_shard_workspace_bytes",
+           "shp_shard_partition", "shp_shard_unpack"]
 
 
 class ShpConfig(ctypes.Structure):
@@ -80,6 +81,11 @@ def lib():
         L.shp_dev_to_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.shp_snapshot.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
         L.shp_restore.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        L.shp_shard_workspace_bytes.restype = ctypes.c_int64
+        L.shp_shard_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int]
+        L.shp_shard_partition.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int] + \
+            [ctypes.c_void_p] * 4
+        L.shp_shard_unpack.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 6
         _lib = L
     return _lib
 

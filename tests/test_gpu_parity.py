@@ -170,3 +170,36 @@ def test_restore_rejects_other_query():
         b.restore(a.snapshot())
     with pytest.raises(ShpError, match="SHP_ERR_ARG"):
         b.restore(b"garbage")
+
+
+def test_shard_partition_and_unpack_are_stable():
+    """shp_shard_partition groups by key % G keeping arrival order; unpack restores the columns."""
+    import ctypes
+
+    import torch
+    from siddhi_amd import native
+    L = native.lib()
+    n, G = 300_001, 4
+    g = small_stream(4, n, 1000)
+    dev = torch.device("cuda", 0)
+    ts = torch.from_numpy(g["ts"]).to(dev)
+    key = torch.from_numpy(g["key"]).to(dev)
+    price = torch.from_numpy(g["price"]).to(dev)
+    stream = torch.from_numpy(g["stream"]).to(dev)
+    out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    ws = torch.empty(int(L.shp_shard_workspace_bytes(n, G)), dtype=torch.uint8, device=dev)
+    counts = (ctypes.c_int64 * G)()
+    assert L.shp_shard_partition(n, ts.data_ptr(), key.data_ptr(), price.data_ptr(), stream.data_ptr(), G,
+                                 out.data_ptr(), counts, ws.data_ptr(), None) == 0
+    o_ts, o_key = torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int32, device=dev)
+    o_p, o_s = torch.empty(n, dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.int32, device=dev)
+    assert L.shp_shard_unpack(n, out.data_ptr(), o_ts.data_ptr(), o_key.data_ptr(), o_p.data_ptr(),
+                              o_s.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    dst = g["key"] % G
+    order = np.argsort(dst, kind="stable")
+    assert list(counts) == [int((dst == r).sum()) for r in range(G)]
+    assert (o_ts.cpu().numpy() == g["ts"][order]).all()
+    assert (o_key.cpu().numpy() == (g["key"] // G)[order]).all()
+    assert (o_s.cpu().numpy() == g["stream"][order]).all()
+    assert (o_p.cpu().numpy().view(np.uint32) == g["price"][order].view(np.uint32)).all()
