@@ -348,7 +348,7 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
     __syncthreads();
     SwRec rec[SWP_SUB];
     uint32_t own[SWP_SUB];
-    uint32_t rk[SWP_SUB];
+    uint32_t rk[SWP_SUB], pc[SWP_SUB], ld[SWP_SUB];
     // all loads of the round first (independent, so they are in flight together), then the
     // key-map lookups, then the ranking
     int32_t kk[SWP_SUB];
@@ -381,13 +381,20 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
         if (!sw_rel_ok(rel)) e |= SWE_RANGE;
         rec[s].kt = sw_kt(km[s] >> 16, rel, (kk[s] & 0x40000000) ? SW_NULL : 0ull);
       }
-      uint64_t peers = sw_match_peers(o, D.own_bits, valid);
-      uint32_t before = 0;
-      if (valid) before = wcnt[w][o];
-      rk[s] = before + (uint32_t)__popcll(peers & lt);
-      if (valid && (peers & lt) == 0) wcnt[w][o] = before + (uint32_t)__popcll(peers);
+      const uint64_t peers = sw_match_peers(o, D.own_bits, valid);
+      rk[s] = (uint32_t)__popcll(peers & lt);
       own[s] = valid ? o : 0xffffffffu;
+      pc[s] = (valid && (peers & lt) == 0) ? (uint32_t)__popcll(peers) : 0u;  // leader: group size
+      ld[s] = peers ? (uint32_t)__ffsll((unsigned long long)peers) - 1u : 0u;    // leader lane
     }
+    // per-wave running counts: the leaders' LDS adds of all sub-rounds issue back to back (LDS
+    // keeps a wave's operations in order, so sub-round s sees s-1's add), one wait, then each
+    // lane takes its leader's old count
+    uint32_t old[SWP_SUB];
+#pragma unroll
+    for (int s = 0; s < SWP_SUB; s++) old[s] = pc[s] ? atomicAdd(&wcnt[w][own[s]], pc[s]) : 0u;
+#pragma unroll
+    for (int s = 0; s < SWP_SUB; s++) rk[s] += __shfl(old[s], (int)ld[s], 64);
     __syncthreads();
     for (int b = threadIdx.x; b < D.nown; b += SW_THREADS) {
       uint32_t g = grun[b];
