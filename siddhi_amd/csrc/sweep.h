@@ -44,6 +44,7 @@ constexpr int SW_THREADS = 256;
 constexpr int SW_WAVES = SW_THREADS / 64;
 constexpr int SW_LK = 255;          // local keys per owner; bin 255 = "no item"
 constexpr int SW_MAXOWN = 2048;     // owners (partition bins)
+constexpr int SW_LKTAB = 65536;     // scatter LDS bound: its counters + the key -> local key table
 // partition
 constexpr int SWP_ROUND = 2048;
 constexpr int SWP_SEG = SWP_ROUND / SW_WAVES;
@@ -123,7 +124,8 @@ struct SweepDev {
   int32_t lk_bits;       // bits of the largest local key id
   int32_t maybe_null;    // some pushed batch carried a null bitmap (sticky; the carry may hold nulls)
   int64_t st_len;
-  const uint32_t* kmap;  // key -> owner | local key << 16
+  const uint8_t* lk8;    // key -> local key id within its owner (the owner is sw_owner(key))
+  int32_t lk_lds;        // scatter stages lk8 in LDS (max_keys <= SW_LKTAB)
   uint32_t* cnt;         // nown * nst + 1: counts, scanned into off
   uint32_t* off;
   SwRec* recs;           // batch capacity
@@ -247,6 +249,11 @@ __device__ __forceinline__ void sw_conv(uint32_t v, bool isfloat, double& f, dou
   }
 }
 
+// key -> owner: Fibonacci hashing (build_map uses the same function, so owners need no table)
+__host__ __device__ __forceinline__ uint32_t sw_owner(uint32_t k, int bits) {
+  return bits == 0 ? 0u : (k * 2654435769u) >> (32 - bits);
+}
+
 __device__ __forceinline__ uint64_t sw_match_peers(uint32_t bin, int bits, bool valid) {
   uint64_t peers = __ballot(valid);
   for (int b = 0; b < bits; b++) {
@@ -294,7 +301,7 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B
   __syncthreads();
   const int64_t lo = (int64_t)st * D.st_len, hi = min(B.n, lo + D.st_len);
   int e = 0;
-  constexpr int U = 8;  // loads of U events in flight per thread before the dependent key-map reads
+  constexpr int U = 8;  // loads of U events in flight per thread before the LDS adds
   for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (int64_t)SW_THREADS * U) {
     int32_t kk[U];
 #pragma unroll
@@ -315,12 +322,9 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B
       }
       kk[u] = k;
     }
-    uint32_t km[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) km[u] = kk[u] >= 0 ? D.kmap[kk[u]] : 0u;
 #pragma unroll
     for (int u = 0; u < U; u++)
-      if (kk[u] >= 0) atomicAdd(&h[km[u] & 0xffffu], 1u);
+      if (kk[u] >= 0) atomicAdd(&h[sw_owner((uint32_t)kk[u], D.own_bits)], 1u);
   }
   if (e) atomicOr(err, e);
   __syncthreads();
@@ -331,12 +335,22 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B
 // ------------------------------------------------------------------ pass 2: stable scatter by owner
 __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView B, const int32_t* __restrict__ key,
                                                            int* err) {
-  __shared__ uint32_t wcnt[SW_WAVES][SW_MAXOWN];  // per-wave counts, then write cursors
-  __shared__ uint32_t grun[SW_MAXOWN];
+  // dynamic LDS: per-wave counts (then write cursors) [SW_WAVES][nown], running owner offsets
+  // [nown], and (lk_lds) the key -> local key table
+  extern __shared__ uint32_t sw_dyn[];
+  const int nown = D.nown;
+  uint32_t* grun = sw_dyn + SW_WAVES * nown;
+  uint8_t* lkt = (uint8_t*)(grun + nown);
   const int st = blockIdx.x;
   const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  uint32_t* wcw = sw_dyn + w * nown;
   const uint64_t lt = sw_lanemask_lt();
-  for (int b = threadIdx.x; b < D.nown; b += SW_THREADS) grun[b] = D.off[(int64_t)b * D.nst + st];
+  for (int b = threadIdx.x; b < nown; b += SW_THREADS) grun[b] = D.off[(int64_t)b * D.nst + st];
+  if (D.lk_lds) {
+    const uint32_t* src = (const uint32_t*)D.lk8;
+    for (int b = threadIdx.x; b < (D.maxkeys + 3) / 4; b += SW_THREADS) ((uint32_t*)lkt)[b] = src[b];
+  }
+  const uint8_t* lkq = D.lk_lds ? (const uint8_t*)lkt : D.lk8;
   const int64_t lo = (int64_t)st * D.st_len, hi = min(B.n, lo + D.st_len);
   const int64_t base = B.n > 0 ? B.ts[0] : 0;
   const uint32_t* vcol = (const uint32_t*)B.cols[0];
@@ -344,7 +358,7 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
   int e = 0;
   int64_t tmax = INT64_MIN;
   for (int64_t r0 = lo; r0 < hi; r0 += SWP_ROUND) {
-    for (int b = lane; b < D.nown; b += 64) wcnt[w][b] = 0;
+    for (int b = lane; b < nown; b += 64) wcw[b] = 0;
     __syncthreads();
     SwRec rec[SWP_SUB];
     uint32_t own[SWP_SUB];
@@ -367,19 +381,19 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
       }
       kk[s] = k;
     }
-    uint32_t km[SWP_SUB];
+    uint32_t lk[SWP_SUB];
 #pragma unroll
-    for (int s = 0; s < SWP_SUB; s++) km[s] = kk[s] >= 0 ? D.kmap[kk[s] & 0x3fffffff] : 0u;
+    for (int s = 0; s < SWP_SUB; s++) lk[s] = kk[s] >= 0 ? lkq[kk[s] & 0x3fffffff] : 0u;
 #pragma unroll
     for (int s = 0; s < SWP_SUB; s++) {
       const bool valid = kk[s] >= 0;
-      const uint32_t o = valid ? km[s] & 0xffffu : 0u;
+      const uint32_t o = valid ? sw_owner((uint32_t)(kk[s] & 0x3fffffff), D.own_bits) : 0u;
       if (valid) {
         const int64_t t = (int64_t)rec[s].kt;
         tmax = max(tmax, t);
         const int64_t rel = t - base;
         if (!sw_rel_ok(rel)) e |= SWE_RANGE;
-        rec[s].kt = sw_kt(km[s] >> 16, rel, (kk[s] & 0x40000000) ? SW_NULL : 0ull);
+        rec[s].kt = sw_kt(lk[s], rel, (kk[s] & 0x40000000) ? SW_NULL : 0ull);
       }
       const uint64_t peers = sw_match_peers(o, D.own_bits, valid);
       rk[s] = (uint32_t)__popcll(peers & lt);
@@ -392,16 +406,16 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
     // lane takes its leader's old count
     uint32_t old[SWP_SUB];
 #pragma unroll
-    for (int s = 0; s < SWP_SUB; s++) old[s] = pc[s] ? atomicAdd(&wcnt[w][own[s]], pc[s]) : 0u;
+    for (int s = 0; s < SWP_SUB; s++) old[s] = pc[s] ? atomicAdd(&wcw[own[s]], pc[s]) : 0u;
 #pragma unroll
     for (int s = 0; s < SWP_SUB; s++) rk[s] += __shfl(old[s], (int)ld[s], 64);
     __syncthreads();
-    for (int b = threadIdx.x; b < D.nown; b += SW_THREADS) {
+    for (int b = threadIdx.x; b < nown; b += SW_THREADS) {
       uint32_t g = grun[b];
 #pragma unroll
       for (int ww = 0; ww < SW_WAVES; ww++) {
-        uint32_t c = wcnt[ww][b];
-        wcnt[ww][b] = g;
+        uint32_t c = sw_dyn[ww * nown + b];
+        sw_dyn[ww * nown + b] = g;
         g += c;
       }
       grun[b] = g;
@@ -409,7 +423,7 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < SWP_SUB; s++)
-      if (own[s] != 0xffffffffu) D.recs[wcnt[w][own[s]] + rk[s]] = rec[s];
+      if (own[s] != 0xffffffffu) D.recs[wcw[own[s]] + rk[s]] = rec[s];
     __syncthreads();
   }
   if (e) atomicOr(err, e);
@@ -1041,7 +1055,7 @@ struct SweepState {
       for (int32_t k = 0; k < max_keys; k++) {
         // Fibonacci hashing: consecutive ids, and any arithmetic progression of ids (the keys
         // one rank of a key-sharded job sees), spread evenly over the owners
-        uint32_t o = bits == 0 ? 0u : ((uint32_t)k * 2654435769u) >> (32 - bits);
+        uint32_t o = sw_owner((uint32_t)k, bits);
         int32_t lk = nloc[o]++;
         mx = std::max(mx, lk + 1);
         kmap[k] = o | ((uint32_t)lk << 16);
@@ -1087,11 +1101,20 @@ struct SweepState {
     }
     nst_max = (int32_t)std::max<int64_t>(1, (cap + st_len - 1) / st_len);
     D.st_len = st_len;
-    uint32_t* km = nullptr;
-    al(km, max_keys);
-    if (hipMemcpy(km, kmap.data(), (size_t)max_keys * 4, hipMemcpyHostToDevice) != hipSuccess)
-      throw std::runtime_error("hipMemcpy failed (sweep key map)");
-    D.kmap = km;
+    {
+      std::vector<uint8_t> l8((size_t)(max_keys + 3) / 4 * 4, 0);
+      for (int32_t k = 0; k < max_keys; k++) {
+        if ((kmap[k] & 0xffffu) != sw_owner((uint32_t)k, D.own_bits))
+          throw std::runtime_error("sweep: key map disagrees with sw_owner");
+        l8[k] = (uint8_t)(kmap[k] >> 16);
+      }
+      uint8_t* lk = nullptr;
+      al(lk, (int64_t)l8.size());
+      if (hipMemcpy(lk, l8.data(), l8.size(), hipMemcpyHostToDevice) != hipSuccess)
+        throw std::runtime_error("hipMemcpy failed (sweep key map)");
+      D.lk8 = lk;
+      D.lk_lds = (int64_t)(SW_WAVES + 1) * nown * 4 + (int64_t)l8.size() <= SW_LKTAB;
+    }
     int64_t nc = (int64_t)nown * nst_max + 1;
     al(D.cnt, nc);
     al(D.off, nc);
@@ -1112,7 +1135,7 @@ struct SweepState {
   }
 
   void release() {
-    void* ps[] = {(void*)D.kmap, D.cnt, D.off, D.recs, D.c_n, D.c_ts, D.c_seq, D.c_v, D.c_lk, D.c_null,
+    void* ps[] = {(void*)D.lk8, D.cnt, D.off, D.recs, D.c_n, D.c_ts, D.c_seq, D.c_v, D.c_lk, D.c_null,
                   D.lastts, D.tsmax, tmp};
     for (void* p : ps)
       if (p) (void)hipFree(p);
@@ -1132,7 +1155,8 @@ struct SweepState {
     size_t tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.cnt, D.off, 0u, nc, rocprim::plus<uint32_t>(), s);
     kt.mark("sw_scatter", s);
-    k_sw_scatter<<<D.nst, SW_THREADS, 0, s>>>(D, B, key, err);
+    const size_t lds = (size_t)(SW_WAVES + 1) * D.nown * 4 + (D.lk_lds ? (size_t)(D.maxkeys + 3) / 4 * 4 : 0);
+    k_sw_scatter<<<D.nst, SW_THREADS, lds, s>>>(D, B, key, err);
     kt.mark("sw_solve", s);
     switch ((D.f1.n * 3 + D.f2.n) * 3 + ct) {
 #define SW_CASE(a, b, c) \

@@ -92,6 +92,20 @@ def test_c2_10k_keys_fast_path_vs_oracle():
     assert sum(len(v) for v in a.values()) > 100_000
 
 
+@pytest.mark.parametrize("keys", [300, 9_000, 200_000])
+def test_sweep_key_counts_vs_oracle(keys):
+    """Sweep at key counts that change its owner layout: few owners, the key -> local key table
+    in LDS (scatter), and the table read from global memory (too many keys for LDS)."""
+    cq = program_for(2)
+    g = small_stream(2, 600_000, keys)
+    a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    eng = hip(3, max_keys=keys, max_batch=1 << 20)(cq.program_json(), 0)
+    assert eng.path == 2
+    b = per_key(run(eng, cq, g, 250_001))
+    assert compare(a, b) is None
+    assert sum(len(v) for v in a.values()) > 1000
+
+
 def test_device_generator_matches_numpy():
     """shp_synth_fill (HIP) is bit-identical to siddhi_amd.synth (numpy PCG32)."""
     from siddhi_amd import native, synth
