@@ -301,6 +301,35 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B
   __syncthreads();
   const int64_t lo = (int64_t)st * D.st_len, hi = min(B.n, lo + D.st_len);
   int e = 0;
+  if (!B.stream && B.partitioned && ((uintptr_t)key & 15) == 0 && (lo & 3) == 0) {
+    // one stream, aligned keys: 16-byte loads, 4 in flight per thread
+    constexpr int U = 4;
+    const int4* k4 = (const int4*)key;
+    const int64_t q0 = lo >> 2, q1 = hi >> 2;
+    for (int64_t i0 = q0 + threadIdx.x; i0 < q1; i0 += (int64_t)SW_THREADS * U) {
+      int4 kv[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t i = i0 + (int64_t)u * SW_THREADS;
+        kv[u] = i < q1 ? k4[i] : make_int4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (i0 + (int64_t)u * SW_THREADS >= q1) continue;
+        const int32_t kq[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          if (kq[c] < 0 || kq[c] >= D.maxkeys) e |= SWE_KEYS;
+          else if (D.fstream == 0) atomicAdd(&h[sw_owner((uint32_t)kq[c], D.own_bits)], 1u);
+        }
+      }
+    }
+    for (int64_t i = q1 * 4 + threadIdx.x; i < hi; i += SW_THREADS) {
+      const int32_t k = key[i];
+      if (k < 0 || k >= D.maxkeys) e |= SWE_KEYS;
+      else if (D.fstream == 0) atomicAdd(&h[sw_owner((uint32_t)k, D.own_bits)], 1u);
+    }
+  } else {
   constexpr int U = 8;  // loads of U events in flight per thread before the LDS adds
   for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (int64_t)SW_THREADS * U) {
     int32_t kk[U];
@@ -325,6 +354,7 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B
 #pragma unroll
     for (int u = 0; u < U; u++)
       if (kk[u] >= 0) atomicAdd(&h[sw_owner((uint32_t)kk[u], D.own_bits)], 1u);
+  }
   }
   if (e) atomicOr(err, e);
   __syncthreads();
