@@ -478,6 +478,7 @@ constexpr int SWS_THREADS = 512;
 constexpr int SWS_WAVES = SWS_THREADS / 64;
 constexpr int SWS_RPT = (SWS_CHUNK + SWS_THREADS - 1) / SWS_THREADS;  // prefetch slots per thread
 constexpr int SWS_PER = (SWS_EMAX + SWS_THREADS - 1) / SWS_THREADS;
+constexpr int SWS_WLCAP = 64 * SWS_PER;  // a wave's positions
 constexpr uint32_t SW_LKF_CAR = 1u << 8, SW_LKF_NULL = 1u << 9, SW_LKF_NONE = 0xFFu;
 constexpr int32_t SW_TS_FLOOR = -(1 << 30) - 1;  // carried ts below this are clamped (all expired)
 constexpr int64_t SW_TS_SPAN = 1ll << 29;        // |event ts - chunk base| bound
@@ -530,8 +531,7 @@ struct SwSolveSmem {
   int64_t lastts[SW_LK];              // batch-relative ts of the key's latest event (INT64_MIN unseen)
   uint32_t wtot[SWS_WAVES];
   unsigned long long gbase;
-  uint16_t wl[SWS_EMAX];              // probe worklist (unresolved candidates)
-  uint32_t wln;
+  uint16_t wl[SWS_WAVES * SWS_WLCAP];  // per-wave probe worklists (unresolved candidates)
 };
 
 template <int NW>
@@ -695,8 +695,8 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       S.tv[E + tid] = make_int2(0, 0);
       S.lkf[E + tid] = (uint16_t)SW_LKF_NONE;
     }
+    if (tid < 8) SWM(E + tid) = -3;
     for (int i = tid; i <= SWS_EMAX / 2; i += SWS_THREADS) S.cnt2[i] = 0;
-    if (tid == 0) S.wln = 0;
     // prefetch the next chunk while this one is solved
     {
       const int64_t nb = cb + SWS_CHUNK;
@@ -715,144 +715,125 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     //    unresolved go to a worklist; each later round gives every worklist entry SW_P2 more
     //    events, so lanes stay busy on the few long scans instead of idling in divergent loops.
     for (int i = tid; i < SWS_WAVES * (SW_LK + 1); i += SWS_THREADS) (&S.wc[0][0])[i] = 0;  // next rank
+    uint16_t* wlw = S.wl + w * SWS_WLCAP;  // this wave's worklist
+    uint32_t nwl = 0;                      // wave-uniform (ballot counts)
     for (int k = 0; k < SWS_PER; k++) {
+      if ((int)(w * 64) + k * SWS_THREADS >= E) break;  // wave-uniform
       const int p = (int)tid + k * SWS_THREADS;
-      if (p >= E) break;
-      const uint32_t f = S.lkf[p];
-      const int2 a = S.tv[p];
-      const bool car = (f & SW_LKF_CAR) != 0;
-      const bool an = vnull || (f & SW_LKF_NULL) != 0;
-      double af = 0, ai = 0;
-      bool cand;
-      if constexpr (CT == 0) {
-        sw_conv((uint32_t)a.y, vflt, af, ai);
-        cand = car || sw_pred<NT1>(f1, af, ai, an, 0.0, 0.0, true);
-      } else {
-        cand = car || sw_open<NT1, CT>(f1, (uint32_t)a.y, an);
-      }
-      const uint32_t lk = f & 0xFFu;
-      const int end = (int)S.binoff[lk + 1];
-      const int fe = (int)S.fe[lk];
-      const int q0 = max(p + 1, fe);  // carried candidates are not events
-      if (!car) {  // per-key timestamp order: the next event, and the key's last ts for its first
-        if (p + 1 < end && S.tv[p + 1].x < a.x) e |= SWE_MONO;
-        if (p == fe) {
-          const int64_t prev = S.lastts[lk];
-          if (prev != INT64_MIN && tb + a.x < prev) e |= SWE_MONO;
+      int res = -3;
+      if (p < E) {
+        const uint32_t f = S.lkf[p];
+        const int2 a = S.tv[p];
+        const bool car = (f & SW_LKF_CAR) != 0;
+        const bool an = vnull || (f & SW_LKF_NULL) != 0;
+        double af = 0, ai = 0;
+        bool cand;
+        if constexpr (CT == 0) {
+          sw_conv((uint32_t)a.y, vflt, af, ai);
+          cand = car || sw_pred<NT1>(f1, af, ai, an, 0.0, 0.0, true);
+        } else {
+          cand = car || sw_open<NT1, CT>(f1, (uint32_t)a.y, an);
         }
+        const uint32_t lk = f & 0xFFu;
+        const int end = (int)S.binoff[lk + 1];
+        const int fe = (int)S.fe[lk];
+        const int q0 = max(p + 1, fe);  // carried candidates are not events
+        if (!car) {  // per-key timestamp order: the next event, and the key's last ts for its first
+          if (p + 1 < end && S.tv[p + 1].x < a.x) e |= SWE_MONO;
+          if (p == fe) {
+            const int64_t prev = S.lastts[lk];
+            if (prev != INT64_MIN && tb + a.x < prev) e |= SWE_MONO;
+          }
+        }
+        const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
+        res = cand ? -4 : -3;  // -4: unresolved
+        res = sw_probe<NT2, CT, SW_P1>(S.tv, S.lkf, q0, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, res);
       }
-      const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
-      int res = cand ? -4 : -3;  // -4: unresolved
-      res = sw_probe<NT2, CT, SW_P1>(S.tv, S.lkf, q0, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, res);
-      if (res == -4) {
-        const uint32_t i = atomicAdd(&S.wln, 1u);
-        S.wl[i] = (uint16_t)p;
-      } else {
+      const bool unres = res == -4;
+      const uint64_t um = __ballot(unres);
+      if (unres) {
+        wlw[nwl + (uint32_t)__popcll(um & lt)] = (uint16_t)p;
+      } else if (p < E) {
         SWM(p) = (int16_t)res;
         if (res >= 0) atomicAdd(&S.cnt2[res >> 1], 1u << ((res & 1) * 16));
       }
+      nwl += (uint32_t)__popcll(um);
     }
-    __syncthreads();
-    for (int round = 0;; round++) {
-      const uint32_t nw = S.wln;
-      if (nw == 0) break;  // uniform: every thread read the same count after the barrier
-      uint32_t item[SWS_PER];
-#pragma unroll
-      for (int k = 0; k < SWS_PER; k++) {
-        const uint32_t i = tid + (uint32_t)k * SWS_THREADS;
-        item[k] = i < nw ? (uint32_t)S.wl[i] : 0xffffffffu;
-      }
-      __syncthreads();
-      if (tid == 0) S.wln = 0;
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < SWS_PER; k++) {
-        if (item[k] == 0xffffffffu) continue;
-        const int p = (int)item[k];
-        const uint32_t f = S.lkf[p];
-        const int2 a = S.tv[p];
-        const bool an = vnull || (f & SW_LKF_NULL) != 0;
-        double af = 0, ai = 0;
-        if constexpr (CT == 0) sw_conv((uint32_t)a.y, vflt, af, ai);
-        const uint32_t lk = f & 0xFFu;
-        const int end = (int)S.binoff[lk + 1];
-        const int qn = max(p + 1, (int)S.fe[lk]) + SW_P1 + round * SW_P2;
-        const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
-        int res = sw_probe<NT2, CT, SW_P2>(S.tv, S.lkf, qn, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, -4);
-        if (res == -4 && qn + SW_P2 >= end) res = -2;  // key run exhausted: still open
-        if (res == -4) {
-          const uint32_t i = atomicAdd(&S.wln, 1u);
-          S.wl[i] = (uint16_t)p;
-        } else {
+    // Later rounds, per wave (no block barrier): every worklist entry gets SW_P2 more events;
+    // still-unresolved entries are compacted in place (an entry moves only to a lower index,
+    // already read: the wave's LDS operations complete in order)
+    for (int round = 0; nwl > 0; round++) {
+      uint32_t nn = 0;
+      for (uint32_t b0 = 0; b0 < nwl; b0 += 64) {
+        const uint32_t idx = b0 + lane;
+        int p = 0, res = -3;
+        if (idx < nwl) {
+          p = (int)wlw[idx];
+          const uint32_t f = S.lkf[p];
+          const int2 a = S.tv[p];
+          const bool an = vnull || (f & SW_LKF_NULL) != 0;
+          double af = 0, ai = 0;
+          if constexpr (CT == 0) sw_conv((uint32_t)a.y, vflt, af, ai);
+          const uint32_t lk = f & 0xFFu;
+          const int end = (int)S.binoff[lk + 1];
+          const int qn = max(p + 1, (int)S.fe[lk]) + SW_P1 + round * SW_P2;
+          const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
+          res = sw_probe<NT2, CT, SW_P2>(S.tv, S.lkf, qn, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, -4);
+          if (res == -4 && qn + SW_P2 >= end) res = -2;  // key run exhausted: still open
+        }
+        const bool unres = res == -4;
+        const uint64_t um = __ballot(unres);
+        if (unres) {
+          wlw[nn + (uint32_t)__popcll(um & lt)] = (uint16_t)p;
+        } else if (idx < nwl) {
           SWM(p) = (int16_t)res;
           if (res >= 0) atomicAdd(&S.cnt2[res >> 1], 1u << ((res & 1) * 16));
         }
+        nn += (uint32_t)__popcll(um);
       }
-      __syncthreads();
+      nwl = nn;
+#ifdef SHP_SW_STAMPS
+      if (lane == 0) {
+        dbg_steps += nwl;
+        dbg_cands++;
+      }
+#endif
     }
-    if (tid < 8) SWM(E + tid) = -3;
     __syncthreads();
     SW_STAMP(1);
-    // 4. closes per event (counted by the probe) -> exclusive output offsets (16-bit, in place of
-    //    the counts), then every matched candidate writes its own pair: its slot among the
-    //    candidates of its closing event q is fixed by how many later candidates q also closed
+    // 4. one block scan gives both the output offsets (closes per closing event, counted by the
+    //    probe; 16-bit, in place of the counts) and the carry slots of still-open candidates
+    //    (packed: closes << 16 | opens; both totals are at most E)
     uint16_t* off16 = reinterpret_cast<uint16_t*>(S.cnt2);
-    uint32_t cq[SWS_PER], tot = 0;
-#pragma unroll
-    for (int k = 0; k < SWS_PER; k++) {
-      const int q = (int)tid * SWS_PER + k;
-      cq[k] = q < E ? off16[q] : 0u;
-      tot += cq[k];
-    }
-    for (int i = tid; i <= SW_LK; i += SWS_THREADS) S.ncar[i] = 0;  // recounted by the carry step
-    uint32_t total;
-    uint32_t off = sw_block_scan_n<SWS_WAVES>(tot, S.wtot, total);
-#pragma unroll
-    for (int k = 0; k < SWS_PER; k++) {
-      const int q = (int)tid * SWS_PER + k;
-      if (q < E) off16[q] = (uint16_t)off;
-      off += cq[k];
-    }
-    if (tid == 0) {
-      off16[E] = (uint16_t)total;
-      const unsigned long long g = total ? atomicAdd(O.count, (unsigned long long)total) : 0ull;
-      if (g + total > (unsigned long long)O.cap) e |= E_OUT;
-      S.gbase = g;
-    }
-    __syncthreads();
-    SW_STAMP(2);
+    const int nx = cur ^ 1;
     {
-      const unsigned long long gb = S.gbase;
-      for (int k = 0; k < SWS_PER; k++) {
-        const int p = (int)tid + k * SWS_THREADS;
-        if (p >= E) break;
-        const int q = SWM(p);
-        if (q < 0) continue;
-        const uint32_t c = (uint32_t)off16[q + 1] - off16[q];
-        uint32_t later = 0;
-#pragma unroll
-        for (int d = 1; d <= SW_PROBE; d++) later += (p + d < q && SWM(p + d) == q) ? 1u : 0u;
-        for (int p2 = p + SW_PROBE + 1; p2 < q; p2++) later += SWM(p2) == q ? 1u : 0u;
-        const uint32_t r = S.ref[p];
-        const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
-        const int64_t sq = B.seq0 + S.ref[q];
-        const uint64_t slot = gb + off16[q] + (c - 1 - later);
-        if (slot < (uint64_t)O.cap) *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
-      }
-    }
-    SW_STAMP(3);
-    SW_STAMP(4);
-    // 6. still-open candidates become the carry (sorted order = key, then i)
-    {
-      uint32_t open = 0;
+      uint32_t cq[SWS_PER], tot = 0, open = 0;
 #pragma unroll
       for (int k = 0; k < SWS_PER; k++) {
-        const int p = (int)tid * SWS_PER + k;
-        open += (p < E && SWM(p) == -2) ? 1u : 0u;
+        const int q = (int)tid * SWS_PER + k;
+        cq[k] = q < E ? off16[q] : 0u;
+        tot += cq[k];
+        open += (q < E && SWM(q) == -2) ? 1u : 0u;
       }
-      uint32_t ntot;
-      uint32_t pre = sw_block_scan_n<SWS_WAVES>(open, S.wtot, ntot);
-      const int nx = cur ^ 1;
+      for (int i = tid; i <= SW_LK; i += SWS_THREADS) S.ncar[i] = 0;  // recounted below
+      uint32_t total;
+      const uint32_t pk = sw_block_scan_n<SWS_WAVES>((tot << 16) | open, S.wtot, total);
+      uint32_t off = pk >> 16, pre = pk & 0xffffu;
+      const uint32_t ctot = total >> 16;
+      uint32_t ntot = total & 0xffffu;
+#pragma unroll
+      for (int k = 0; k < SWS_PER; k++) {
+        const int q = (int)tid * SWS_PER + k;
+        if (q < E) off16[q] = (uint16_t)off;
+        off += cq[k];
+      }
+      if (tid == 0) {
+        off16[E] = (uint16_t)ctot;
+        const unsigned long long g = ctot ? atomicAdd(O.count, (unsigned long long)ctot) : 0ull;
+        if (g + ctot > (unsigned long long)O.cap) e |= E_OUT;
+        S.gbase = g;
+      }
+      // 5. still-open candidates become the next carry (sorted order = key, then i)
 #pragma unroll
       for (int k = 0; k < SWS_PER; k++) {
         const int p = (int)tid * SWS_PER + k;
@@ -885,13 +866,40 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
         ntot = SWS_CCAP;
       }
       nc = (int)ntot;
-      cur = nx;
     }
     __syncthreads();
+    SW_STAMP(2);
+    // 6. every matched candidate writes its own pair: its slot among the candidates of its
+    //    closing event q is fixed by how many later candidates q also closed.  No barrier after
+    //    it: the next chunk's rank step touches only S.wc, and its first barrier comes before
+    //    anything this step reads is rewritten.
+    {
+      const unsigned long long gb = S.gbase;
+      for (int k = 0; k < SWS_PER; k++) {
+        const int p = (int)tid + k * SWS_THREADS;
+        if (p >= E) break;
+        const int q = SWM(p);
+        if (q < 0) continue;
+        const uint32_t c = (uint32_t)off16[q + 1] - off16[q];
+        uint32_t later = 0;
+#pragma unroll
+        for (int d = 1; d <= SW_PROBE; d++) later += (p + d < q && SWM(p + d) == q) ? 1u : 0u;
+        for (int p2 = p + SW_PROBE + 1; p2 < q; p2++) later += SWM(p2) == q ? 1u : 0u;
+        const uint32_t r = S.ref[p];
+        const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
+        const int64_t sq = B.seq0 + S.ref[q];
+        const uint64_t slot = gb + off16[q] + (c - 1 - later);
+        if (slot < (uint64_t)O.cap) *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
+      }
+    }
+    cur = nx;
+    SW_STAMP(3);
+    SW_STAMP(4);
     SW_STAMP(5);
     SW_STAMP(6);
     SW_STAMP(7);
   }
+  __syncthreads();
 #ifdef SHP_SW_STAMPS
   atomicAdd(&dbg_sum[0], dbg_steps);
   atomicAdd(&dbg_sum[1], dbg_cands);
@@ -1075,7 +1083,8 @@ struct SweepState {
   // host key map: key -> owner | local key << 16; false when keys cannot be spread under the caps
   static bool build_map(int32_t max_keys, int32_t& nown, std::vector<uint32_t>& kmap) {
     nown = 1;
-    while (nown < SW_MAXOWN && (int64_t)nown * 10 < max_keys) nown *= 2;
+    static const int kpo = getenv("SHP_SW_KPO") ? std::max(1, atoi(getenv("SHP_SW_KPO"))) : 10;  // diagnostics
+    while (nown < SW_MAXOWN && (int64_t)nown * kpo < max_keys) nown *= 2;
     for (;;) {
       std::vector<int32_t> nloc(nown, 0);
       kmap.assign(max_keys, 0);

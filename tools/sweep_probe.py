@@ -55,11 +55,11 @@ def main():
             cands = (raw[:, 7] & np.uint64(0xffffff)).astype(np.float64)
             chunks = (raw[:, 6] >> np.uint64(40)).astype(np.float64)
             ncs = (raw[:, 6] & np.uint64(0xffffffffff)).astype(np.float64)
-            print(f"  steps/cand={steps.sum() / max(1, cands.sum()):.2f} cands/owner={cands.mean():.0f} "
+            print(f"  worklist items/round={steps.sum() / max(1, cands.sum()):.2f} rounds/owner={cands.mean():.0f} "
                   f"chunks/owner={chunks.mean():.1f} mean carried/chunk={ncs.sum() / max(1, chunks.sum()):.1f}")
             st[:, 6:] = 0
             tot = st.sum(1)
-            names = ["gather+rank+place", "fwd scan", "count", "offsets", "emit", "mono", "carry", "stamp ovh"]
+            names = ["rank+place", "probe", "offsets+carry", "emit", "-", "-", "-", "-"]
             print(f"  owners={nown} cycles/owner mean={tot.mean():.3e} max={tot.max():.3e}")
             for k in range(6):
                 print(f"    {names[k]:<18} mean={st[:, k].mean():.3e} ({100 * st[:, k].sum() / tot.sum():.1f}%)")
