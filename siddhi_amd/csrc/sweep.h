@@ -193,6 +193,29 @@ __device__ __forceinline__ bool sw_cmp(int32_t mask, T A, T B) {
   const bool un = !(lt || eq || gt);
   return (lt & ((mask & 1) != 0)) | (eq & ((mask & 2) != 0)) | (gt & ((mask & 4) != 0)) | (un & ((mask & 8) != 0));
 }
+// The standard comparison masks as single compares (Java semantics: false on NaN, except !=).
+// OPC 0 is the generic mask form; the solve picks OPC once per launch (uniform branch).
+__host__ __device__ inline int sw_opclass(int32_t mask) {
+  switch (mask) {
+    case 1: return 1;   // <
+    case 2: return 2;   // ==
+    case 3: return 3;   // <=
+    case 4: return 4;   // >
+    case 6: return 5;   // >=
+    case 13: return 6;  // !=
+    default: return 0;
+  }
+}
+template <int OPC, class T>
+__device__ __forceinline__ bool sw_cmp_op(int32_t mask, T A, T B) {
+  if constexpr (OPC == 1) return A < B;
+  else if constexpr (OPC == 2) return A == B;
+  else if constexpr (OPC == 3) return A <= B;
+  else if constexpr (OPC == 4) return A > B;
+  else if constexpr (OPC == 5) return A >= B;
+  else if constexpr (OPC == 6) return !(A == B);
+  else return sw_cmp(mask, A, B);
+}
 template <int CT>
 __device__ __forceinline__ typename SwTy<CT>::T sw_val(uint32_t v, double f, double i, bool flt) {
   if constexpr (CT == 1) return __uint_as_float(v);
@@ -210,13 +233,13 @@ __device__ __forceinline__ SwCand<CT> sw_cand(const SwPred& p, uint32_t av, doub
   }
   return c;
 }
-template <int NT, int CT>
+template <int NT, int CT, int OPC = 0>
 __device__ __forceinline__ bool sw_close(const SwPred& p, const SwCand<CT>& c, uint32_t ev, double ef, double ei,
                                          bool en) {
   if constexpr (NT == 0) {
     return true;
   } else if constexpr (NT == 1) {
-    return !en & !c.bn[0] & sw_cmp(p.t[0].mask, sw_val<CT>(ev, ef, ei, p.t[0].flt), c.b[0]);
+    return !en & !c.bn[0] & sw_cmp_op<OPC>(p.t[0].mask, sw_val<CT>(ev, ef, ei, p.t[0].flt), c.b[0]);
   } else {
     const bool a = !en & !c.bn[0] & sw_cmp(p.t[0].mask, sw_val<CT>(ev, ef, ei, p.t[0].flt), c.b[0]);
     const bool b = !en & !c.bn[1] & sw_cmp(p.t[1].mask, sw_val<CT>(ev, ef, ei, p.t[1].flt), c.b[1]);
@@ -486,7 +509,7 @@ constexpr int64_t SW_TS_SPAN = 1ll << 29;        // |event ts - chunk base| boun
 // One straight-line batch of P probes for a candidate (ts a_ts, resolved values cbv) starting at
 // sorted position qb of its key run ending at `end`: -2 run ended (open), -1 expired, q closing
 // event, -4 unresolved.  `res` carries an earlier resolution through unchanged.
-template <int NT2, int CT, int P>
+template <int NT2, int CT, int P, int OPC>
 __device__ __forceinline__ int sw_probe(const int2* tv, const uint16_t* lkf, int qb, int end, int32_t a_ts, int32_t W,
                                         const SwPred& f2, const SwCand<CT>& cbv, bool vflt, bool vnull, bool maybe_null,
                                         int res) {
@@ -507,12 +530,24 @@ __device__ __forceinline__ int sw_probe(const int2* tv, const uint16_t* lkf, int
     if constexpr (CT == 0) sw_conv((uint32_t)b[d].y, vflt, ef, ei);
     const bool inrun = qb + d < end;
     const bool expired = b[d].x - a_ts > W;
-    const bool hit = sw_close<NT2, CT>(f2, cbv, (uint32_t)b[d].y, ef, ei, vnull || (bf[d] & SW_LKF_NULL) != 0);
+    const bool hit = sw_close<NT2, CT, OPC>(f2, cbv, (uint32_t)b[d].y, ef, ei, vnull || (bf[d] & SW_LKF_NULL) != 0);
     const int r = !inrun ? -2 : (expired ? -1 : (hit ? qb + d : -4));
     res = res == -4 ? r : res;
   }
   return res;
 }
+
+// probe call specialised on the f2 comparison (single-term f2 only; uniform branch)
+#define SW_PROBE_OPC(CALL, P, ARGS)                     \
+  switch (opc) {                                        \
+    case 1: CALL<NT2, CT, P, 1> ARGS; break;            \
+    case 2: CALL<NT2, CT, P, 2> ARGS; break;            \
+    case 3: CALL<NT2, CT, P, 3> ARGS; break;            \
+    case 4: CALL<NT2, CT, P, 4> ARGS; break;            \
+    case 5: CALL<NT2, CT, P, 5> ARGS; break;            \
+    case 6: CALL<NT2, CT, P, 6> ARGS; break;            \
+    default: CALL<NT2, CT, P, 0> ARGS; break;           \
+  }
 
 struct SwSolveSmem {
   int2 tv[SWS_EMAX + 2 * SW_PROBE];   // (ts - chunk base, value) by sorted position, then sentinels
@@ -573,6 +608,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
   const bool vflt = D.vtag == T_FLOAT;
   const bool maybe_null = D.maybe_null != 0;
   const int lkbits = D.lk_bits;
+  const int opc = NT2 == 1 ? sw_opclass(f2.t[0].mask) : 0;
   int e = 0;
   // carry and last ts from the previous push
   int nc = D.c_n[o];
@@ -747,7 +783,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
         }
         const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
         res = cand ? -4 : -3;  // -4: unresolved
-        res = sw_probe<NT2, CT, SW_P1>(S.tv, S.lkf, q0, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, res);
+        SW_PROBE_OPC(res = sw_probe, SW_P1, (S.tv, S.lkf, q0, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, res));
       }
       const bool unres = res == -4;
       const uint64_t um = __ballot(unres);
@@ -778,7 +814,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
           const int end = (int)S.binoff[lk + 1];
           const int qn = max(p + 1, (int)S.fe[lk]) + SW_P1 + round * SW_P2;
           const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
-          res = sw_probe<NT2, CT, SW_P2>(S.tv, S.lkf, qn, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, -4);
+          SW_PROBE_OPC(res = sw_probe, SW_P2, (S.tv, S.lkf, qn, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, -4));
           if (res == -4 && qn + SW_P2 >= end) res = -2;  // key run exhausted: still open
         }
         const bool unres = res == -4;
@@ -881,9 +917,14 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
         const int q = SWM(p);
         if (q < 0) continue;
         const uint32_t c = (uint32_t)off16[q + 1] - off16[q];
+        // the next SW_PROBE entries are read unconditionally (guard entries past E), so the
+        // reads issue back to back instead of one branch and wait per entry
+        int16_t mm[SW_PROBE];
+#pragma unroll
+        for (int d = 0; d < SW_PROBE; d++) mm[d] = SWM(p + 1 + d);
         uint32_t later = 0;
 #pragma unroll
-        for (int d = 1; d <= SW_PROBE; d++) later += (p + d < q && SWM(p + d) == q) ? 1u : 0u;
+        for (int d = 0; d < SW_PROBE; d++) later += ((p + 1 + d < q) & (mm[d] == q)) ? 1u : 0u;
         for (int p2 = p + SW_PROBE + 1; p2 < q; p2++) later += SWM(p2) == q ? 1u : 0u;
         const uint32_t r = S.ref[p];
         const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;

@@ -217,3 +217,43 @@ def test_shard_partition_and_unpack_are_stable():
     assert (o_key.cpu().numpy() == (g["key"] // G)[order]).all()
     assert (o_s.cpu().numpy() == g["stream"][order]).all()
     assert (o_p.cpu().numpy().view(np.uint32) == g["price"][order].view(np.uint32)).all()
+
+
+def _pred_stream(typ, n, keys, seed, nan_rate=0.02):
+    rng = np.random.default_rng(seed)
+    ts = np.cumsum(rng.integers(0, 2, n)).astype(np.int64) + 1_000
+    key = rng.integers(0, keys, n).astype(np.int32)
+    small = rng.integers(0, 10, n)
+    if typ == "float":
+        v = small.astype(np.float32) + np.where(rng.random(n) < 0.3, np.float32(0.5), np.float32(0))
+        v[rng.random(n) < nan_rate] = np.nan
+        v[rng.random(n) < 0.01] = -0.0
+    else:
+        v = (small - 2).astype(np.int32)
+    return ts, key, np.zeros(n, np.int32), v
+
+
+@pytest.mark.parametrize("typ", ["float", "int"])
+@pytest.mark.parametrize("op", ["<", "<=", ">", ">=", "==", "!="])
+@pytest.mark.parametrize("with_nulls", [False, True], ids=["dense", "nulls"])
+def test_sweep_comparison_grid_vs_oracle(op, typ, with_nulls):
+    """Every comparison of `e2.v OP e1.v` on the sweep (specialised compares), float with NaN and
+    -0.0, int, with and without null bitmaps, split batches."""
+    from siddhi_amd.query.compiler import compile_app
+    app = (f"define stream S (k string, v {typ}); partition with (k of S) begin "
+           f"@info(name='q') from every e1=S[v > 3] -> e2=S[v {op} e1.v] within 1 sec "
+           f"select e1.v as a, e2.v as b insert into Out; end;")
+    cq = compile_app(app)[1][0]
+    ts, key, st, v = _pred_stream(typ, 60_000, 300, seed=len(op) * 7 + (typ == "int") + 2 * with_nulls)
+    nul = (np.random.default_rng(5).random(len(ts)) < 0.03).astype(np.uint8) if with_nulls else None
+    outs = []
+    for eng in (OracleEngine(cq.program_json(), 0), hip(3, max_keys=300, max_batch=1 << 16)(cq.program_json(), 0)):
+        if hasattr(eng, "path"):
+            assert eng.path == 2
+        for lo in range(0, len(ts), 17_011):
+            hi = min(len(ts), lo + 17_011)
+            eng.push(ts[lo:hi], key[lo:hi], st[lo:hi], [v[lo:hi]], [None if nul is None else nul[lo:hi]])
+        outs.append(per_key(eng.fetch()))
+    a, b = outs
+    assert compare(a, b) is None, compare(a, b)
+    assert sum(len(x) for x in a.values()) > 100
