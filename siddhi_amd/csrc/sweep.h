@@ -76,6 +76,7 @@ constexpr uint64_t SW_TSBIAS = 1ull << 49;
 constexpr uint64_t SW_TSMASK = (1ull << 50) - 1;
 constexpr uint64_t SW_CARRIED = 1ull << 55;
 constexpr uint64_t SW_NULL = 1ull << 54;
+constexpr uint64_t SW_F1 = 1ull << 53;  // the event satisfies e1's filter (evaluated by the scatter)
 
 __device__ __forceinline__ uint32_t sw_lk(uint64_t kt) { return (uint32_t)(kt >> 56); }
 __device__ __forceinline__ int64_t sw_ts(uint64_t kt) { return (int64_t)(kt & SW_TSMASK) - (int64_t)SW_TSBIAS; }
@@ -408,6 +409,7 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
   const int64_t base = B.n > 0 ? B.ts[0] : 0;
   const uint32_t* vcol = (const uint32_t*)B.cols[0];
   const uint8_t* ncol = B.nulls[0];
+  const bool vnull = D.vtag == T_NULL, vflt = D.vtag == T_FLOAT;
   int e = 0;
   int64_t tmax = INT64_MIN;
   for (int64_t r0 = lo; r0 < hi; r0 += SWP_ROUND) {
@@ -446,7 +448,19 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
         tmax = max(tmax, t);
         const int64_t rel = t - base;
         if (!sw_rel_ok(rel)) e |= SWE_RANGE;
-        rec[s].kt = sw_kt(lk[s], rel, (kk[s] & 0x40000000) ? SW_NULL : 0ull);
+        const bool nl = (kk[s] & 0x40000000) != 0;
+        double af, ai;
+        sw_conv(rec[s].v, vflt, af, ai);
+        const bool an = vnull || nl;
+        bool c1 = true;  // e1's filter, generic (exact) double compares: this pass has ALU to spare
+        if (D.f1.n == 1) {
+          c1 = sw_term(D.f1.t[0], af, ai, an, 0.0, 0.0, true);
+        } else if (D.f1.n == 2) {
+          const bool x = sw_term(D.f1.t[0], af, ai, an, 0.0, 0.0, true);
+          const bool y = sw_term(D.f1.t[1], af, ai, an, 0.0, 0.0, true);
+          c1 = D.f1.combine ? (x || y) : (x && y);
+        }
+        rec[s].kt = sw_kt(lk[s], rel, (nl ? SW_NULL : 0ull) | (c1 ? SW_F1 : 0ull));
       }
       const uint64_t peers = sw_match_peers(o, D.own_bits, valid);
       rk[s] = (uint32_t)__popcll(peers & lt);
@@ -502,7 +516,7 @@ constexpr int SWS_WAVES = SWS_THREADS / 64;
 constexpr int SWS_RPT = (SWS_CHUNK + SWS_THREADS - 1) / SWS_THREADS;  // prefetch slots per thread
 constexpr int SWS_PER = (SWS_EMAX + SWS_THREADS - 1) / SWS_THREADS;
 constexpr int SWS_WLCAP = 64 * SWS_PER;  // a wave's positions
-constexpr uint32_t SW_LKF_CAR = 1u << 8, SW_LKF_NULL = 1u << 9, SW_LKF_NONE = 0xFFu;
+constexpr uint32_t SW_LKF_CAR = 1u << 8, SW_LKF_NULL = 1u << 9, SW_LKF_F1 = 1u << 10, SW_LKF_NONE = 0xFFu;
 constexpr int32_t SW_TS_FLOOR = -(1 << 30) - 1;  // carried ts below this are clamped (all expired)
 constexpr int64_t SW_TS_SPAN = 1ll << 29;        // |event ts - chunk base| bound
 
@@ -714,7 +728,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       const int64_t rel = sw_ts(pf[s].kt) - tb;
       if (rel >= SW_TS_SPAN || rel <= -SW_TS_SPAN) e |= SWE_RANGE;
       S.tv[p] = make_int2((int32_t)rel, (int32_t)pf[s].v);
-      S.lkf[p] = (uint16_t)(bin[s] | ((pf[s].kt & SW_NULL) ? SW_LKF_NULL : 0u));
+      S.lkf[p] = (uint16_t)(bin[s] | ((pf[s].kt & SW_NULL) ? SW_LKF_NULL : 0u) | ((pf[s].kt & SW_F1) ? SW_LKF_F1 : 0u));
       S.ref[p] = pf[s].ref;
     }
     for (int x = tid; x < nc; x += SWS_THREADS) {
@@ -760,27 +774,13 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       if (p < E) {
         const uint32_t f = S.lkf[p];
         const int2 a = S.tv[p];
-        const bool car = (f & SW_LKF_CAR) != 0;
         const bool an = vnull || (f & SW_LKF_NULL) != 0;
         double af = 0, ai = 0;
-        bool cand;
-        if constexpr (CT == 0) {
-          sw_conv((uint32_t)a.y, vflt, af, ai);
-          cand = car || sw_pred<NT1>(f1, af, ai, an, 0.0, 0.0, true);
-        } else {
-          cand = car || sw_open<NT1, CT>(f1, (uint32_t)a.y, an);
-        }
+        if constexpr (CT == 0) sw_conv((uint32_t)a.y, vflt, af, ai);
+        const bool cand = (f & (SW_LKF_CAR | SW_LKF_F1)) != 0;  // carried, or e1's filter (scatter)
         const uint32_t lk = f & 0xFFu;
         const int end = (int)S.binoff[lk + 1];
-        const int fe = (int)S.fe[lk];
-        const int q0 = max(p + 1, fe);  // carried candidates are not events
-        if (!car) {  // per-key timestamp order: the next event, and the key's last ts for its first
-          if (p + 1 < end && S.tv[p + 1].x < a.x) e |= SWE_MONO;
-          if (p == fe) {
-            const int64_t prev = S.lastts[lk];
-            if (prev != INT64_MIN && tb + a.x < prev) e |= SWE_MONO;
-          }
-        }
+        const int q0 = max(p + 1, (int)S.fe[lk]);  // carried candidates are not events
         const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
         res = cand ? -4 : -3;  // -4: unresolved
         SW_PROBE_OPC(res = sw_probe, SW_P1, (S.tv, S.lkf, q0, end, a.x, W, f2, cbv, vflt, vnull, maybe_null, res));
@@ -870,14 +870,33 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
         S.gbase = g;
       }
       // 5. still-open candidates become the next carry (sorted order = key, then i)
+      // per-key timestamp order: consecutive events of a key (same key, neither carried) ...
+      {
+        uint32_t fq[SWS_PER + 1];
+        int32_t tq[SWS_PER + 1];
+#pragma unroll
+        for (int k = 0; k <= SWS_PER; k++) {
+          const int p = (int)tid * SWS_PER + k;
+          fq[k] = p < E ? (uint32_t)S.lkf[p] : SW_LKF_CAR;
+          tq[k] = p < E ? S.tv[p].x : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < SWS_PER; k++)
+          if (((fq[k] | fq[k + 1]) & SW_LKF_CAR) == 0 && ((fq[k] ^ fq[k + 1]) & 0xFFu) == 0 && tq[k + 1] < tq[k])
+            e |= SWE_MONO;
+      }
+      // ... and a key's first event against its latest ts so far, which then moves to its last
+      for (int b = tid; b < (int)min(nonebin, (uint32_t)SW_LK); b += SWS_THREADS) {
+        const int fe = (int)S.fe[b], end = (int)S.binoff[b + 1];
+        if (fe < end) {
+          const int64_t prev = S.lastts[b];
+          if (prev != INT64_MIN && tb + S.tv[fe].x < prev) e |= SWE_MONO;
+          S.lastts[b] = tb + S.tv[end - 1].x;
+        }
+      }
 #pragma unroll
       for (int k = 0; k < SWS_PER; k++) {
         const int p = (int)tid * SWS_PER + k;
-        if (p < E) {  // the key's latest ts (its last event in the chunk)
-          const uint32_t f = S.lkf[p];
-          const uint32_t lk = f & 0xFFu;
-          if (!(f & SW_LKF_CAR) && p + 1 == (int)S.binoff[lk + 1]) S.lastts[lk] = tb + S.tv[p].x;
-        }
         if (p < E && SWM(p) == -2) {
           if (pre < (uint32_t)SWS_CCAP) {
             const uint32_t f = S.lkf[p];
