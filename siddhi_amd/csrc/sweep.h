@@ -46,8 +46,10 @@ constexpr int SW_LK = 255;          // local keys per owner; bin 255 = "no item"
 constexpr int SW_MAXOWN = 2048;     // owners (partition bins)
 constexpr int SW_LKTAB = 65536;     // scatter LDS bound: its counters + the key -> local key table
 // partition
-constexpr int SWP_ROUND = 2048;
-constexpr int SWP_SEG = SWP_ROUND / SW_WAVES;
+constexpr int SWP_THREADS = 512;  // scatter workgroup
+constexpr int SWP_WAVES = SWP_THREADS / 64;
+constexpr int SWP_ROUND = 4096;  // events ranked per round: 8 per lane
+constexpr int SWP_SEG = SWP_ROUND / SWP_WAVES;
 constexpr int SWP_SUB = SWP_SEG / 64;
 // solve
 constexpr int SWS_CHUNK = 1984;  // records per chunk: with ~<64 carried, E <= 2048 = 4 per thread
@@ -387,22 +389,22 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B
 }
 
 // ------------------------------------------------------------------ pass 2: stable scatter by owner
-__global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView B, const int32_t* __restrict__ key,
+__global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchView B, const int32_t* __restrict__ key,
                                                            int* err) {
-  // dynamic LDS: per-wave counts (then write cursors) [SW_WAVES][nown], running owner offsets
+  // dynamic LDS: per-wave counts (then write cursors) [SWP_WAVES][nown], running owner offsets
   // [nown], and (lk_lds) the key -> local key table
   extern __shared__ uint32_t sw_dyn[];
   const int nown = D.nown;
-  uint32_t* grun = sw_dyn + SW_WAVES * nown;
+  uint32_t* grun = sw_dyn + SWP_WAVES * nown;
   uint8_t* lkt = (uint8_t*)(grun + nown);
   const int st = blockIdx.x;
   const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
   uint32_t* wcw = sw_dyn + w * nown;
   const uint64_t lt = sw_lanemask_lt();
-  for (int b = threadIdx.x; b < nown; b += SW_THREADS) grun[b] = D.off[(int64_t)b * D.nst + st];
+  for (int b = threadIdx.x; b < nown; b += SWP_THREADS) grun[b] = D.off[(int64_t)b * D.nst + st];
   if (D.lk_lds) {
     const uint32_t* src = (const uint32_t*)D.lk8;
-    for (int b = threadIdx.x; b < (D.maxkeys + 3) / 4; b += SW_THREADS) ((uint32_t*)lkt)[b] = src[b];
+    for (int b = threadIdx.x; b < (D.maxkeys + 3) / 4; b += SWP_THREADS) ((uint32_t*)lkt)[b] = src[b];
   }
   const uint8_t* lkq = D.lk_lds ? (const uint8_t*)lkt : D.lk8;
   const int64_t lo = (int64_t)st * D.st_len, hi = min(B.n, lo + D.st_len);
@@ -477,10 +479,10 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_scatter(SweepDev D, BatchView
 #pragma unroll
     for (int s = 0; s < SWP_SUB; s++) rk[s] += __shfl(old[s], (int)ld[s], 64);
     __syncthreads();
-    for (int b = threadIdx.x; b < nown; b += SW_THREADS) {
+    for (int b = threadIdx.x; b < nown; b += SWP_THREADS) {
       uint32_t g = grun[b];
 #pragma unroll
-      for (int ww = 0; ww < SW_WAVES; ww++) {
+      for (int ww = 0; ww < SWP_WAVES; ww++) {
         uint32_t c = sw_dyn[ww * nown + b];
         sw_dyn[ww * nown + b] = g;
         g += c;
@@ -1143,7 +1145,7 @@ struct SweepState {
   // host key map: key -> owner | local key << 16; false when keys cannot be spread under the caps
   static bool build_map(int32_t max_keys, int32_t& nown, std::vector<uint32_t>& kmap) {
     nown = 1;
-    static const int kpo = getenv("SHP_SW_KPO") ? std::max(1, atoi(getenv("SHP_SW_KPO"))) : 10;  // diagnostics
+    static const int kpo = getenv("SHP_SW_KPO") ? std::max(1, atoi(getenv("SHP_SW_KPO"))) : 20;  // diagnostics
     while (nown < SW_MAXOWN && (int64_t)nown * kpo < max_keys) nown *= 2;
     for (;;) {
       std::vector<int32_t> nloc(nown, 0);
@@ -1212,7 +1214,12 @@ struct SweepState {
       if (hipMemcpy(lk, l8.data(), l8.size(), hipMemcpyHostToDevice) != hipSuccess)
         throw std::runtime_error("hipMemcpy failed (sweep key map)");
       D.lk8 = lk;
-      D.lk_lds = (int64_t)(SW_WAVES + 1) * nown * 4 + (int64_t)l8.size() <= SW_LKTAB;
+      D.lk_lds = (int64_t)(SWP_WAVES + 1) * nown * 4 + (int64_t)l8.size() <= SW_LKTAB;
+      const size_t lds = (size_t)(SWP_WAVES + 1) * nown * 4 + (D.lk_lds ? l8.size() : 0);
+      if (lds > 65536 &&
+          hipFuncSetAttribute((const void*)k_sw_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+              hipSuccess)
+        throw std::runtime_error("sweep: scatter LDS request refused");
     }
     int64_t nc = (int64_t)nown * nst_max + 1;
     al(D.cnt, nc);
@@ -1254,8 +1261,8 @@ struct SweepState {
     size_t tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.cnt, D.off, 0u, nc, rocprim::plus<uint32_t>(), s);
     kt.mark("sw_scatter", s);
-    const size_t lds = (size_t)(SW_WAVES + 1) * D.nown * 4 + (D.lk_lds ? (size_t)(D.maxkeys + 3) / 4 * 4 : 0);
-    k_sw_scatter<<<D.nst, SW_THREADS, lds, s>>>(D, B, key, err);
+    const size_t lds = (size_t)(SWP_WAVES + 1) * D.nown * 4 + (D.lk_lds ? (size_t)(D.maxkeys + 3) / 4 * 4 : 0);
+    k_sw_scatter<<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
     kt.mark("sw_solve", s);
     switch ((D.f1.n * 3 + D.f2.n) * 3 + ct) {
 #define SW_CASE(a, b, c) \
