@@ -6,6 +6,7 @@ the library is missing, and engine creation fails when no HIP device is present.
 from __future__ import annotations
 
 import ctypes
+import sys
 import os
 
 import numpy as np
@@ -60,6 +61,11 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run `python -m siddhi_amd.build` "
                               f"(there is no CPU fallback for the state path)")
+        # PyTorch-ROCm ships its own HIP runtime. When the caller uses torch as well, its runtime
+        # must initialise the device first: the two coexist in that order, not the other.
+        torch = sys.modules.get("torch")
+        if torch is not None and hasattr(torch, "cuda"):
+            torch.cuda.is_available()
         L = ctypes.CDLL(LIB_PATH)
         L.shp_engine_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(ShpConfig), ctypes.POINTER(ctypes.c_void_p)]
         for f in ("shp_push_batch", "shp_push_batch_device"):
