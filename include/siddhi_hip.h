@@ -53,7 +53,8 @@ typedef struct shp_config {
   int32_t force_general;   /* 0 auto; 1 general NFA lanes only; 2 no sweep path (scan kernels or
                               lanes); 3 sweep path whenever the shape allows (any key count) */
   int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
-  int32_t match_layout;    /* SHP_LAYOUT_FULL (0) or SHP_LAYOUT_PAIRS (1, sweep path only) */
+  int32_t match_layout;    /* SHP_LAYOUT_FULL (0), SHP_LAYOUT_PAIRS (1) or SHP_LAYOUT_AGG (2);
+                              PAIRS and AGG need the sweep path */
 } shp_config;
 
 /* Match layouts. FULL: every field of shp_matches is valid. PAIRS (2-state sweep path,
@@ -62,6 +63,13 @@ typedef struct shp_config {
  * key/ts = those of event refs[2i+1] in the pushed batch. shp_fetch_matches expands them. */
 #define SHP_LAYOUT_FULL 0
 #define SHP_LAYOUT_PAIRS 1
+/* AGG (sweep path, program with an "aggregate" select item): the selector's running aggregate
+ * is computed on the device (replaces QuerySelector.processInBatchNoGroupBy with
+ * AvgAttributeAggregatorExecutor / Sum / Count, core/query/selector/QuerySelector.java:271-313).
+ * Only `key` and `agg` are written: match i is one output row (partition key, the aggregate's
+ * value after that match, double), in per-key emission order. The aggregate state per key
+ * carries across pushes. Null values in the aggregated column are rejected (SHP_ERR_UNSUPPORTED). */
+#define SHP_LAYOUT_AGG 2
 
 /* One batch of events in SoA form. Column c follows program["columns"][c]:
  * int->int32, long->int64, float->float32, double->float64, bool->uint8,
@@ -89,7 +97,8 @@ typedef struct shp_matches {
   const int64_t* ref_off;
   const int16_t* slot_len;
   const int64_t* refs;
-  int32_t layout;          /* SHP_LAYOUT_FULL or SHP_LAYOUT_PAIRS (see above) */
+  int32_t layout;          /* SHP_LAYOUT_FULL, SHP_LAYOUT_PAIRS or SHP_LAYOUT_AGG (see above) */
+  const double* agg;       /* SHP_LAYOUT_AGG: the aggregate's value per match */
 } shp_matches;
 
 int shp_engine_create(const char* nfa_program_json, const shp_config* cfg, shp_engine** out);

@@ -27,9 +27,20 @@ class ProgramCompiler {
  public:
   DevProg P{};
   FastShape fast{};
+  // select-side aggregate over the matches (SHP_LAYOUT_AGG): 0 none, 1 avg, 2 sum, 3 count;
+  // over the value of state agg_state in predicate column agg_col (count: no argument)
+  int agg_fn = 0, agg_state = -1, agg_col = -1;
 
   void compile(const char* json) {
     JV root = JReader(json).read();
+    if (root.present("aggregate")) {
+      const JV& a = root.get("aggregate");
+      const std::string& fn = a.get("fn").sv;
+      agg_fn = fn == "avg" ? 1 : fn == "sum" ? 2 : fn == "count" ? 3 : 0;
+      if (!agg_fn) throw CompileError(-2, "aggregate: avg, sum or count");
+      agg_state = a.present("state") ? (int)a.get("state").i() : -1;
+      agg_col = a.present("column") ? (int)a.get("column").i() : -1;
+    }
     P.type = root.get("type").sv == "sequence" ? SEQUENCE : PATTERN;
     P.within = root.get("within").i();
     P.playback = root.get("playback").b();

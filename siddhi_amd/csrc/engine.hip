@@ -146,6 +146,8 @@ struct shp_engine {
   int64_t *d_mts = nullptr, *d_mpos = nullptr, *d_moff = nullptr, *d_refs = nullptr;
   int8_t* d_mtype = nullptr;
   int16_t* d_mslot = nullptr;
+  double* d_magg = nullptr;
+  std::vector<double> h_agg;
   // host copies
   std::vector<int32_t> h_key;
   std::vector<int64_t> h_ts, h_pos, h_off, h_refs;
@@ -191,6 +193,7 @@ struct shp_engine {
     F(d_refs);
     F(d_mtype);
     F(d_mslot);
+    F(d_magg);
     fs.release();
     sw.release();
     kt.release();
@@ -242,6 +245,14 @@ struct shp_engine {
       fast = 2;
     if (cfg.match_layout == SHP_LAYOUT_PAIRS && fast != 2)
       throw CompileError(-2, "match_layout PAIRS needs the sweep path");
+    if (cfg.match_layout == SHP_LAYOUT_AGG) {
+      // the aggregate reads e2's value: the sweep's single predicate column (count: none)
+      const bool col_ok = comp.agg_fn == 3 || (comp.agg_state == 1 && comp.agg_col == 0 && comp.P.ncol == 1);
+      if (fast != 2 || !comp.agg_fn || !col_ok)
+        throw CompileError(-2, "match_layout AGG needs the sweep path and an avg/sum/count over e2's filtered column");
+    } else if (cfg.match_layout != SHP_LAYOUT_FULL && cfg.match_layout != SHP_LAYOUT_PAIRS) {
+      throw CompileError(-1, "unknown match_layout");
+    }
     kt.enabled = cfg.profile_kernels != 0;
     cap = cfg.max_batch + 1;
     alloc(d_ts, cap);
@@ -269,6 +280,7 @@ struct shp_engine {
     alloc(d_refs, rcap);
     alloc(d_mtype, mcap);
     alloc(d_mslot, mcap * MAXS);
+    if (cfg.match_layout == SHP_LAYOUT_AGG) alloc(d_magg, mcap);
     // scratch for rocPRIM
     size_t b1 = 0, b2 = 0, b3 = 0;
     HIP_OK(rocprim::radix_sort_pairs(nullptr, b1, d_skey, d_skey2, d_idx, d_perm, (size_t)cap, 0, key_bits + 1,
@@ -281,6 +293,7 @@ struct shp_engine {
     HIP_OK(hipMalloc(&d_tmp, tmp_bytes));
     if (fast == 2) {
       sw.create(comp.P, comp.fast, cfg.max_keys, cap, nown, kmap, stream);
+      if (cfg.match_layout == SHP_LAYOUT_AGG) sw.enable_agg(comp.agg_fn, cfg.max_keys, kmap, stream);
 #ifdef SHP_SW_STAMPS
       HIP_OK(hipMalloc((void**)&sw.D.stamps, (size_t)nown * 8 * sizeof(unsigned long long)));
       HIP_OK(hipMemset(sw.D.stamps, 0, (size_t)nown * 8 * sizeof(unsigned long long)));
@@ -324,7 +337,7 @@ struct shp_engine {
       B.cols[c] = in ? in->cols[c] : d_cols[c];
       B.nulls[c] = in ? (in->nulls ? in->nulls[c] : nullptr) : d_nulls[c];
     }
-    MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs};
+    MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs, d_magg};
     int64_t tsmax = INT64_MIN;
     if (fast == 2) {
       // sweep: no clock scan, no global sort (the engine clock is the running max of ts)
@@ -398,6 +411,7 @@ struct shp_engine {
       if (herr & E_OUT) return fail(SHP_ERR_OUTPUT, "match buffer too small for this batch (max_matches)");
       if (herr & SWE_MONO) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state fast path");
       if (herr & SWE_RANGE) return fail(SHP_ERR_UNSUPPORTED, "timestamps span more than 2^49 ms on the sweep path");
+      if (herr & SWE_AGGNULL) return fail(SHP_ERR_UNSUPPORTED, "null value in the aggregated column (match_layout AGG)");
       return fail(SHP_ERR_CAPACITY, "per-key table capacity exceeded (code " + std::to_string(herr) + ")");
     }
     return SHP_OK;
@@ -417,6 +431,10 @@ struct shp_engine {
       const int64_t no = D.nown, cc = (int64_t)no * SWS_CCAP;
       v = {{D.c_n, (size_t)no * 4}, {D.c_ts, (size_t)cc * 8}, {D.c_seq, (size_t)cc * 8}, {D.c_v, (size_t)cc * 4},
            {D.c_lk, (size_t)cc}, {D.c_null, (size_t)cc}, {D.lastts, (size_t)no * SW_LK * 8}, {D.tsmax, 8}};
+      if (D.agg) {
+        v.push_back({D.agg_s, (size_t)no * SW_LK * 8});
+        v.push_back({D.agg_c, (size_t)no * SW_LK * 8});
+      }
     } else if (fast == 1) {
       const FastDev& F = fs.F;
       v = {{F.c_seq, (size_t)nk * FCC * 8}, {F.c_ts, (size_t)nk * FCC * 8}, {F.c_val, (size_t)nk * FCC * 16},
@@ -507,8 +525,8 @@ struct shp_engine {
 
   // sweep path, PAIRS layout: materialise the full records of the last push on demand
   void ensure_expanded() {
-    if (fast != 2 || expanded) return;
-    MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs};
+    if (fast != 2 || expanded || cfg.match_layout == SHP_LAYOUT_AGG) return;
+    MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs, d_magg};
     sw.expand(lastB, lastKey, O, stream, kt);
     HIP_OK(hipStreamSynchronize(stream));
     expanded = true;
@@ -535,6 +553,16 @@ struct shp_engine {
   }
 
   void fill_device(shp_matches* out) {
+    out->agg = nullptr;
+    if (cfg.match_layout == SHP_LAYOUT_AGG) {
+      *out = shp_matches{};
+      out->layout = SHP_LAYOUT_AGG;
+      out->m = last_m;
+      out->num_states = comp.P.nstates;
+      out->key = d_mkey;
+      out->agg = d_magg;
+      return;
+    }
     out->layout = expanded ? SHP_LAYOUT_FULL : SHP_LAYOUT_PAIRS;
     out->m = last_m;
     out->num_states = comp.P.nstates;
@@ -549,6 +577,22 @@ struct shp_engine {
 
   // copy to host and order by (pos, per-lane order) so callbacks follow reference emission order
   void fetch(shp_matches* out) {
+    if (cfg.match_layout == SHP_LAYOUT_AGG) {  // per-key emission order as produced
+      const int64_t m = last_m;
+      h_key.resize(m);
+      h_agg.resize(m);
+      if (m) {
+        HIP_OK(hipMemcpy(h_key.data(), d_mkey, m * 4, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(h_agg.data(), d_magg, m * 8, hipMemcpyDeviceToHost));
+      }
+      *out = shp_matches{};
+      out->layout = SHP_LAYOUT_AGG;
+      out->m = m;
+      out->num_states = comp.P.nstates;
+      out->key = h_key.data();
+      out->agg = h_agg.data();
+      return;
+    }
     ensure_expanded();
     out->layout = SHP_LAYOUT_FULL;
     int64_t m = last_m;
@@ -609,6 +653,7 @@ struct shp_engine {
     out->ref_off = h_off.data();
     out->slot_len = h_slot.data();
     out->refs = h_refs.data();
+    out->agg = nullptr;
   }
 };
 

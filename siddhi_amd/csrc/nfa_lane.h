@@ -93,6 +93,7 @@ struct MatchOut {
   int64_t* ref_off;
   int16_t* slot_len;           // cap * MAXS
   int64_t* refs;
+  double* agg;                 // SHP_LAYOUT_AGG (sweep): aggregate value per match
 };
 
 struct Val {

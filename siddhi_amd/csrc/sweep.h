@@ -65,6 +65,7 @@ constexpr int SW_P2 = 8;     // probes per worklist round
 constexpr int SWE_KEYS = 1 << 20;   // key id outside [0, max_keys)
 constexpr int SWE_MONO = 1 << 21;   // ts decreases within a key
 constexpr int SWE_RANGE = 1 << 23;  // ts outside base +- 2^49 ms
+constexpr int SWE_AGGNULL = 1 << 24; // SHP_LAYOUT_AGG: a closing event's aggregated value is null
 
 // 16-byte record.  kt: [63:56] local key (0xFF = none), [55] carried, [54] null,
 // [49:0] ts - base + 2^49.  ref: batch index (events) or carry slot (carried).
@@ -141,6 +142,13 @@ struct SweepDev {
   uint8_t* c_null;
   int64_t* lastts;       // nown * SW_LK, absolute ts, INT64_MIN when unseen
   int64_t* tsmax;        // running max of ts (engine clock)
+  // SHP_LAYOUT_AGG: selector aggregate over e2's value (1 avg, 2 sum, 3 count; 0 off), its
+  // running per-key state (sum, count as doubles: exact integers to 2^53) and the owner-local
+  // key -> partition key map for the output rows
+  int32_t agg;
+  double* agg_s;         // nown * SW_LK
+  double* agg_c;
+  int32_t* inv;          // nown * SW_LK
   unsigned long long* stamps;  // diagnostic build: nown * 8 phase cycle counts (else unused)
 };
 
@@ -582,8 +590,60 @@ struct SwSolveSmem {
   int64_t lastts[SW_LK];              // batch-relative ts of the key's latest event (INT64_MIN unseen)
   uint32_t wtot[SWS_WAVES];
   unsigned long long gbase;
-  uint16_t wl[SWS_WAVES * SWS_WLCAP];  // per-wave probe worklists (unresolved candidates)
+  union {
+    uint16_t wl[SWS_WAVES * SWS_WLCAP];  // per-wave probe worklists (unresolved candidates)
+    double ainit[2 * SW_LK];             // after the probe, AGG: per-key (sum, count) carried in
+  };
+  double aws[SWS_WAVES], awn[SWS_WAVES];  // AGG: segmented-scan wave totals
+  uint32_t awf[SWS_WAVES];
 };
+
+// exclusive segmented block scan (head flags) of one (sum, count) pair per thread; in: the
+// thread's inclusive aggregate and whether a segment starts in it; out: the sum and count the
+// thread's first position continues from (0 after a segment start in an earlier thread...
+// combined in order)
+__device__ __forceinline__ void sw_block_segscan(double& s, double& n, bool f, double* ws, double* wn, uint32_t* wf) {
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  double is = s, in = n;
+  bool inf = f;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double ys = __shfl_up(is, d, 64), yn = __shfl_up(in, d, 64);
+    const int yf = __shfl_up((int)inf, d, 64);
+    if (lane >= (uint32_t)d) {
+      if (!inf) {
+        is += ys;
+        in += yn;
+      }
+      inf = inf || yf;
+    }
+  }
+  double es = __shfl_up(is, 1, 64), en = __shfl_up(in, 1, 64);
+  int ef = __shfl_up((int)inf, 1, 64);
+  if (lane == 0) {
+    es = 0;
+    en = 0;
+    ef = 0;
+  }
+  if (lane == 63) {
+    ws[w] = is;
+    wn[w] = in;
+    wf[w] = inf ? 1u : 0u;
+  }
+  __syncthreads();
+  double as = 0, an = 0;
+  for (uint32_t i = 0; i < w; i++) {
+    if (wf[i]) {
+      as = ws[i];
+      an = wn[i];
+    } else {
+      as += ws[i];
+      an += wn[i];
+    }
+  }
+  s = ef ? es : as + es;
+  n = ef ? en : an + en;
+}
 
 template <int NW>
 __device__ __forceinline__ uint32_t sw_block_scan_n(uint32_t v, uint32_t* wtot, uint32_t& total) {
@@ -854,6 +914,12 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
         open += (q < E && SWM(q) == -2) ? 1u : 0u;
       }
       for (int i = tid; i <= SW_LK; i += SWS_THREADS) S.ncar[i] = 0;  // recounted below
+      if (D.agg) {  // per-key aggregate state carried in (read before any run end rewrites it)
+        for (int b = tid; b < (int)min(nonebin, (uint32_t)SW_LK); b += SWS_THREADS) {
+          S.ainit[b] = D.agg_s[(int64_t)o * SW_LK + b];
+          S.ainit[SW_LK + b] = D.agg_c[(int64_t)o * SW_LK + b];
+        }
+      }
       uint32_t total;
       const uint32_t pk = sw_block_scan_n<SWS_WAVES>((tot << 16) | open, S.wtot, total);
       uint32_t off = pk >> 16, pre = pk & 0xffffu;
@@ -870,6 +936,68 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
         const unsigned long long g = ctot ? atomicAdd(O.count, (unsigned long long)ctot) : 0ull;
         if (g + ctot > (unsigned long long)O.cap) e |= E_OUT;
         S.gbase = g;
+      }
+      if (D.agg) {
+        // SHP_LAYOUT_AGG: the selector's running aggregate per match, in place of the pairs.
+        // Per closing event q (c closes, value v): the r-th match adds v once more, so its
+        // output is (S + (r+1) v) / (N + r + 1) for avg, where (S, N) is the key's state before
+        // q: a segmented scan over positions (key runs) seeded with the carried-in state.
+        double ts_ = 0, tn_ = 0;
+        bool tf = false;
+#pragma unroll
+        for (int k = 0; k < SWS_PER; k++) {
+          const int q = (int)tid * SWS_PER + k;
+          if (q < E) {
+            const uint32_t f = S.lkf[q];
+            const uint32_t lk = f & 0xFFu;
+            const double v = vflt ? (double)__uint_as_float((uint32_t)S.tv[q].y) : (double)S.tv[q].y;
+            if (cq[k] && ((f & SW_LKF_NULL) || vnull)) e |= SWE_AGGNULL;
+            if ((uint32_t)q == S.binoff[lk]) {
+              ts_ = S.ainit[lk];
+              tn_ = S.ainit[SW_LK + lk];
+              tf = true;
+            }
+            ts_ += (double)cq[k] * v;
+            tn_ += (double)cq[k];
+          }
+        }
+        sw_block_segscan(ts_, tn_, tf, S.aws, S.awn, S.awf);
+        const unsigned long long gb = S.gbase;
+        uint32_t so = pk >> 16;
+        double ps = ts_, pn = tn_;
+#pragma unroll
+        for (int k = 0; k < SWS_PER; k++) {
+          const int q = (int)tid * SWS_PER + k;
+          if (q < E) {
+            const uint32_t f = S.lkf[q];
+            const uint32_t lk = f & 0xFFu;
+            const double v = vflt ? (double)__uint_as_float((uint32_t)S.tv[q].y) : (double)S.tv[q].y;
+            if ((uint32_t)q == S.binoff[lk]) {
+              ps = S.ainit[lk];
+              pn = S.ainit[SW_LK + lk];
+            }
+            const uint32_t c = cq[k];
+            if (c) {
+              const int32_t kid = D.inv[(int64_t)o * SW_LK + lk];
+              for (uint32_t r = 0; r < c; r++) {
+                const double sr = ps + (double)(r + 1) * v, nr = pn + (double)(r + 1);
+                const double val = D.agg == 1 ? sr / nr : (D.agg == 2 ? sr : nr);
+                const uint64_t slot = gb + so + r;
+                if (slot < (uint64_t)O.cap) {
+                  O.key[slot] = kid;
+                  O.agg[slot] = val;
+                }
+              }
+            }
+            ps += (double)c * v;
+            pn += (double)c;
+            so += c;
+            if ((uint32_t)q + 1 == S.binoff[lk + 1]) {  // run end: the key's state after this chunk
+              D.agg_s[(int64_t)o * SW_LK + lk] = ps;
+              D.agg_c[(int64_t)o * SW_LK + lk] = pn;
+            }
+          }
+        }
       }
       // 5. still-open candidates become the next carry (sorted order = key, then i)
       // per-key timestamp order: consecutive events of a key (same key, neither carried) ...
@@ -930,7 +1058,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     //    closing event q is fixed by how many later candidates q also closed.  No barrier after
     //    it: the next chunk's rank step touches only S.wc, and its first barrier comes before
     //    anything this step reads is rewritten.
-    {
+    if (!D.agg) {
       const unsigned long long gb = S.gbase;
       for (int k = 0; k < SWS_PER; k++) {
         const int p = (int)tid + k * SWS_THREADS;
@@ -1240,8 +1368,22 @@ struct SweepState {
     k_sw_init<<<(unsigned)((ninit + 255) / 256), 256, 0, s>>>(D);
   }
 
+  // SHP_LAYOUT_AGG: per-key aggregate state (zero) and the (owner, local key) -> key map
+  void enable_agg(int fn, int32_t max_keys, const std::vector<uint32_t>& kmap, hipStream_t s) {
+    const int64_t nk = (int64_t)D.nown * SW_LK;
+    std::vector<int32_t> inv(nk, -1);
+    for (int32_t k = 0; k < max_keys; k++) inv[(int64_t)(kmap[k] & 0xffffu) * SW_LK + (kmap[k] >> 16)] = k;
+    al(D.agg_s, nk);
+    al(D.agg_c, nk);
+    al(D.inv, nk);
+    if (hipMemcpy(D.inv, inv.data(), nk * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemsetAsync(D.agg_s, 0, nk * 8, s) != hipSuccess || hipMemsetAsync(D.agg_c, 0, nk * 8, s) != hipSuccess)
+      throw std::runtime_error("sweep: aggregate state");
+    D.agg = fn;
+  }
+
   void release() {
-    void* ps[] = {(void*)D.lk8, D.cnt, D.off, D.recs, D.c_n, D.c_ts, D.c_seq, D.c_v, D.c_lk, D.c_null,
+    void* ps[] = {(void*)D.lk8, D.agg_s, D.agg_c, D.inv, D.cnt, D.off, D.recs, D.c_n, D.c_ts, D.c_seq, D.c_v, D.c_lk, D.c_null,
                   D.lastts, D.tsmax, tmp};
     for (void* p : ps)
       if (p) (void)hipFree(p);

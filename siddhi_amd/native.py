@@ -34,7 +34,7 @@ class ShpConfig(ctypes.Structure):
                 ("force_general", ctypes.c_int32), ("profile_kernels", ctypes.c_int32),
                 ("match_layout", ctypes.c_int32)]
 
-LAYOUT_FULL, LAYOUT_PAIRS = 0, 1
+LAYOUT_FULL, LAYOUT_PAIRS, LAYOUT_AGG = 0, 1, 2
 
 
 class ShpBatch(ctypes.Structure):
@@ -46,7 +46,7 @@ class ShpMatches(ctypes.Structure):
     _fields_ = [("m", ctypes.c_int64), ("num_states", ctypes.c_int32),
                 ("key", ctypes.c_void_p), ("ts", ctypes.c_void_p), ("type", ctypes.c_void_p),
                 ("pos", ctypes.c_void_p), ("ref_off", ctypes.c_void_p), ("slot_len", ctypes.c_void_p),
-                ("refs", ctypes.c_void_p), ("layout", ctypes.c_int32)]
+                ("refs", ctypes.c_void_p), ("layout", ctypes.c_int32), ("agg", ctypes.c_void_p)]
 
 
 class ShpError(RuntimeError):
@@ -105,6 +105,8 @@ def _arr(ptr, n, dtype):
 
 def matches_to_numpy(mt: ShpMatches):
     m, S = mt.m, mt.num_states
+    if mt.layout == LAYOUT_AGG:  # one output row per match: (partition key, aggregate value)
+        return {"key": _arr(mt.key, m, np.int32), "agg": _arr(mt.agg, m, np.float64)}
     slot_len = _arr(mt.slot_len, m * S, np.int16).reshape(m, S).astype(np.int32)
     nrefs = int(slot_len.sum())
     return {
@@ -130,6 +132,7 @@ class HipEngine:
         self.h = h
         self.S = L.shp_engine_num_states(h)
         self.max_batch = max_batch
+        self.layout = int(match_layout)
         self._pending = None
 
     @property
@@ -160,15 +163,15 @@ class HipEngine:
             mt = ShpMatches()
             self._check(L.shp_push_batch(self.h, ctypes.byref(b), ctypes.byref(mt)))
             out_all.append(matches_to_numpy(mt))
-        self._pending = _concat(out_all, self._pending, self.S)
+        self._pending = _concat(out_all, self._pending, self.S, self.layout)
 
     def advance(self, now):
         mt = ShpMatches()
         self._check(lib().shp_advance_clock(self.h, int(now), ctypes.byref(mt)))
-        self._pending = _concat([matches_to_numpy(mt)], self._pending, self.S)
+        self._pending = _concat([matches_to_numpy(mt)], self._pending, self.S, self.layout)
 
     def fetch(self):
-        out = self._pending if self._pending is not None else _concat([], None, self.S)
+        out = self._pending if self._pending is not None else _concat([], None, self.S, self.layout)
         self._pending = None
         return out
 
@@ -198,8 +201,10 @@ class HipEngine:
             pass
 
 
-def _concat(parts, prev, S):
+def _concat(parts, prev, S, layout=LAYOUT_FULL):
     parts = ([prev] if prev is not None else []) + list(parts)
+    if not parts and layout == LAYOUT_AGG:
+        return {"key": np.zeros(0, np.int32), "agg": np.zeros(0, np.float64)}
     if not parts:
         return {"key": np.zeros(0, np.int32), "ts": np.zeros(0, np.int64), "type": np.zeros(0, np.int8),
                 "pos": np.zeros(0, np.int64), "slot_len": np.zeros((0, S), np.int32),

@@ -314,8 +314,31 @@ class QueryCompiler:
             "states": states,
             "tree": tree,
         }
+        agg = self._device_aggregate(sel)
+        if agg is not None:
+            program["aggregate"] = agg
         return CompiledQuery(q.name, program, q, self.leaves, self.stream_index, self.columns,
                              sel, names, q.partition)
+
+    def _device_aggregate(self, sel):
+        """The select's aggregate, when the engine can run it (SHP_LAYOUT_AGG): exactly one
+        avg/sum/count whose argument is a filter column of one state; the other items must not
+        aggregate.  Mirrors the selector's aggregator (QuerySelector.java:271-313)."""
+        funcs = [it for it in sel if it["op"] == "func"]
+        if len(funcs) != 1 or funcs[0]["name"] not in ("avg", "sum", "count"):
+            return None
+        f = funcs[0]
+        if f["name"] == "count":
+            return {"fn": "count"} if not f["args"] else None
+        if len(f["args"]) != 1 or f["args"][0]["op"] != "var" or f["args"][0].get("multi"):
+            return None
+        a = f["args"][0]
+        leaf = self.leaves[a["state"]]
+        key = (self.stream_index[leaf.stream], a["attr"])
+        for ci, (s, at, _t) in enumerate(self.columns):
+            if (s, at) == key:
+                return {"fn": f["name"], "state": a["state"], "column": ci}
+        return None
 
 
 class Dictionary:

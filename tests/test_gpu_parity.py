@@ -9,7 +9,7 @@
 import numpy as np
 import pytest
 
-from diff_util import compare, per_key, program_for, run, small_stream
+from diff_util import columns_for, compare, per_key, program_for, run, small_stream
 from golden_runner import load_fixtures, run_fixture
 from oracle.oracle import OracleEngine
 from test_oracle_golden import OUT_OF_SCOPE
@@ -257,3 +257,90 @@ def test_sweep_comparison_grid_vs_oracle(op, typ, with_nulls):
     a, b = outs
     assert compare(a, b) is None, compare(a, b)
     assert sum(len(x) for x in a.values()) > 100
+
+
+def _agg_app(fn, typ="float"):
+    arg = "" if fn == "count" else "e2.price"
+    return (f"define stream StockStream (symbol string, price {typ}, volume long); "
+            f"partition with (symbol of StockStream) begin "
+            f"@info(name='q') from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
+            f"select e1.symbol as symbol, {fn}({arg}) as a insert into Out; end;")
+
+
+def _expected_agg(oracle_mb, price, fn):
+    """Per key, the selector's running aggregate over the oracle's matches in emission order
+    (AvgAttributeAggregatorExecutor: double sum += (double)x, count++, sum / count)."""
+    out = {}
+    state = {}
+    S = oracle_mb["slot_len"].shape[1]
+    off = 0
+    for i in range(len(oracle_mb["key"])):
+        k = int(oracle_mb["key"][i])
+        lens = [int(x) for x in oracle_mb["slot_len"][i]]
+        e2 = int(oracle_mb["refs"][off + lens[0]])
+        off += sum(lens)
+        s, c = state.get(k, (0.0, 0))
+        s += float(price[e2])
+        c += 1
+        state[k] = (s, c)
+        out.setdefault(k, []).append(s / c if fn == "avg" else (s if fn == "sum" else float(c)))
+    return out
+
+
+@pytest.mark.parametrize("fn", ["avg", "sum", "count"])
+@pytest.mark.parametrize("typ", ["float", "int"])
+def test_device_aggregate_vs_oracle_selector(fn, typ):
+    """SHP_LAYOUT_AGG (row 18 / §8f-1): the running per-key avg/sum/count over the matches,
+    on the device, against the oracle's matches folded by the reference aggregator's arithmetic.
+    Keys and per-key counts exact; values within 1e-9 relative (the device sums in a different
+    association; north_star allows 1e-6)."""
+    from siddhi_amd.native import LAYOUT_AGG
+    from siddhi_amd.query.compiler import compile_app
+    cq = compile_app(_agg_app(fn, typ))[1][0]
+    assert cq.program["aggregate"]["fn"] == fn
+    g = small_stream(5, 80_000, 300)
+    if typ == "int":
+        g["price"] = (g["price"] * 10).astype(np.int32)
+    a = run(OracleEngine(cq.program_json(), 0), cq, g)
+    want = _expected_agg(a, columns_for(cq, g)[0], fn)
+    eng = hip(3, max_keys=300, max_batch=1 << 15, match_layout=LAYOUT_AGG)(cq.program_json(), 0)
+    assert eng.path == 2
+    b = run(eng, cq, g, 17_011)
+    got = {}
+    for k, v in zip(b["key"], b["agg"]):
+        got.setdefault(int(k), []).append(float(v))
+    assert set(got) == set(want)
+    for k in want:
+        assert len(got[k]) == len(want[k]), k
+        np.testing.assert_allclose(got[k], want[k], rtol=1e-9, atol=0)
+    assert sum(len(v) for v in want.values()) > 1000
+
+
+def test_device_aggregate_snapshot_restore():
+    from siddhi_amd.native import LAYOUT_AGG, _concat
+    cq = program_for(5)
+    g = small_stream(5, 40_000, 300)
+    want = _expected_agg(run(OracleEngine(cq.program_json(), 0), cq, g), columns_for(cq, g)[0], "avg")
+    half = {k: v[:20000] for k, v in g.items()}
+    rest = {k: v[20000:] for k, v in g.items()}
+    mk = hip(0, max_keys=300, max_batch=1 << 15, match_layout=LAYOUT_AGG)
+    a = mk(cq.program_json(), 0)
+    first = run(a, cq, half)
+    b = mk(cq.program_json(), 0)
+    b.restore(a.snapshot())
+    second = run(b, cq, rest)
+    got = {}
+    for part in (first, second):
+        for k, v in zip(part["key"], part["agg"]):
+            got.setdefault(int(k), []).append(float(v))
+    assert set(got) == set(want)
+    for k in want:
+        np.testing.assert_allclose(got[k], want[k], rtol=1e-9, atol=0)
+
+
+def test_device_aggregate_rejects_other_shapes():
+    from siddhi_amd.native import LAYOUT_AGG, ShpError
+    with pytest.raises(ShpError):
+        hip(0, max_keys=300, match_layout=LAYOUT_AGG)(program_for(2).program_json(), 0)  # no aggregate
+    with pytest.raises(ShpError):
+        hip(1, max_keys=300, match_layout=LAYOUT_AGG)(program_for(5).program_json(), 0)  # lanes path
