@@ -29,7 +29,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 BYTES_PER_EVENT = 16    # ts 8 + key 4 + price 4
-BYTES_PER_MATCH = 16    # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
+BYTES_PER_MATCH = {"pairs": 16,  # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
+                   "agg": 12,    # (key u32, aggregate f64) per match (SHP_LAYOUT_AGG, C5)
+                   "full": 16}
 KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_solve", "sw_expand",
            "radix_sort", "clock_scan", "key_hist", "key_scan", "sort_keys", "iota", "clamp_clock",
            "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry", "nfa_lanes")
@@ -60,6 +62,9 @@ def parse():
     ap.add_argument("--same-device", action="store_true",
                     help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, collectives over gloo")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
+    ap.add_argument("--latency-batches", type=int, default=200,
+                    help="§8d latency: batches of --latency-events, push + D2H of the match payload (0: skip)")
+    ap.add_argument("--latency-events", type=int, default=16_000_000)
     return ap.parse_args()
 
 
@@ -96,10 +101,12 @@ def main():
     K_local = -(-K // G)  # each rank's engine holds a dense dictionary of the keys it owns
     cap = int(N * 1.08) + 4096 if G > 1 else N
     force = {"auto": 0, "general": 1, "scan": 2}[a.path]
+    sweep = force == 0 and _sweep_shape(cq, local, K_local)
+    layout = ("agg" if "aggregate" in cq.program else "pairs") if sweep else "full"
     eng = native.HipEngine(cq.program_json(), 0, max_keys=K_local, max_batch=cap, max_matches=cap,
                            device=local, force_general=force, profile_kernels=True,
-                           match_layout=native.LAYOUT_PAIRS if force == 0 and _sweep_shape(cq, local, K_local)
-                           else native.LAYOUT_FULL)
+                           match_layout={"agg": native.LAYOUT_AGG, "pairs": native.LAYOUT_PAIRS,
+                                         "full": native.LAYOUT_FULL}[layout])
     L = native.lib()
     steps = a.warmup + a.steps
 
@@ -178,19 +185,26 @@ def main():
     else:
         ev_total, m_total = ev_local, m_local
 
+    latency = None
+    if rank == 0 and G == 1 and a.latency_batches > 0 and layout != "full":
+        latency = batch_latency(eng, L, native, spec, K, layout, a.latency_events, a.latency_batches,
+                                (a.warmup + a.steps + 1) * N)
+
     if rank == 0:
         value = ev_total / elapsed
         dom = max(kernel_ms, key=lambda k: kernel_ms[k])
         dom_ms = kernel_ms[dom] / a.steps
         ev_per_launch = ev_local / a.steps
         m_per_launch = m_local / a.steps
-        alg_bytes = BYTES_PER_EVENT * ev_per_launch + BYTES_PER_MATCH * m_per_launch
+        alg_bytes = BYTES_PER_EVENT * ev_per_launch + BYTES_PER_MATCH[layout] * m_per_launch
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(a.pmc):
             try:
                 pm = json.load(open(a.pmc))
-                traffic = pm.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+                # PMC passes are of one bench command (tools/pmc_run.sh): its config only
+                if str(pm.get("config", "2")) == str(cfg_id) and int(pm.get("keys", K)) == K:
+                    traffic = pm.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         cpu = None
@@ -220,6 +234,8 @@ def main():
                 "matches_per_step_gpu0": m_per_launch,
                 "p50_batch_ms": float(np.percentile(lat, 50)),
                 "p99_batch_ms": float(np.percentile(lat, 99)),
+                "match_layout": layout,
+                "latency": latency,
             },
             "roofline": {
                 "bound": "hbm",
@@ -237,6 +253,39 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def batch_latency(eng, L, native, spec, K, layout, n, batches, start):
+    """SURVEY §8d latency: batches of n events (device-resident input, generated untimed), each
+    timed from shp_push_batch_device entry until its match payload (pairs, or (key, aggregate)
+    rows) is in host memory (hipMemcpy to pageable memory), over `batches` batches."""
+    import torch
+    bufs = [(torch.empty(n, dtype=torch.int64, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
+             torch.empty(n, dtype=torch.float32, device="cuda")) for _ in range(2)]
+    per = BYTES_PER_MATCH[layout]
+    host = np.empty(int(n * 1.1) * 2, dtype=np.int64)
+    lat = []
+    for b in range(batches):
+        ts, key, price = bufs[b & 1]
+        assert L.shp_synth_fill(spec.config, start + b * n, n, K, 1, int(spec.dense), ts.data_ptr(), key.data_ptr(),
+                                price.data_ptr(), None, None, None) == 0
+        torch.cuda.synchronize()
+        colp = (ctypes.c_void_p * 1)(price.data_ptr())
+        bt = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), None, ctypes.cast(colp, ctypes.c_void_p), None)
+        mt = native.ShpMatches()
+        t0 = time.perf_counter()
+        rc = L.shp_push_batch_device(eng.h, ctypes.byref(bt), ctypes.byref(mt))
+        if rc != 0:
+            raise native.ShpError(rc, L.shp_last_error(eng.h).decode())
+        if layout == "agg":
+            L.shp_dev_to_host(host.ctypes.data, mt.key, mt.m * 4)
+            L.shp_dev_to_host(host.ctypes.data + mt.m * 4, mt.agg, mt.m * 8)
+        else:
+            L.shp_dev_to_host(host.ctypes.data, mt.refs, mt.m * 16)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    return {"batch_events": n, "batches": batches, "bytes_per_match_to_host": per,
+            "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+            "what": "shp_push_batch_device entry -> match payload in host memory"}
 
 
 def _sweep_shape(cq, device, keys):

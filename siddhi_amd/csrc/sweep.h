@@ -44,6 +44,7 @@ constexpr int SW_THREADS = 256;
 constexpr int SW_WAVES = SW_THREADS / 64;
 constexpr int SW_LK = 255;          // local keys per owner; bin 255 = "no item"
 constexpr int SW_MAXOWN = 2048;     // owners (partition bins)
+constexpr int SW_PREF_OWN = 1024;   // owner count the map stops at unless keys would crowd them
 constexpr int SW_LKTAB = 65536;     // scatter LDS bound: its counters + the key -> local key table
 // partition
 constexpr int SWP_THREADS = 512;  // scatter workgroup
@@ -1274,7 +1275,12 @@ struct SweepState {
   static bool build_map(int32_t max_keys, int32_t& nown, std::vector<uint32_t>& kmap) {
     nown = 1;
     static const int kpo = getenv("SHP_SW_KPO") ? std::max(1, atoi(getenv("SHP_SW_KPO"))) : 20;  // diagnostics
-    while (nown < SW_MAXOWN && (int64_t)nown * kpo < max_keys) nown *= 2;
+    // about kpo keys per owner, but at most SW_PREF_OWN owners while an owner stays under
+    // ~200 keys: fewer, longer per-owner runs per scatter round (full-line writes), and 1024
+    // owners already give every CU its workgroups
+    while (nown < SW_MAXOWN && (int64_t)nown * kpo < max_keys &&
+           (nown < SW_PREF_OWN || (int64_t)nown * 200 < max_keys))
+      nown *= 2;
     for (;;) {
       std::vector<int32_t> nloc(nown, 0);
       kmap.assign(max_keys, 0);

@@ -1,6 +1,8 @@
 #!/bin/bash
 # GPU box: kernel-trace stats + two PMC passes (FETCH_SIZE, WRITE_SIZE) over a short bench run.
 # Writes gpurun_out/{stats,pmc_fetch,pmc_write}/ and gpurun_out/pmc.json.
+# BENCH_ARGS other than the default C2 run: also set PMC_CONFIG / PMC_KEYS (recorded in pmc.json,
+# bench.py uses the traffic only for the same config and key count).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 ARGS="--steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS}"

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--keys", type=int, default=10_000)
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--agg", action="store_true", help="SHP_LAYOUT_AGG (the query must have an aggregate)")
     a = ap.parse_args()
     import torch
     from siddhi_amd import native, synth
@@ -28,7 +29,7 @@ def main():
     cq = qs[0]
     N, K = a.events, a.keys
     eng = native.HipEngine(cq.program_json(), 0, max_keys=K, max_batch=N, max_matches=N, profile_kernels=True,
-                           match_layout=native.LAYOUT_PAIRS)
+                           match_layout=native.LAYOUT_AGG if a.agg else native.LAYOUT_PAIRS)
     L = native.lib()
     stamps = hasattr(L, "shp_debug_sw_stamps")
     for rep in range(a.reps):
