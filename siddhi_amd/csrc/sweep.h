@@ -597,6 +597,7 @@ struct SwSolveSmem {
   };
   double aws[SWS_WAVES], awn[SWS_WAVES];  // AGG: segmented-scan wave totals
   uint32_t awf[SWS_WAVES];
+  int32_t ainv[SW_LK];                    // AGG: local key -> partition key of this owner
 };
 
 // exclusive segmented block scan (head flags) of one (sum, count) pair per thread; in: the
@@ -705,6 +706,8 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     const int64_t t = D.lastts[(int64_t)o * SW_LK + i];
     S.lastts[i] = t == INT64_MIN ? INT64_MIN : t - base;
   }
+  if (D.agg)
+    for (int i = tid; i < SW_LK; i += SWS_THREADS) S.ainv[i] = D.inv[(int64_t)o * SW_LK + i];
   int cur = 0;
   // prefetch chunk 0: record j of a chunk = w * (64 * SWS_RPT) + s * 64 + lane
   SwRec pf[SWS_RPT];
@@ -979,7 +982,7 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
             }
             const uint32_t c = cq[k];
             if (c) {
-              const int32_t kid = D.inv[(int64_t)o * SW_LK + lk];
+              const int32_t kid = S.ainv[lk];
               for (uint32_t r = 0; r < c; r++) {
                 const double sr = ps + (double)(r + 1) * v, nr = pn + (double)(r + 1);
                 const double val = D.agg == 1 ? sr / nr : (D.agg == 2 ? sr : nr);
