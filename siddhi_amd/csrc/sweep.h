@@ -501,7 +501,11 @@ __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchVie
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < SWP_SUB; s++)
+#ifdef SHP_SCATTER_DIAG  // diagnostics only: coalesced stores at the event's own index (wrong output)
+      if (own[s] != 0xffffffffu) D.recs[rec[s].ref] = rec[s];
+#else
       if (own[s] != 0xffffffffu) D.recs[wcw[own[s]] + rk[s]] = rec[s];
+#endif
     __syncthreads();
   }
   if (e) atomicOr(err, e);
