@@ -46,17 +46,34 @@ __global__ void k_iota(uint32_t* v, int64_t n) {
   for (; i < n; i += (int64_t)gridDim.x * blockDim.x) v[i] = (uint32_t)i;
 }
 
+// per-key event counts.  Up to KEY_HIST_LDS keys the block counts in LDS and adds its nonzero
+// bins once (few keys would otherwise serialise every event on one global atomic: C1 has one)
+constexpr int KEY_HIST_LDS = 8192;
 __global__ void k_key_hist(const int32_t* key, const int32_t* stream, int64_t n, uint32_t* cnt, int32_t max_keys,
                            int partitioned, int* err) {
+  extern __shared__ uint32_t h[];
+  const bool lds = max_keys <= KEY_HIST_LDS;
+  if (lds) {
+    for (int b = threadIdx.x; b < max_keys; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+  }
+  int e = 0;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int32_t k = partitioned ? key[i] : 0;
     if (stream[i] < 0) continue;  // clock-only event (advance)
     if (k < 0 || k >= max_keys) {
-      atomicOr(err, 1 << 20);
+      e = 1 << 20;
       continue;
     }
-    atomicAdd(&cnt[k], 1u);
+    if (lds) atomicAdd(&h[k], 1u);
+    else atomicAdd(&cnt[k], 1u);
+  }
+  if (e) atomicOr(err, e);
+  if (lds) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < max_keys; b += blockDim.x)
+      if (h[b]) atomicAdd(&cnt[b], h[b]);
   }
 }
 
@@ -106,8 +123,67 @@ __global__ __launch_bounds__(64) void k_nfa_lanes(const DevProg* __restrict__ Pp
   }
 }
 
+// copy one lane's state between two arena layouts (element i of lane l at field[i * L + l])
+__device__ inline void lane_copy(const LaneLayout& Yd, char* dst, int64_t ld, const LaneLayout& Ys, const char* src,
+                                 int64_t ls) {
+  for (int f = 0; f < Ys.nf; f++) {
+    const int sz = Ys.f_sz[f];
+    for (int i = 0; i < Ys.f_elems[f]; i++) {
+      char* d = dst + Yd.f_off[f] + ((int64_t)i * Yd.L + ld) * sz;
+      const char* s = src + Ys.f_off[f] + ((int64_t)i * Ys.L + ls) * sz;
+      switch (sz) {
+        case 8: *(uint64_t*)d = *(const uint64_t*)s; break;
+        case 4: *(uint32_t*)d = *(const uint32_t*)s; break;
+        case 2: *(uint16_t*)d = *(const uint16_t*)s; break;
+        default: *d = *s; break;
+      }
+    }
+  }
+}
+
+// Few keys: the lanes' state lives in LDS for the batch (copied in and out of the HBM arena),
+// so the per-event chain of dependent state accesses runs at LDS latency instead of HBM
+// latency.  Same Lane code, one lane per thread, blockDim lanes per workgroup.
+__global__ __launch_bounds__(64) void k_nfa_lanes_lds(const DevProg* __restrict__ Pp, LaneLayout Y, char* arena, LaneLayout Yl,
+                                BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
+                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt, int32_t nlanes,
+                                int* err) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int32_t t = threadIdx.x;
+  const int32_t k = blockIdx.x * blockDim.x + t;
+  if (k >= nlanes) return;
+  lane_copy(Yl, lds, t, Y, arena, k);
+  const DevProg& P = *Pp;
+  Lane ln(P, Yl, lds, t, k, B, O);
+  if (!B.partitioned && !ln.at<uint8_t>(Yl.o_kinit, 0)) {
+    ln.clock = B.init_clock;
+    ln.emit_pos = B.seq0;
+    ln.init_partition();
+  }
+  int64_t lo = 0;
+  uint32_t b = kbeg[k], e = b + kcnt[k];
+  for (uint32_t p = b; p < e && !ln.err; p++) {
+    int64_t g = perm[p];
+    ln.maybe_gc();
+    ln.timers(lo, g);
+    ln.on_event(g);
+    lo = g + 1;
+  }
+  if (!ln.err) {
+    ln.maybe_gc();
+    ln.timers(lo, B.n - 1);
+  }
+  ln.flush_ret();
+  if (ln.err) {
+    ln.at<int32_t>(Yl.o_err, 0) |= ln.err;
+    atomicOr(err, ln.err);
+  }
+  lane_copy(Y, arena, k, Yl, lds, t);
+}
+
 // ---------------------------------------------------------------- engine
 constexpr int32_t SWEEP_MIN_KEYS = 256;
+constexpr int32_t LDS_LANES_MAX_KEYS = 8192;  // general lanes with state in LDS up to this many keys
 
 struct shp_engine {
   KTimer kt;
@@ -158,6 +234,8 @@ struct shp_engine {
   int64_t seq = 0;
   int64_t clock = 0;
   int key_bits = 1;
+  LaneLayout Yl{};     // per-workgroup LDS layout of the lanes (lds_lanes > 0)
+  int lds_lanes = 0;
   double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
   int64_t last_m = 0;
 
@@ -302,6 +380,17 @@ struct shp_engine {
       fs.create(comp.P, comp.fast, cfg.max_keys, cap, mcap, stream);
     } else {
       Y.build(cfg.max_keys);
+      // few keys: lanes in LDS, as many per workgroup as fit 64 KB (at most 16)
+      lds_lanes = 0;
+      if (cfg.max_keys <= LDS_LANES_MAX_KEYS && !getenv("SHP_NO_LDS_LANES")) {
+        for (int lw = 16; lw >= 1; lw /= 2) {
+          Yl.build(lw);
+          if (Yl.bytes <= 65536) {
+            lds_lanes = lw;
+            break;
+          }
+        }
+      }
       HIP_OK(hipMalloc((void**)&arena, Y.bytes));
       HIP_OK(hipMemsetAsync(arena, 0, Y.bytes, stream));
     }
@@ -363,7 +452,8 @@ struct shp_engine {
       // 2. partition by key (stable)
       HIP_OK(hipMemsetAsync(d_kcnt, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
       kt.mark("key_hist", stream);
-      k_key_hist<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_kcnt, cfg.max_keys, P.partitioned, d_err);
+      k_key_hist<<<gb, 256, cfg.max_keys <= KEY_HIST_LDS ? (size_t)cfg.max_keys * 4 : 0, stream>>>(
+          x_key, x_stream, n, d_kcnt, cfg.max_keys, P.partitioned, d_err);
       tb = tmp_bytes;
       kt.mark("key_scan", stream);
       HIP_OK(rocprim::exclusive_scan(d_tmp, tb, d_kcnt, d_kbeg, 0u, (size_t)cfg.max_keys, rocprim::plus<uint32_t>(),
@@ -383,7 +473,12 @@ struct shp_engine {
       } else {
         int L = cfg.max_keys;
         kt.mark("nfa_lanes", stream);
-        k_nfa_lanes<<<(L + 63) / 64, 64, 0, stream>>>(dprog, Y, arena, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+        if (lds_lanes > 0) {
+          k_nfa_lanes_lds<<<(L + lds_lanes - 1) / lds_lanes, lds_lanes, (size_t)Yl.bytes, stream>>>(
+              dprog, Y, arena, Yl, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+        } else {
+          k_nfa_lanes<<<(L + 63) / 64, 64, 0, stream>>>(dprog, Y, arena, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+        }
         kt.mark(nullptr, stream);
       }
       if (n > 0) HIP_OK(hipMemcpyAsync(&tsmax, d_rmax + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, stream));

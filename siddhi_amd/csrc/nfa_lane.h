@@ -33,12 +33,21 @@ struct LaneLayout {
   int64_t o_se_ts, o_se_slot, o_se_type, o_nd_seq, o_nd_ts, o_nd_val, o_nd_next, o_nd_null;
   int64_t o_se_used, o_nd_used, o_lst_len, o_lst, o_pflags, o_lsched, o_larr, o_ret, o_q, o_qhead, o_qlen;
   int64_t o_kinit, o_err, bytes;
+  // the field table (offset, elements per lane, element bytes), for copying one lane's state
+  // between two layouts (k_nfa_lanes_lds)
+  int32_t nf;
+  int64_t f_off[24];
+  int32_t f_elems[24], f_sz[24];
 
   void build(int64_t lanes) {
     L = lanes;
     int64_t o = 0;
+    nf = 0;
     auto f = [&](int64_t& off, int64_t elems, int64_t sz) {
       off = o;
+      f_off[nf] = o;
+      f_elems[nf] = (int32_t)elems;
+      f_sz[nf++] = (int32_t)sz;
       o += ((elems * L * sz + 255) / 256) * 256;
     };
     f(o_se_ts, NSE, 8);
@@ -1273,14 +1282,35 @@ struct Lane {
     if (lo > hi) return -1;
     if (clock_before(lo) < due) {
       // rmax is monotone: lower_bound(rmax[lo..hi] >= due); that event raised the clock -> a call
-      if (B.rmax[hi] < due) return -1;
-      int64_t a = lo, b = hi;
-      while (a < b) {
-        int64_t m = a + (b - a) / 2;
-        if (B.rmax[m] >= due) b = m;
-        else a = m + 1;
+      const int64_t rh = B.rmax[hi];
+      if (rh < due) return -1;
+      const int64_t rl = B.rmax[lo];
+      if (rl >= due) return lo;
+      // lower bound in (a, b] with rmax[a] < due <= rmax[b]: interpolation steps (event-time
+      // clocks are close to linear in the index, so this takes a few dependent loads, not
+      // log2(range)), alternating with bisection for the worst case
+      int64_t a = lo, b = hi, ra = rl, rb = rh;
+      bool interp = true;
+      while (b - a > 1) {
+        int64_t m;
+        if (interp && rb > ra) {
+          const double f = (double)(due - ra) / (double)(rb - ra);
+          m = a + (int64_t)(f * (double)(b - a));
+          m = m <= a ? a + 1 : (m >= b ? b - 1 : m);
+        } else {
+          m = a + (b - a) / 2;
+        }
+        interp = !interp;
+        const int64_t rm = B.rmax[m];
+        if (rm >= due) {
+          b = m;
+          rb = rm;
+        } else {
+          a = m;
+          ra = rm;
+        }
       }
-      return a;
+      return b;
     }
     for (int64_t c = lo; c <= hi; c++) {
       if (P.playback ? is_call(c) : (B.ts[c] >= due)) return c;

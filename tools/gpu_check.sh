@@ -18,6 +18,6 @@ step smoke timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke(
 step bench timeout -k 10 400 python -u bench.py ${BENCH_ARGS}
 if [ -n "$PROF" ]; then
   export TMPDIR=/tmp
-  step prof timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 -u bench.py --no-cpu-baseline ${BENCH_ARGS}
+  step prof timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 -u bench.py --no-cpu-baseline --latency-batches 0 ${BENCH_ARGS}
 fi
 exit 0
