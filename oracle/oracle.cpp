@@ -381,6 +381,32 @@ struct Engine {
       r.b = a.t == T_NULL;
       return r;
     }
+    // scalar functions: FunctionExecutor.execute (core/executor/function/FunctionExecutor.java:85-99)
+    // evaluates every argument, then the function body
+    if (op == "ifthenelse") {  // IfThenElseFunctionExecutor.execute: Boolean.TRUE.equals(data[0])
+      Val c = eval(e->args[0].get(), se);
+      Val a = eval(e->args[1].get(), se);
+      Val b = eval(e->args[2].get(), se);
+      return (c.t == T_BOOL && c.b) ? a : b;
+    }
+    if (op == "coalesce") {  // CoalesceFunctionExecutor.execute: the first non-null argument
+      Val out;
+      bool found = false;
+      for (auto& x : e->args) {
+        Val v = eval(x.get(), se);
+        if (!found && v.t != T_NULL) {
+          out = v;
+          found = true;
+        }
+      }
+      return out;
+    }
+    if (op == "instanceof") {  // InstanceOf*FunctionExecutor.execute: data instanceof <Type>
+      Val a = eval(e->args[0].get(), se);
+      r.t = T_BOOL;
+      r.b = a.t == e->type && a.t != T_NULL;
+      return r;
+    }
     if (op == "isnullstate") {  // IsNullStreamConditionExpressionExecutor.java:36-52
       r.t = T_BOOL;
       r.b = get_stream_event(se, e->state, e->index) == nullptr;
@@ -1282,6 +1308,13 @@ struct Engine {
       e->args.push_back(buildExpr(v["a"]));
       e->args.push_back(buildExpr(v["b"]));
     } else if (e->op == "not" || e->op == "isnull") {
+      e->args.push_back(buildExpr(v["a"]));
+    } else if (e->op == "ifthenelse" || e->op == "coalesce") {
+      e->type = type_of(v["type"].str);
+      const ojson::Value& a = v["args"];
+      for (size_t i = 0; i < a.arr.size(); i++) e->args.push_back(buildExpr(a.arr[i]));
+    } else if (e->op == "instanceof") {
+      e->type = type_of(v["tag"].str);
       e->args.push_back(buildExpr(v["a"]));
     } else {
       e->type = type_of(v["type"].str);

@@ -65,6 +65,7 @@ class ProgramCompiler {
     for (int i = 0; i < P.nstates; i++) {
       filterPc_.push_back(-1);
       if (states[i].present("filter")) {
+        if (depth(states[i].get("filter")) > MAXSTACK) throw CompileError(-2, "filter expression too deep");
         filterPc_[i] = (int)code_.size();
         emit(states[i].get("filter"));
         code_.push_back(Instr{OP_END, 0, 0, 0, 0, 0});
@@ -181,14 +182,43 @@ class ProgramCompiler {
       in.a = op == "add" ? 0 : op == "sub" ? 1 : op == "mul" ? 2 : op == "div" ? 3 : 4;
       in.b = (uint8_t)tagOf(e.get("type").sv);
       code_.push_back(in);
+    } else if (op == "ifthenelse" || op == "coalesce") {
+      const JV& a = e.get("args");
+      for (size_t i = 0; i < a.size(); i++) emit(a[i]);
+      in.op = op == "ifthenelse" ? OP_IFTE : OP_COALESCE;
+      in.a = (uint8_t)a.size();
+      if (op == "ifthenelse" && a.size() != 3) throw CompileError(-2, "ifThenElse takes 3 arguments");
+      if (a.size() < 1 || a.size() > 8) throw CompileError(-2, "coalesce takes 1..8 arguments");
+      code_.push_back(in);
+    } else if (op == "instanceof") {
+      emit(e.get("a"));
+      in.op = OP_INSTOF;
+      in.a = (uint8_t)tagOf(e.get("tag").sv);
+      code_.push_back(in);
     } else {
       throw CompileError(-2, "unsupported predicate op " + op);
     }
   }
 
+  // evaluation-stack depth of an expression (the VM's stack holds MAXSTACK values)
+  int depth(const JV& e) {
+    const std::string& op = e.get("op").sv;
+    if (op == "const" || op == "var" || op == "isnullstate") return 1;
+    if (op == "and" || op == "or") return std::max(depth(e.get("a")), depth(e.get("b")));
+    if (op == "not" || op == "isnull" || op == "instanceof") return depth(e.get("a"));
+    if (op == "ifthenelse" || op == "coalesce") {
+      const JV& a = e.get("args");
+      int d = 0;
+      for (size_t i = 0; i < a.size(); i++) d = std::max(d, (int)i + depth(a[i]));
+      return d;
+    }
+    return std::max(depth(e.get("a")), 1 + depth(e.get("b")));  // cmp, arithmetic
+  }
+
   int8_t tagExpr(const JV& e) {
     const std::string& op = e.get("op").sv;
-    if (op == "const" || op == "var" || op == "add" || op == "sub" || op == "mul" || op == "div" || op == "mod")
+    if (op == "const" || op == "var" || op == "add" || op == "sub" || op == "mul" || op == "div" || op == "mod" ||
+        op == "ifthenelse" || op == "coalesce")
       return tagOf(e.get("type").sv);
     return T_BOOL;
   }

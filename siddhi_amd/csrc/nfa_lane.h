@@ -298,6 +298,27 @@ SHP_HD inline bool run_filter(const DevProg& P, int pc, const Res& res) {
         st[sp++] = java_arith(in, x, y);
         break;
       }
+      case OP_IFTE: {  // IfThenElseFunctionExecutor.execute (all three arguments evaluated)
+        Val b = st[--sp];
+        Val a = st[--sp];
+        Val c = st[--sp];
+        st[sp++] = (c.tag == T_BOOL && c.bits) ? a : b;
+        break;
+      }
+      case OP_COALESCE: {  // CoalesceFunctionExecutor.execute
+        const int n = in.a;
+        sp -= n;
+        Val r{T_NULL, 0};
+        for (int i = n - 1; i >= 0; i--)
+          if (st[sp + i].tag != T_NULL) r = st[sp + i];
+        st[sp++] = r;
+        break;
+      }
+      case OP_INSTOF: {  // InstanceOf*FunctionExecutor.execute: data instanceof <Type>
+        Val x = st[--sp];
+        st[sp++] = Val{T_BOOL, (x.tag == (int8_t)in.a && x.tag != T_NULL) ? 1 : 0};
+        break;
+      }
       default:
         return false;
     }

@@ -43,6 +43,9 @@ enum Op : uint8_t {
   OP_ISNULL,       // pop x; push x==NULL
   OP_CMP,          // a=cmp(0 gt 1 ge 2 lt 3 le 4 eq 5 ne), b=promoted tag
   OP_ARITH,        // a=op(0 add 1 sub 2 mul 3 div 4 mod), b=result tag
+  OP_IFTE,         // pop else, then, cond; push cond==TRUE ? then : else (ifThenElse)
+  OP_COALESCE,     // a=n: pop n values; push the first non-null in argument order (coalesce)
+  OP_INSTOF,       // a=tag: pop x; push x's tag == a (instanceOf*; null -> FALSE)
 };
 
 struct Instr {

@@ -246,7 +246,41 @@ class QueryCompiler:
                 raise SiddhiAppCreationException(f"arithmetic on {ta}/{tb}")
             rt = ta if NUM_RANK[ta] >= NUM_RANK[tb] else tb
             return {"op": op, "type": rt, "a": a, "b": b}, rt
+        if op == "func":
+            return self._cfunc(e, current)
         raise SiddhiAppCreationException(f"unsupported expression {op} in a state filter")
+
+    INSTANCE_OF = {"instanceofboolean": "bool", "instanceofdouble": "double", "instanceoffloat": "float",
+                   "instanceofinteger": "int", "instanceoflong": "long", "instanceofstring": "string"}
+
+    def _cfunc(self, e: Expr, current: LeafState):
+        """Scalar functions in filters (core/executor/function/*; FunctionExecutor.execute evaluates
+        every argument before the function body), with the reference's validation rules."""
+        name = e.value
+        args = [self._cexpr(a, current) for a in e.args]
+        if name == "ifthenelse":  # IfThenElseFunctionExecutor.java
+            if len(args) != 3:
+                raise SiddhiAppCreationException(
+                    f"Invalid no of arguments passed to ifThenElse() function, required only 3, but found {len(args)}")
+            if args[0][1] != "bool":
+                raise SiddhiAppCreationException("Input type of if in ifThenElse function should be of type BOOL")
+            if args[1][1] != args[2][1]:
+                raise SiddhiAppCreationException("Input type of then in ifThenElse function and else in "
+                                                 "ifThenElse function should be of equivalent type")
+            t = args[1][1]
+            return {"op": "ifthenelse", "type": t, "args": [a for a, _ in args]}, t
+        if name == "coalesce":  # CoalesceFunctionExecutor.java
+            if not args:
+                raise SiddhiAppCreationException("Coalesce must have at least one parameter")
+            t = args[0][1]
+            if any(ta != t for _, ta in args):
+                raise SiddhiAppCreationException("Coalesce cannot have parameters with different type")
+            return {"op": "coalesce", "type": t, "args": [a for a, _ in args]}, t
+        if name in self.INSTANCE_OF:  # InstanceOf*FunctionExecutor.java: data instanceof <Type>
+            if len(args) != 1:
+                raise SiddhiAppCreationException(f"Invalid no of arguments passed to {name}")
+            return {"op": "instanceof", "tag": self.INSTANCE_OF[name], "a": args[0][0]}, "bool"
+        raise SiddhiAppCreationException(f"function {name} is not supported in a state filter")
 
     # --------------------------------------------------------------- select
     def compile_select(self):

@@ -344,3 +344,38 @@ def test_device_aggregate_rejects_other_shapes():
         hip(0, max_keys=300, match_layout=LAYOUT_AGG)(program_for(2).program_json(), 0)  # no aggregate
     with pytest.raises(ShpError):
         hip(1, max_keys=300, match_layout=LAYOUT_AGG)(program_for(5).program_json(), 0)  # lanes path
+
+
+FUNC_APPS = [
+    "define stream S (k string, v float); partition with (k of S) begin @info(name='q') "
+    "from every e1=S[ifThenElse(v > 50.0f, v > 70.0f, v < 20.0f)] -> e2=S[coalesce(v, 0.0f) > e1.v] within 1 sec "
+    "select e1.v as a, e2.v as b insert into Out; end;",
+    "define stream S (k string, v float); partition with (k of S) begin @info(name='q') "
+    "from every e1=S[instanceOfFloat(v)] -> e2=S[not instanceOfFloat(v) or v > e1.v] within 1 sec "
+    "select e1.v as a, e2.v as b insert into Out; end;",
+    "define stream S (k string, v float); partition with (k of S) begin @info(name='q') "
+    "from every e1=S[v > 30.0f], e2=S[ifThenElse(e2[last].v is null, e1.v <= v, e2[last].v <= v)]+, "
+    "e3=S[e2[last].v > v] select e1.v as a, e2[last].v as b, e3.v as c insert into Out; end;",
+]
+
+
+@pytest.mark.parametrize("app", FUNC_APPS, ids=["ifte-coalesce", "instanceof", "seq-ifte"])
+@pytest.mark.parametrize("general", [1, 0], ids=["lanes", "default"])
+def test_filter_functions_vs_oracle(app, general):
+    """§8f-4: ifThenElse / coalesce / instanceOf* in state filters (predicate VM), with nulls."""
+    from siddhi_amd.query.compiler import compile_app
+    cq = compile_app(app)[1][0]
+    rng = np.random.default_rng(7)
+    n, keys = 30_000, 64
+    ts = np.cumsum(rng.integers(0, 40, n)).astype(np.int64) + 1_000
+    key = rng.integers(0, keys, n).astype(np.int32)
+    v = (rng.random(n) * 100).astype(np.float32)
+    nul = (rng.random(n) < 0.05).astype(np.uint8)
+    outs = []
+    for eng in (OracleEngine(cq.program_json(), 0), hip(general, max_keys=keys, max_batch=1 << 14)(cq.program_json(), 0)):
+        for lo in range(0, n, 9_001):
+            hi = min(n, lo + 9_001)
+            eng.push(ts[lo:hi], key[lo:hi], np.zeros(hi - lo, np.int32), [v[lo:hi]], [nul[lo:hi]])
+        outs.append(per_key(eng.fetch()))
+    assert compare(*outs) is None, compare(*outs)
+    assert sum(len(x) for x in outs[0].values()) > 100

@@ -3,7 +3,7 @@
 The fixtures under tests/golden/ are data transcribed from the reference's TestNG
 suites (tests/golden/extract_golden.py).  Constructs outside the state path
 (group by, select *, inner '#' streams, non-partitioned streams inside a
-partition, scalar functions in filters) are listed in OUT_OF_SCOPE.
+partition) are listed in OUT_OF_SCOPE.
 """
 import pytest
 
@@ -16,7 +16,6 @@ OUT_OF_SCOPE = {
     "PatternPartitionTestCase.testPatternPartitionQuery30": "unkeyed stream broadcast into a partition",
     "PatternPartitionTestCase.testPatternPartitionQuery32": "inner '#' streams",
     "PatternPartitionTestCase.testPatternPartitionQuery33": "inner '#' streams",
-    "SequenceTestCase.testQuery20_2": "scalar function in a filter (SURVEY §8f next-4)",
 }
 
 FIXTURES = load_fixtures()
