@@ -45,6 +45,7 @@ constexpr int SW_WAVES = SW_THREADS / 64;
 constexpr int SW_LK = 255;          // local keys per owner; bin 255 = "no item"
 constexpr int SW_MAXOWN = 2048;     // owners (partition bins)
 constexpr int SW_PREF_OWN = 1024;   // owner count the map stops at unless keys would crowd them
+constexpr int SW_MIN_OWN = 512;     // owner count the map grows to while owners keep ~2 keys (fill the CUs)
 constexpr int SW_LKTAB = 65536;     // scatter LDS bound: its counters + the key -> local key table
 // partition
 constexpr int SWP_THREADS = 512;  // scatter workgroup
@@ -1285,8 +1286,13 @@ struct SweepState {
     // about kpo keys per owner, but at most SW_PREF_OWN owners while an owner stays under
     // ~200 keys: fewer, longer per-owner runs per scatter round (full-line writes), and 1024
     // owners already give every CU its workgroups
-    while (nown < SW_MAXOWN && (int64_t)nown * kpo < max_keys &&
-           (nown < SW_PREF_OWN || (int64_t)nown * 200 < max_keys))
+    // ... and at least SW_MIN_OWN owners (two solve workgroups per CU) while an owner keeps
+    // about two keys: one rank of a key-sharded job holds K/N keys (1250 of C2's 10k at N=8),
+    // and K/N/20 owners would leave most CUs without a solve workgroup
+    static const int minown = getenv("SHP_SW_MINOWN") ? std::max(1, atoi(getenv("SHP_SW_MINOWN"))) : SW_MIN_OWN;
+    while (nown < SW_MAXOWN &&
+           (((int64_t)nown * kpo < max_keys && (nown < SW_PREF_OWN || (int64_t)nown * 200 < max_keys)) ||
+            (nown < minown && (int64_t)nown * 2 <= max_keys)))
       nown *= 2;
     for (;;) {
       std::vector<int32_t> nloc(nown, 0);
