@@ -7,8 +7,9 @@ e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec ... end`
 A step = one shp_push_batch_device of the next 100M events of the stream through the engine
 (partition by key + NFA + match compaction into HBM), per-key state carried across steps.
 N>1: one process per GPU; each rank ingests its slice of the global stream and the events are
-redistributed by key owner (key % N) with one RCCL all-to-all per step (torch.distributed nccl),
-so per-GPU work is fixed (weak scaling).
+redistributed by key owner (key % N): a HIP stable split into destination-grouped SoA columns,
+then one RCCL all-to-all per column (torch.distributed nccl) whose receive buffers are the owner's
+engine input as they stand, so per-GPU work is fixed (weak scaling).
 
 Prints ONE JSON line (rank 0) with roofline (dominant kernel, HIP events on the engine stream)
 and cpu_baseline (the oracle, single-threaded, on a bounded sample of the same stream).
@@ -131,7 +132,7 @@ def main():
 
     def step(i):
         """One batch through the hot path.  N>1: batch i was exchanged by key owner while step i-1
-        ran (one RCCL all-to-all of packed records, overlapped with the engine); the exchange of
+        ran (RCCL all-to-alls of its SoA columns, overlapped with the engine); the exchange of
         batch i+1 is started here, before this batch's push."""
         ts, key, price, stream = batches[i]
         if G > 1:
@@ -227,8 +228,8 @@ def main():
                 "workload": WORKLOADS.get(str(cfg_id), f"C{cfg_id}") + f"; {K} keys",
                 "events_per_gpu_per_step": N,
                 "keys": K,
-                "parallelism": f"key-sharded x{G}" + (" (one RCCL all-to-all of packed records per batch, "
-                                                      "overlapped with the previous batch)" if G > 1 else ""),
+                "parallelism": f"key-sharded x{G}" + (" (RCCL all-to-all of the batch's SoA columns by key "
+                                                      "owner, overlapped with the previous batch)" if G > 1 else ""),
                 "engine_path": PATHS.get(eng.path, str(eng.path)),
                 "matches_per_s": m_total / elapsed,
                 "matches_per_step_gpu0": m_per_launch,

@@ -134,6 +134,11 @@ int shp_shard_partition(int64_t n, const int64_t* ts, const int32_t* key, const 
                         int G, void* out, int64_t* counts, void* ws, void* hip_stream);
 int shp_shard_unpack(int64_t m, const void* in, int64_t* ts, int32_t* key, void* value, int32_t* stream,
                      void* hip_stream);
+/* The same split into destination-grouped SoA columns (out_key = key / G; out_value / out_stream
+ * NULL when value / stream is): one all-to-all per column lands the owner's engine input as is. */
+int shp_shard_partition_soa(int64_t n, const int64_t* ts, const int32_t* key, const void* value,
+                            const int32_t* stream, int G, int64_t* out_ts, int32_t* out_key, void* out_value,
+                            int32_t* out_stream, int64_t* counts, void* ws, void* hip_stream);
 /* Bench/test utilities: device memory without a second HIP runtime in the process. */
 void* shp_dev_alloc(int64_t bytes);
 int shp_dev_free(void* p);

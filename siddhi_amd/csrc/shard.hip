@@ -4,7 +4,10 @@
 //                        16-byte records {ts:int64, stream<<24 | key/G : u32, value:u32},
 //                        grouped by destination, arrival order kept within each destination
 //   shp_shard_unpack     packed records -> the engine's SoA columns (ts, key, stream, value)
-// One all-to-all of the packed buffer (RCCL) sits between the two (siddhi_amd/shard.py).
+//   shp_shard_partition_soa  the same split into destination-grouped SoA columns: one
+//                        all-to-all per column lands the owner's engine input, no unpack pass
+// siddhi_amd/shard.py uses the SoA form (one all-to-all per column; RCCL); the packed form
+// (one all-to-all of 16-byte records, then an unpack) is kept for the parity test.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -15,7 +18,10 @@ namespace {
 
 constexpr int SH_THREADS = 256;
 constexpr int SH_TILE = 65536;  // events per super-tile (one workgroup)
-constexpr int SH_ROUND = 2048;
+#ifndef SH_ROUND_EVENTS
+#define SH_ROUND_EVENTS 2048
+#endif
+constexpr int SH_ROUND = SH_ROUND_EVENTS;
 constexpr int SH_SUB = SH_ROUND / SH_THREADS;
 constexpr int SH_MAXG = 16;
 
@@ -44,12 +50,22 @@ __global__ __launch_bounds__(SH_THREADS) void k_shard_count(const int32_t* __res
   if (t == 0 && threadIdx.x == 0) cnt[(int64_t)G * ntiles] = 0;
 }
 
+// SoA destination columns (shp_shard_partition_soa): the received buffers of one all-to-all
+// per column are the engine's input columns as they stand, with no unpack pass
+struct ShSoa {
+  int64_t* ts;
+  int32_t* key;
+  uint32_t* val;
+  int32_t* stream;
+};
+
+template <bool SOA>
 __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __restrict__ ts,
                                                               const int32_t* __restrict__ key,
                                                               const uint32_t* __restrict__ val,
                                                               const int32_t* __restrict__ stream, int64_t n, int G,
                                                               int gbits, int ntiles, const uint32_t* __restrict__ off,
-                                                              ShRec* out) {
+                                                              ShRec* out, ShSoa so) {
   __shared__ uint32_t wc[SH_THREADS / 64][SH_MAXG];
   __shared__ uint32_t run[SH_MAXG];
   const int t = blockIdx.x;
@@ -100,8 +116,18 @@ __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __r
     }
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < SH_SUB; s++)
-      if (dst[s] < SH_MAXG) out[wc[w][dst[s]] + rk[s]] = rec[s];
+    for (int s = 0; s < SH_SUB; s++) {
+      if (dst[s] >= SH_MAXG) continue;
+      const uint32_t o = wc[w][dst[s]] + rk[s];
+      if constexpr (SOA) {
+        so.ts[o] = rec[s].ts;
+        so.key[o] = (int32_t)(rec[s].key & 0xffffffu);
+        if (so.stream) so.stream[o] = (int32_t)(rec[s].key >> 24);
+        if (so.val) so.val[o] = rec[s].v;
+      } else {
+        out[o] = rec[s];
+      }
+    }
     __syncthreads();
   }
 }
@@ -136,9 +162,9 @@ extern "C" int64_t shp_shard_workspace_bytes(int64_t n, int G) {
 // n events (device SoA) -> out: n packed records grouped by destination rank key % G (stable);
 // counts[g] (host) = records for rank g.  Keys must be < 2^24 * G, stream ids < 256.
 // ws: device workspace of shp_shard_workspace_bytes(n, G) bytes.
-extern "C" int shp_shard_partition(int64_t n, const int64_t* ts, const int32_t* key, const void* value,
-                                   const int32_t* stream, int G, void* out, int64_t* counts, void* ws,
-                                   void* hip_stream) {
+static int shard_partition(int64_t n, const int64_t* ts, const int32_t* key, const void* value,
+                           const int32_t* stream, int G, void* out, const ShSoa* so, int64_t* counts, void* ws,
+                           void* hip_stream) {
   if (G < 1 || G > SH_MAXG || n < 0 || !ws) return -1;
   hipStream_t s = (hipStream_t)hip_stream;
   const int ntiles = (int)((n + SH_TILE - 1) / SH_TILE);
@@ -156,14 +182,37 @@ extern "C" int shp_shard_partition(int64_t n, const int64_t* ts, const int32_t* 
   while ((1 << gbits) < G) gbits++;
   k_shard_count<<<ntiles, SH_THREADS, 0, s>>>(key, n, G, ntiles, cnt);
   if (rocprim::exclusive_scan(tmp, tb, cnt, off, 0u, nc, rocprim::plus<uint32_t>(), s) != hipSuccess) return -5;
-  k_shard_scatter<<<ntiles, SH_THREADS, 0, s>>>(ts, key, (const uint32_t*)value, stream, n, G, gbits, ntiles, off,
-                                                (ShRec*)out);
+  if (so)
+    k_shard_scatter<true><<<ntiles, SH_THREADS, 0, s>>>(ts, key, (const uint32_t*)value, stream, n, G, gbits, ntiles,
+                                                        off, nullptr, *so);
+  else
+    k_shard_scatter<false><<<ntiles, SH_THREADS, 0, s>>>(ts, key, (const uint32_t*)value, stream, n, G, gbits, ntiles,
+                                                         off, (ShRec*)out, ShSoa{});
   uint32_t h[SH_MAXG + 1];
   for (int g = 0; g <= G; g++)
     if (hipMemcpyAsync(&h[g], off + (size_t)g * ntiles, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -5;
   if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) return -5;
   for (int g = 0; g < G; g++) counts[g] = (int64_t)h[g + 1] - h[g];
   return 0;
+}
+
+extern "C" int shp_shard_partition(int64_t n, const int64_t* ts, const int32_t* key, const void* value,
+                                   const int32_t* stream, int G, void* out, int64_t* counts, void* ws,
+                                   void* hip_stream) {
+  if (!out && n > 0) return -1;
+  return shard_partition(n, ts, key, value, stream, G, out, nullptr, counts, ws, hip_stream);
+}
+
+// The same stable split into destination-grouped SoA columns: out_ts/out_key(key / G)/out_value
+// (NULL when value is NULL)/out_stream (NULL when stream is NULL), each of n elements.  One
+// all-to-all per column then delivers the owner's engine input directly (no unpack).
+extern "C" int shp_shard_partition_soa(int64_t n, const int64_t* ts, const int32_t* key, const void* value,
+                                       const int32_t* stream, int G, int64_t* out_ts, int32_t* out_key,
+                                       void* out_value, int32_t* out_stream, int64_t* counts, void* ws,
+                                       void* hip_stream) {
+  if (n > 0 && (!out_ts || !out_key || (value && !out_value) || (stream && !out_stream))) return -1;
+  const ShSoa so{out_ts, out_key, value ? (uint32_t*)out_value : nullptr, stream ? out_stream : nullptr};
+  return shard_partition(n, ts, key, value, stream, G, nullptr, &so, counts, ws, hip_stream);
 }
 
 extern "C" int shp_shard_unpack(int64_t m, const void* in, int64_t* ts, int32_t* key, void* value, int32_t* stream,

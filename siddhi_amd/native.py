@@ -25,7 +25,7 @@ SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_
            "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
            "shp_dev_to_host", "shp_snapshot", "shp_restore", "shp_shard_workspace_bytes",
-           "shp_shard_partition", "shp_shard_unpack"]
+           "shp_shard_partition", "shp_shard_unpack", "shp_shard_partition_soa"]
 
 
 class ShpConfig(ctypes.Structure):
@@ -92,6 +92,8 @@ def lib():
         L.shp_shard_partition.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int] + \
             [ctypes.c_void_p] * 4
         L.shp_shard_unpack.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 6
+        L.shp_shard_partition_soa.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int] + \
+            [ctypes.c_void_p] * 7
         _lib = L
     return _lib
 

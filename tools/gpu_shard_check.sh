@@ -1,0 +1,5 @@
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_shard_device.py -x -v --timeout 120 --timeout-method thread > gpurun_out/shard_tests.log 2>&1 || exit $?
+timeout -k 10 120 python -u tools/shard_probe.py > gpurun_out/shard_probe.log 2>&1 || exit $?
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --same-device --steps 3 --warmup 1 > gpurun_out/same_device.log 2>&1 || exit $?
