@@ -23,6 +23,7 @@ import numpy as np
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -124,23 +125,14 @@ def main():
         assert rc == 0
         return ts, key, price, stream
 
-    batches = [gen(s) for s in range(steps + (1 if G > 1 else 0))]
+    # N>1: two batches beyond the timed ones, so every timed step also exchanges a later batch
+    batches = [gen(s) for s in range(steps + (2 if G > 1 else 0))]
     torch.cuda.synchronize()
     xch = shard.DeviceExchange(N, G, dist, torch.device("cuda", local), spec.n_streams > 1,
                                cpu_collectives=backend == "gloo") if G > 1 else None
-    pending = {}
+    ready, pending = {}, {}
 
-    def step(i):
-        """One batch through the hot path.  N>1: batch i was exchanged by key owner while step i-1
-        ran (RCCL all-to-alls of its SoA columns, overlapped with the engine); the exchange of
-        batch i+1 is started here, before this batch's push."""
-        ts, key, price, stream = batches[i]
-        if G > 1:
-            p = pending.pop(i) if i in pending else xch.start(ts, key, price, stream)
-            ts, key, price, stream = xch.finish(p)
-            torch.cuda.current_stream().synchronize()  # the engine runs on its own HIP stream
-            if i + 1 < len(batches):
-                pending[i + 1] = xch.start(*batches[i + 1])
+    def push(ts, key, price, stream):
         n = ts.numel()
         # one pointer per program column (cq.columns: (stream, attr, type)); every stream's
         # predicate attribute is the synthetic price column
@@ -153,6 +145,45 @@ def main():
         if rc != 0:
             raise native.ShpError(rc, L.shp_last_error(eng.h).decode())
         return n, mt.m
+
+    def exchange_ahead(i):
+        """Main thread, while batch i is in the engine: land batch i+1 (its all-to-alls were
+        started one step earlier) and start batch i+2's split + all-to-alls."""
+        if i + 1 in pending:
+            ready[i + 1] = xch.finish(pending.pop(i + 1))
+            torch.cuda.current_stream().synchronize()  # the engine runs on its own HIP stream
+        if i + 2 < len(batches):
+            pending[i + 2] = xch.start(*batches[i + 2])
+
+    if G > 1:  # fill the pipeline (untimed)
+        ready[0] = xch(*batches[0])
+        torch.cuda.current_stream().synchronize()
+        pending[1] = xch.start(*batches[1])
+
+    def step(i):
+        """One batch through the hot path.  N>1: the engine runs batch i (already exchanged by key
+        owner) on a worker thread -- the blocking C call releases the GIL -- while this thread
+        lands batch i+1 and starts the HIP split and RCCL all-to-alls of batch i+2, so the
+        exchange overlaps the engine instead of adding to it."""
+        if G == 1:
+            return push(*batches[i])
+        out = {}
+
+        def work():
+            try:
+                out["r"] = push(*ready.pop(i))
+            except BaseException as ex:  # re-raised on the main thread
+                out["e"] = ex
+
+        th = threading.Thread(target=work)
+        th.start()
+        try:
+            exchange_ahead(i)
+        finally:
+            th.join()
+        if "e" in out:
+            raise out["e"]
+        return out["r"]
 
     for i in range(a.warmup):
         step(i)
@@ -176,6 +207,9 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    for p in list(pending.values()):  # drain the exchange started past the last step (untimed)
+        xch.finish(p)
+    pending.clear()
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

@@ -59,6 +59,9 @@ struct ShSoa {
   int32_t* stream;
 };
 
+// Per round of SH_ROUND events: rank by destination (wave ballots), stage the records in LDS
+// grouped by destination, then write each destination's run with consecutive lanes on
+// consecutive addresses (full-line stores, not 8-way scattered ones).
 template <bool SOA>
 __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __restrict__ ts,
                                                               const int32_t* __restrict__ key,
@@ -66,21 +69,26 @@ __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __r
                                                               const int32_t* __restrict__ stream, int64_t n, int G,
                                                               int gbits, int ntiles, const uint32_t* __restrict__ off,
                                                               ShRec* out, ShSoa so) {
-  __shared__ uint32_t wc[SH_THREADS / 64][SH_MAXG];
-  __shared__ uint32_t run[SH_MAXG];
+  constexpr int NW = SH_THREADS / 64;
+  __shared__ uint32_t wc[NW][SH_MAXG];   // per-wave counts, then the wave's LDS slot base
+  __shared__ uint32_t run[SH_MAXG];      // next global position per destination
+  __shared__ uint32_t gst[SH_MAXG];      // this round's global start per destination
+  __shared__ uint32_t lst[SH_MAXG + 1];  // this round's LDS start per destination
+  __shared__ ShRec srec[SH_ROUND];
+  __shared__ uint8_t sdst[SH_ROUND];
   const int t = blockIdx.x;
   const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   if (threadIdx.x < G) run[threadIdx.x] = off[(int64_t)threadIdx.x * ntiles + t];
   const int64_t lo = (int64_t)t * SH_TILE, hi = min(n, lo + SH_TILE);
   for (int64_t r0 = lo; r0 < hi; r0 += SH_ROUND) {
-    if (threadIdx.x < (SH_THREADS / 64) * SH_MAXG) (&wc[0][0])[threadIdx.x] = 0;
+    if (threadIdx.x < NW * SH_MAXG) (&wc[0][0])[threadIdx.x] = 0;
     __syncthreads();
     ShRec rec[SH_SUB];
     uint32_t dst[SH_SUB], rk[SH_SUB];
 #pragma unroll
     for (int s = 0; s < SH_SUB; s++) {  // wave w owns items [w*SEG, (w+1)*SEG) of the round
-      const int64_t i = r0 + (int64_t)w * (SH_ROUND / 4) + s * 64 + lane;
+      const int64_t i = r0 + (int64_t)w * (SH_ROUND / NW) + s * 64 + lane;
       if (i < hi) {
         const uint32_t k = (uint32_t)key[i];
         rec[s].ts = ts[i];
@@ -105,27 +113,41 @@ __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __r
       if (valid && (peers & lt) == 0) wc[w][dst[s]] = before + (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    if (threadIdx.x < G) {
-      uint32_t g = run[threadIdx.x];
-      for (int ww = 0; ww < SH_THREADS / 64; ww++) {
-        const uint32_t c = wc[ww][threadIdx.x];
-        wc[ww][threadIdx.x] = g;
-        g += c;
+    if (threadIdx.x == 0) {  // G <= 16 destinations x NW waves: one thread
+      uint32_t l = 0;
+      for (int d = 0; d < G; d++) {
+        lst[d] = l;
+        gst[d] = run[d];
+        for (int ww = 0; ww < NW; ww++) {
+          const uint32_t c = wc[ww][d];
+          wc[ww][d] = l;
+          l += c;
+        }
+        run[d] += l - lst[d];
       }
-      run[threadIdx.x] = g;
+      lst[G] = l;
     }
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < SH_SUB; s++) {
       if (dst[s] >= SH_MAXG) continue;
-      const uint32_t o = wc[w][dst[s]] + rk[s];
+      const uint32_t slot = wc[w][dst[s]] + rk[s];
+      srec[slot] = rec[s];
+      sdst[slot] = (uint8_t)dst[s];
+    }
+    __syncthreads();
+    const int nv = (int)lst[G];
+    for (int x = threadIdx.x; x < nv; x += SH_THREADS) {
+      const uint32_t d = sdst[x];
+      const uint32_t o = gst[d] + ((uint32_t)x - lst[d]);
+      const ShRec r = srec[x];
       if constexpr (SOA) {
-        so.ts[o] = rec[s].ts;
-        so.key[o] = (int32_t)(rec[s].key & 0xffffffu);
-        if (so.stream) so.stream[o] = (int32_t)(rec[s].key >> 24);
-        if (so.val) so.val[o] = rec[s].v;
+        so.ts[o] = r.ts;
+        so.key[o] = (int32_t)(r.key & 0xffffffu);
+        if (so.stream) so.stream[o] = (int32_t)(r.key >> 24);
+        if (so.val) so.val[o] = r.v;
       } else {
-        out[o] = rec[s];
+        out[o] = r;
       }
     }
     __syncthreads();
