@@ -1347,6 +1347,7 @@ struct SweepState {
       D.lk_bits = 0;
       while ((1u << D.lk_bits) <= mx) D.lk_bits++;
     }
+    if (getenv("SHP_SW_STLEN")) st_len = std::max<int64_t>(4096, atoll(getenv("SHP_SW_STLEN")));  // diagnostics
     nst_max = (int32_t)std::max<int64_t>(1, (cap + st_len - 1) / st_len);
     D.st_len = st_len;
     {
