@@ -90,14 +90,22 @@ __global__ void k_clamp_clock(int64_t* rmax, int64_t n, int64_t clock0) {
     if (rmax[i] < clock0) rmax[i] = clock0;
 }
 
-__global__ __launch_bounds__(64) void k_nfa_lanes(const DevProg* __restrict__ Pp, LaneLayout Y, char* arena,
+// SHP_LANES_WPE: waves per EU requested from the compiler for the lane kernels (diagnostic A/B:
+// fewer VGPRs and more waves to hide the lanes' dependent memory latency, against more spills)
+#ifdef SHP_LANES_WPE
+#define SHP_LANES_ATTR __attribute__((amdgpu_waves_per_eu(SHP_LANES_WPE, SHP_LANES_WPE)))
+#else
+#define SHP_LANES_ATTR
+#endif
+
+__global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes(const DevProg* __restrict__ Pp, LaneLayout Y, char* arena,
                                                   BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
                                                   const uint32_t* __restrict__ kbeg,
                                                   const uint32_t* __restrict__ kcnt, int32_t nlanes, int* err) {
   int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nlanes) return;
   const DevProg& P = *Pp;
-  Lane ln(P, Y, arena, k, k, B, O);
+  LaneT<1> ln(P, Y, arena, k, k, B, O);
   if (!B.partitioned && !ln.at<uint8_t>(Y.o_kinit, 0)) {
     ln.clock = B.init_clock;
     ln.emit_pos = B.seq0;
@@ -144,7 +152,7 @@ __device__ inline void lane_copy(const LaneLayout& Yd, char* dst, int64_t ld, co
 // Few keys: the lanes' state lives in LDS for the batch (copied in and out of the HBM arena),
 // so the per-event chain of dependent state accesses runs at LDS latency instead of HBM
 // latency.  Same Lane code, one lane per thread, blockDim lanes per workgroup.
-__global__ __launch_bounds__(64) void k_nfa_lanes_lds(const DevProg* __restrict__ Pp, LaneLayout Y, char* arena, LaneLayout Yl,
+__global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes_lds(const DevProg* __restrict__ Pp, LaneLayout Y, char* arena, LaneLayout Yl,
                                 BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
                                 const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt, int32_t nlanes,
                                 int* err) {
@@ -154,7 +162,7 @@ __global__ __launch_bounds__(64) void k_nfa_lanes_lds(const DevProg* __restrict_
   if (k >= nlanes) return;
   lane_copy(Yl, lds, t, Y, arena, k);
   const DevProg& P = *Pp;
-  Lane ln(P, Yl, lds, t, k, B, O);
+  LaneT<3> ln(P, Yl, lds, t, k, B, O);
   if (!B.partitioned && !ln.at<uint8_t>(Yl.o_kinit, 0)) {
     ln.clock = B.init_clock;
     ln.emit_pos = B.seq0;

@@ -341,9 +341,28 @@ SHP_HD inline Val load_col(const BatchView& B, const DevProg& P, int col, int64_
 }
 
 // ---------------------------------------------------------------------------
-// The lane.
+// The lane.  AS = address space of the state arena on the device: 1 = global (HBM), 3 = LDS,
+// 0 = generic (host builds).  Every state access goes through at(), which derives the element
+// pointer from an AS-qualified base, so the compiler emits global_* / ds_* instructions instead
+// of flat ones (flat accesses count against both the LDS and the memory wait counters).
 // ---------------------------------------------------------------------------
-struct Lane {
+template <int AS>
+struct LaneAS {
+  typedef char type;
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+template <>
+struct LaneAS<1> {
+  typedef __attribute__((address_space(1))) char type;
+};
+template <>
+struct LaneAS<3> {
+  typedef __attribute__((address_space(3))) char type;
+};
+#endif
+
+template <int AS>
+struct LaneT {
   const DevProg& P;
   const LaneLayout& Y;
   char* base;
@@ -356,7 +375,7 @@ struct Lane {
   int32_t err = 0;
   uint32_t ret;       // PostStateProcessor.isEventReturned bits (per key here)
 
-  SHP_HD Lane(const DevProg& p, const LaneLayout& y, char* b, int64_t l, int32_t k, const BatchView& bv,
+  SHP_HD LaneT(const DevProg& p, const LaneLayout& y, char* b, int64_t l, int32_t k, const BatchView& bv,
               const MatchOut& o)
       : P(p), Y(y), base(b), lane(l), key(k), B(bv), O(o), clock(0), emit_pos(0) {
     ret = at<uint32_t>(Y.o_ret, 0);
@@ -365,7 +384,9 @@ struct Lane {
 
   template <class T>
   SHP_HD T& at(int64_t off, int64_t i) const {
-    return ((T*)(base + off))[i * Y.L + lane];
+    typedef typename LaneAS<AS>::type C;
+    C* q = (C*)base + off + (i * Y.L + lane) * (int64_t)sizeof(T);
+    return *(T*)q;
   }
 
   // ------------------------------------------------------------ pools
@@ -569,7 +590,7 @@ struct Lane {
 
   // ------------------------------------------------------------ filter
   struct Res {
-    const Lane* L;
+    const LaneT* L;
     int se;
     SHP_HD Val value(int state, int index, int col) const {
       Val v{T_NULL, 0};
@@ -1426,5 +1447,7 @@ struct Lane {
     }
   }
 };
+
+using Lane = LaneT<0>;
 
 }  // namespace shp
