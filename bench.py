@@ -31,7 +31,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 BYTES_PER_EVENT = 16    # ts 8 + key 4 + price 4
-BYTES_PER_MATCH = {"pairs": 16,  # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
+BYTES_PER_MATCH = {"pairs32": 8,  # (e2 batch index, e2 seq - e1 seq) as two u32 (SHP_LAYOUT_PAIRS32)
+                   "pairs": 16,  # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
                    "agg": 12,    # (key u32, aggregate f64) per match (SHP_LAYOUT_AGG, C5)
                    "full": 16}
 KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_solve", "sw_expand",
@@ -67,6 +68,8 @@ def parse():
     ap.add_argument("--latency-batches", type=int, default=200,
                     help="§8d latency: batches of --latency-events, push + D2H of the match payload (0: skip)")
     ap.add_argument("--latency-events", type=int, default=16_000_000)
+    ap.add_argument("--pairs-layout", choices=["pairs32", "pairs"], default="pairs32",
+                    help="match payload of the 2-state sweep: 8-byte PAIRS32 (default) or 16-byte PAIRS")
     return ap.parse_args()
 
 
@@ -104,11 +107,11 @@ def main():
     cap = int(N * 1.08) + 4096 if G > 1 else N
     force = {"auto": 0, "general": 1, "scan": 2}[a.path]
     sweep = force == 0 and _sweep_shape(cq, local, K_local)
-    layout = ("agg" if "aggregate" in cq.program else "pairs") if sweep else "full"
+    layout = ("agg" if "aggregate" in cq.program else a.pairs_layout) if sweep else "full"
     eng = native.HipEngine(cq.program_json(), 0, max_keys=K_local, max_batch=cap, max_matches=cap,
                            device=local, force_general=force, profile_kernels=True,
                            match_layout={"agg": native.LAYOUT_AGG, "pairs": native.LAYOUT_PAIRS,
-                                         "full": native.LAYOUT_FULL}[layout])
+                                         "pairs32": native.LAYOUT_PAIRS32, "full": native.LAYOUT_FULL}[layout])
     L = native.lib()
     steps = a.warmup + a.steps
 
@@ -293,33 +296,51 @@ def main():
 def batch_latency(eng, L, native, spec, K, layout, n, batches, start):
     """SURVEY §8d latency: batches of n events (device-resident input, generated untimed), each
     timed from shp_push_batch_device entry until its match payload (pairs, or (key, aggregate)
-    rows) is in host memory (hipMemcpy to pageable memory), over `batches` batches."""
+    rows) is in host memory, over `batches` batches.  The payload lands in page-locked memory
+    (shp_host_alloc = hipHostMalloc, as a Java host would pin its receive segment with
+    shp_host_register); the same batches into pageable memory are reported beside it."""
     import torch
     bufs = [(torch.empty(n, dtype=torch.int64, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
              torch.empty(n, dtype=torch.float32, device="cuda")) for _ in range(2)]
     per = BYTES_PER_MATCH[layout]
-    host = np.empty(int(n * 1.1) * 2, dtype=np.int64)
-    lat = []
-    for b in range(batches):
-        ts, key, price = bufs[b & 1]
-        assert L.shp_synth_fill(spec.config, start + b * n, n, K, 1, int(spec.dense), ts.data_ptr(), key.data_ptr(),
-                                price.data_ptr(), None, None, None) == 0
-        torch.cuda.synchronize()
-        colp = (ctypes.c_void_p * 1)(price.data_ptr())
-        bt = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), None, ctypes.cast(colp, ctypes.c_void_p), None)
-        mt = native.ShpMatches()
-        t0 = time.perf_counter()
-        rc = L.shp_push_batch_device(eng.h, ctypes.byref(bt), ctypes.byref(mt))
-        if rc != 0:
-            raise native.ShpError(rc, L.shp_last_error(eng.h).decode())
-        if layout == "agg":
-            L.shp_dev_to_host(host.ctypes.data, mt.key, mt.m * 4)
-            L.shp_dev_to_host(host.ctypes.data + mt.m * 4, mt.agg, mt.m * 8)
-        else:
-            L.shp_dev_to_host(host.ctypes.data, mt.refs, mt.m * 16)
-        lat.append((time.perf_counter() - t0) * 1e3)
+    hbytes = int(n * 1.1) * 16
+    pinned = L.shp_host_alloc(hbytes)
+    if not pinned:
+        raise RuntimeError("shp_host_alloc failed")
+    pageable = np.empty(hbytes // 8, dtype=np.int64)
+    res = {}
+    try:
+        for kind, dst in (("pinned", pinned), ("pageable", pageable.ctypes.data)):
+            lat = []
+            for b in range(batches):
+                ts, key, price = bufs[b & 1]
+                assert L.shp_synth_fill(spec.config, start + b * n, n, K, 1, int(spec.dense), ts.data_ptr(),
+                                        key.data_ptr(), price.data_ptr(), None, None, None) == 0
+                torch.cuda.synchronize()
+                colp = (ctypes.c_void_p * 1)(price.data_ptr())
+                bt = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), None, ctypes.cast(colp, ctypes.c_void_p), None)
+                mt = native.ShpMatches()
+                t0 = time.perf_counter()
+                rc = L.shp_push_batch_device(eng.h, ctypes.byref(bt), ctypes.byref(mt))
+                if rc != 0:
+                    raise native.ShpError(rc, L.shp_last_error(eng.h).decode())
+                if mt.m * per > hbytes:
+                    raise RuntimeError("latency host buffer too small")
+                if layout == "agg":
+                    assert L.shp_dev_to_host(dst, mt.key, mt.m * 4) == 0
+                    assert L.shp_dev_to_host(dst + mt.m * 4, mt.agg, mt.m * 8) == 0
+                else:
+                    assert L.shp_dev_to_host(dst, mt.refs, mt.m * per) == 0
+                lat.append((time.perf_counter() - t0) * 1e3)
+            res[kind] = lat
+            start += batches * n
+    finally:
+        L.shp_host_free(pinned)
+    pl, pg = res["pinned"], res["pageable"]
     return {"batch_events": n, "batches": batches, "bytes_per_match_to_host": per,
-            "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+            "p50_ms": float(np.percentile(pl, 50)), "p99_ms": float(np.percentile(pl, 99)),
+            "host_buffer": "page-locked (shp_host_alloc)",
+            "pageable_p50_ms": float(np.percentile(pg, 50)), "pageable_p99_ms": float(np.percentile(pg, 99)),
             "what": "shp_push_batch_device entry -> match payload in host memory"}
 
 

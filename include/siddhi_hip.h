@@ -53,8 +53,8 @@ typedef struct shp_config {
   int32_t force_general;   /* 0 auto; 1 general NFA lanes only; 2 no sweep path (scan kernels or
                               lanes); 3 sweep path whenever the shape allows (any key count) */
   int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
-  int32_t match_layout;    /* SHP_LAYOUT_FULL (0), SHP_LAYOUT_PAIRS (1) or SHP_LAYOUT_AGG (2);
-                              PAIRS and AGG need the sweep path */
+  int32_t match_layout;    /* SHP_LAYOUT_FULL (0), SHP_LAYOUT_PAIRS (1), SHP_LAYOUT_AGG (2) or
+                              SHP_LAYOUT_PAIRS32 (3); PAIRS, PAIRS32 and AGG need the sweep path */
 } shp_config;
 
 /* Match layouts. FULL: every field of shp_matches is valid. PAIRS (2-state sweep path,
@@ -63,6 +63,10 @@ typedef struct shp_config {
  * key/ts = those of event refs[2i+1] in the pushed batch. shp_fetch_matches expands them. */
 #define SHP_LAYOUT_FULL 0
 #define SHP_LAYOUT_PAIRS 1
+/* PAIRS32 (as PAIRS, half the bytes): `refs` holds m pairs of uint32 (e2's index in the pushed
+ * batch, e2 seq - e1 seq): e2 seq = batch seq0 + index, e1 seq = e2 seq - delta.  A match whose
+ * events are 2^32 or more events apart fails the push with SHP_ERR_UNSUPPORTED. */
+#define SHP_LAYOUT_PAIRS32 3
 /* AGG (sweep path, program with an "aggregate" select item): the selector's running aggregate
  * is computed on the device (replaces QuerySelector.processInBatchNoGroupBy with
  * AvgAttributeAggregatorExecutor / Sum / Count, core/query/selector/QuerySelector.java:271-313).
@@ -97,7 +101,7 @@ typedef struct shp_matches {
   const int64_t* ref_off;
   const int16_t* slot_len;
   const int64_t* refs;
-  int32_t layout;          /* SHP_LAYOUT_FULL, SHP_LAYOUT_PAIRS or SHP_LAYOUT_AGG (see above) */
+  int32_t layout;          /* SHP_LAYOUT_FULL, SHP_LAYOUT_PAIRS, SHP_LAYOUT_AGG or SHP_LAYOUT_PAIRS32 */
   const double* agg;       /* SHP_LAYOUT_AGG: the aggregate's value per match */
 } shp_matches;
 
@@ -143,6 +147,12 @@ int shp_shard_partition_soa(int64_t n, const int64_t* ts, const int32_t* key, co
 void* shp_dev_alloc(int64_t bytes);
 int shp_dev_free(void* p);
 int shp_dev_to_host(void* dst, const void* src, int64_t bytes);
+/* Page-locked host memory for match payloads (hipHostMalloc / hipHostRegister): a D2H copy into it
+ * runs at DMA rate.  A Java host pins its receive MemorySegment once with shp_host_register. */
+void* shp_host_alloc(int64_t bytes);
+int shp_host_free(void* p);
+int shp_host_register(void* p, int64_t bytes);
+int shp_host_unregister(void* p);
 /* Device time (ms) of the last push measured with HIP events on the engine stream:
  * which = "total" | "partition" | "nfa" | a kernel name (needs cfg.profile_kernels), e.g.
  * "radix_sort", "nfa_lanes", "fast_search", "fast_emit". */

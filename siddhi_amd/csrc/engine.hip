@@ -329,14 +329,15 @@ struct shp_engine {
     if (fast && want_sweep && SweepState::shape_ok(comp.P, comp.fast) &&
         SweepState::build_map(cfg.max_keys, nown, kmap))
       fast = 2;
-    if (cfg.match_layout == SHP_LAYOUT_PAIRS && fast != 2)
-      throw CompileError(-2, "match_layout PAIRS needs the sweep path");
+    if ((cfg.match_layout == SHP_LAYOUT_PAIRS || cfg.match_layout == SHP_LAYOUT_PAIRS32) && fast != 2)
+      throw CompileError(-2, "match_layout PAIRS / PAIRS32 needs the sweep path");
     if (cfg.match_layout == SHP_LAYOUT_AGG) {
       // the aggregate reads e2's value: the sweep's single predicate column (count: none)
       const bool col_ok = comp.agg_fn == 3 || (comp.agg_state == 1 && comp.agg_col == 0 && comp.P.ncol == 1);
       if (fast != 2 || !comp.agg_fn || !col_ok)
         throw CompileError(-2, "match_layout AGG needs the sweep path and an avg/sum/count over e2's filtered column");
-    } else if (cfg.match_layout != SHP_LAYOUT_FULL && cfg.match_layout != SHP_LAYOUT_PAIRS) {
+    } else if (cfg.match_layout != SHP_LAYOUT_FULL && cfg.match_layout != SHP_LAYOUT_PAIRS &&
+               cfg.match_layout != SHP_LAYOUT_PAIRS32) {
       throw CompileError(-1, "unknown match_layout");
     }
     kt.enabled = cfg.profile_kernels != 0;
@@ -380,6 +381,7 @@ struct shp_engine {
     if (fast == 2) {
       sw.create(comp.P, comp.fast, cfg.max_keys, cap, nown, kmap, stream);
       if (cfg.match_layout == SHP_LAYOUT_AGG) sw.enable_agg(comp.agg_fn, cfg.max_keys, kmap, stream);
+      sw.D.p32 = cfg.match_layout == SHP_LAYOUT_PAIRS32;
 #ifdef SHP_SW_STAMPS
       HIP_OK(hipMalloc((void**)&sw.D.stamps, (size_t)nown * 8 * sizeof(unsigned long long)));
       HIP_OK(hipMemset(sw.D.stamps, 0, (size_t)nown * 8 * sizeof(unsigned long long)));
@@ -515,6 +517,8 @@ struct shp_engine {
       if (herr & SWE_MONO) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state fast path");
       if (herr & SWE_RANGE) return fail(SHP_ERR_UNSUPPORTED, "timestamps span more than 2^49 ms on the sweep path");
       if (herr & SWE_AGGNULL) return fail(SHP_ERR_UNSUPPORTED, "null value in the aggregated column (match_layout AGG)");
+      if (herr & SWE_P32)
+        return fail(SHP_ERR_UNSUPPORTED, "a match spans 2^32 or more events (match_layout PAIRS32; use PAIRS)");
       return fail(SHP_ERR_CAPACITY, "per-key table capacity exceeded (code " + std::to_string(herr) + ")");
     }
     return SHP_OK;
@@ -630,7 +634,7 @@ struct shp_engine {
   void ensure_expanded() {
     if (fast != 2 || expanded || cfg.match_layout == SHP_LAYOUT_AGG) return;
     MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs, d_magg};
-    sw.expand(lastB, lastKey, O, stream, kt);
+    sw.expand(lastB, lastKey, O, stream, kt, last_m);
     HIP_OK(hipStreamSynchronize(stream));
     expanded = true;
   }
@@ -666,7 +670,7 @@ struct shp_engine {
       out->agg = d_magg;
       return;
     }
-    out->layout = expanded ? SHP_LAYOUT_FULL : SHP_LAYOUT_PAIRS;
+    out->layout = expanded ? SHP_LAYOUT_FULL : cfg.match_layout;
     out->m = last_m;
     out->num_states = comp.P.nstates;
     out->key = d_mkey;

@@ -68,6 +68,7 @@ constexpr int SWE_KEYS = 1 << 20;   // key id outside [0, max_keys)
 constexpr int SWE_MONO = 1 << 21;   // ts decreases within a key
 constexpr int SWE_RANGE = 1 << 23;  // ts outside base +- 2^49 ms
 constexpr int SWE_AGGNULL = 1 << 24; // SHP_LAYOUT_AGG: a closing event's aggregated value is null
+constexpr int SWE_P32 = 1 << 25;     // SHP_LAYOUT_PAIRS32: e2 seq - e1 seq >= 2^32
 
 // 16-byte record.  kt: [63:56] local key (0xFF = none), [55] carried, [54] null,
 // [49:0] ts - base + 2^49.  ref: batch index (events) or carry slot (carried).
@@ -148,6 +149,7 @@ struct SweepDev {
   // running per-key state (sum, count as doubles: exact integers to 2^53) and the owner-local
   // key -> partition key map for the output rows
   int32_t agg;
+  int32_t p32;           // SHP_LAYOUT_PAIRS32: (e2 index in the batch, e2 seq - e1 seq) as two u32
   double* agg_s;         // nown * SW_LK
   double* agg_c;
   int32_t* inv;          // nown * SW_LK
@@ -1088,7 +1090,15 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
         const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
         const int64_t sq = B.seq0 + S.ref[q];
         const uint64_t slot = gb + off16[q] + (c - 1 - later);
-        if (slot < (uint64_t)O.cap) *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
+        if (slot < (uint64_t)O.cap) {
+          if (D.p32) {
+            const int64_t dq = sq - si;  // >= 1
+            if (dq >= (1ll << 32)) e |= SWE_P32;
+            reinterpret_cast<uint2*>(O.refs)[slot] = make_uint2(S.ref[q], (uint32_t)dq);
+          } else {
+            *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
+          }
+        }
       }
     }
     cur = nx;
@@ -1127,12 +1137,22 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
   if (e) atomicOr(err, e);
 }
 
-// full match records from the (i, j) pairs (shp_push_batch / shp_fetch_matches)
-__global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchOut O) {
+// full match records from the (i, j) pairs (shp_push_batch / shp_fetch_matches).  p32: the
+// pairs are SHP_LAYOUT_PAIRS32 (e2 batch index, e2 seq - e1 seq), staged by the caller in O.pos
+// (8 bytes per match); thread i reads its pair before it writes O.pos[i].
+__global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchOut O, int p32) {
   const int64_t m = min((int64_t)*O.count, O.cap);
   if (blockIdx.x == 0 && threadIdx.x == 0) O.count[1] = 2ull * (unsigned long long)m;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t j = O.refs[2 * i + 1];
+    int64_t j;
+    if (p32) {
+      const uint2 pr = reinterpret_cast<const uint2*>(O.pos)[i];
+      j = B.seq0 + (int64_t)pr.x;
+      O.refs[2 * i] = j - (int64_t)pr.y;
+      O.refs[2 * i + 1] = j;
+    } else {
+      j = O.refs[2 * i + 1];
+    }
     int64_t g = j - B.seq0;
     O.key[i] = B.partitioned ? key[g] : 0;
     O.ts[i] = B.ts[g];
@@ -1439,9 +1459,12 @@ struct SweepState {
     kt.mark(nullptr, s);
   }
 
-  void expand(const BatchView& B, const int32_t* key, const MatchOut& O, hipStream_t s, KTimer& kt) {
+  void expand(const BatchView& B, const int32_t* key, const MatchOut& O, hipStream_t s, KTimer& kt,
+              int64_t m_host = -1) {
+    if (D.p32 && m_host > 0)  // stage the 8-byte pairs where k_sw_expand reads them
+      (void)hipMemcpyAsync(O.pos, O.refs, (size_t)m_host * 8, hipMemcpyDeviceToDevice, s);
     kt.mark("sw_expand", s);
-    k_sw_expand<<<2048, 256, 0, s>>>(B, key, O);
+    k_sw_expand<<<2048, 256, 0, s>>>(B, key, O, D.p32);
     kt.mark(nullptr, s);
   }
 };

@@ -88,3 +88,15 @@ extern "C" int shp_dev_free(void* p) { return hipFree(p) == hipSuccess ? 0 : -5;
 extern "C" int shp_dev_to_host(void* dst, const void* src, int64_t bytes) {
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -5;
 }
+// Page-locked host memory for match payloads: a D2H copy into it runs at the DMA engine's rate
+// instead of through a pageable bounce buffer.  (A Java host would pin its receive segment once
+// with shp_host_register, which wraps hipHostRegister.)
+extern "C" void* shp_host_alloc(int64_t bytes) {
+  void* p = nullptr;
+  return hipHostMalloc(&p, bytes > 0 ? bytes : 1, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+extern "C" int shp_host_free(void* p) { return hipHostFree(p) == hipSuccess ? 0 : -5; }
+extern "C" int shp_host_register(void* p, int64_t bytes) {
+  return hipHostRegister(p, (size_t)bytes, hipHostRegisterDefault) == hipSuccess ? 0 : -5;
+}
+extern "C" int shp_host_unregister(void* p) { return hipHostUnregister(p) == hipSuccess ? 0 : -5; }

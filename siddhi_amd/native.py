@@ -24,7 +24,8 @@ SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACIT
 SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches",
            "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
-           "shp_dev_to_host", "shp_snapshot", "shp_restore", "shp_shard_workspace_bytes",
+           "shp_dev_to_host", "shp_host_alloc", "shp_host_free", "shp_host_register",
+           "shp_host_unregister", "shp_snapshot", "shp_restore", "shp_shard_workspace_bytes",
            "shp_shard_partition", "shp_shard_unpack", "shp_shard_partition_soa"]
 
 
@@ -34,7 +35,7 @@ class ShpConfig(ctypes.Structure):
                 ("force_general", ctypes.c_int32), ("profile_kernels", ctypes.c_int32),
                 ("match_layout", ctypes.c_int32)]
 
-LAYOUT_FULL, LAYOUT_PAIRS, LAYOUT_AGG = 0, 1, 2
+LAYOUT_FULL, LAYOUT_PAIRS, LAYOUT_AGG, LAYOUT_PAIRS32 = 0, 1, 2, 3
 
 
 class ShpBatch(ctypes.Structure):
@@ -85,6 +86,11 @@ def lib():
         L.shp_dev_alloc.argtypes = [ctypes.c_int64]
         L.shp_dev_free.argtypes = [ctypes.c_void_p]
         L.shp_dev_to_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        L.shp_host_alloc.restype = ctypes.c_void_p
+        L.shp_host_alloc.argtypes = [ctypes.c_int64]
+        L.shp_host_free.argtypes = [ctypes.c_void_p]
+        L.shp_host_register.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        L.shp_host_unregister.argtypes = [ctypes.c_void_p]
         L.shp_snapshot.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
         L.shp_restore.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         L.shp_shard_workspace_bytes.restype = ctypes.c_int64

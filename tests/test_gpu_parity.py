@@ -379,3 +379,65 @@ def test_filter_functions_vs_oracle(app, general):
         outs.append(per_key(eng.fetch()))
     assert compare(*outs) is None, compare(*outs)
     assert sum(len(x) for x in outs[0].values()) > 100
+
+
+@pytest.mark.parametrize("keys", [1_250, 10_000])
+def test_pairs32_layout_vs_oracle(keys):
+    """SHP_LAYOUT_PAIRS32 (half the match bytes): through shp_push_batch (expanded on fetch)
+    bit-exact against the oracle, with state carried across split pushes."""
+    from siddhi_amd.native import LAYOUT_PAIRS32
+    cq = program_for(2)
+    g = small_stream(2, 1_000_000, keys)
+    a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    eng = hip(3, max_keys=keys, max_batch=1 << 19, match_layout=LAYOUT_PAIRS32)(cq.program_json(), 0)
+    assert eng.path == 2
+    b = per_key(run(eng, cq, g, 333_331))
+    assert compare(a, b) is None
+    assert sum(len(v) for v in a.values()) > 100_000
+
+
+def test_pairs32_device_pairs_decode_to_pairs():
+    """The raw PAIRS32 device output decodes (e2 = seq0 + index, e1 = e2 - delta) to exactly the
+    PAIRS layout's (e1 seq, e2 seq) records, push after push."""
+    import ctypes
+
+    import torch
+    from siddhi_amd import native
+    L = native.lib()
+    cq = program_for(2)
+    n, K = 400_000, 2_000
+    engs = {lay: native.HipEngine(cq.program_json(), 0, max_keys=K, max_batch=n, max_matches=n, force_general=3,
+                                  match_layout=lay) for lay in (native.LAYOUT_PAIRS, native.LAYOUT_PAIRS32)}
+    dev = torch.device("cuda", 0)
+    for b in range(3):
+        ts = torch.empty(n, dtype=torch.int64, device=dev)
+        key = torch.empty(n, dtype=torch.int32, device=dev)
+        price = torch.empty(n, dtype=torch.float32, device=dev)
+        assert L.shp_synth_fill(2, b * n, n, K, 1, 0, ts.data_ptr(), key.data_ptr(), price.data_ptr(),
+                                None, None, None) == 0
+        torch.cuda.synchronize()
+        colp = (ctypes.c_void_p * 1)(price.data_ptr())
+        got = {}
+        for lay, eng in engs.items():
+            bt = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), None, ctypes.cast(colp, ctypes.c_void_p), None)
+            mt = native.ShpMatches()
+            assert L.shp_push_batch_device(eng.h, ctypes.byref(bt), ctypes.byref(mt)) == 0
+            assert mt.layout == lay
+            if lay == native.LAYOUT_PAIRS:
+                h = np.empty(2 * mt.m, np.int64)
+                assert L.shp_dev_to_host(h.ctypes.data, mt.refs, mt.m * 16) == 0
+                got[lay] = h.reshape(-1, 2)
+            else:
+                h = np.empty(2 * mt.m, np.uint32)
+                assert L.shp_dev_to_host(h.ctypes.data, mt.refs, mt.m * 8) == 0
+                h = h.reshape(-1, 2).astype(np.int64)
+                e2 = b * n + h[:, 0]
+                got[lay] = np.stack([e2 - h[:, 1], e2], axis=1)
+        p64, p32 = got[native.LAYOUT_PAIRS], got[native.LAYOUT_PAIRS32]
+        assert len(p64) > 100_000
+        # same match set; per e2 (hence per key) the same order of e1s
+        o64 = np.lexsort((np.arange(len(p64)), p64[:, 1]))
+        o32 = np.lexsort((np.arange(len(p32)), p32[:, 1]))
+        assert (p64[o64] == p32[o32]).all()
+    for eng in engs.values():
+        eng.close()
