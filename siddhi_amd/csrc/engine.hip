@@ -792,7 +792,26 @@ int shp_engine_create(const char* json, const shp_config* cfg, shp_engine** out)
   return SHP_OK;
 }
 
+// The engine's HIP calls run on its own device whatever thread calls in: HIP's current device
+// is per thread (a Java host, or bench.py's worker thread, may call from a thread whose
+// current device is another GPU).  The caller's current device is restored on return.
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  int restore_to(int dev) const { return prev >= 0 && prev != dev ? prev : -1; }
+};
+
 static int guarded(shp_engine* e, const std::function<int()>& f) {
+  const DeviceScope ds(e->cfg.device);
+  struct Restore {
+    int d;
+    ~Restore() {
+      if (d >= 0) (void)hipSetDevice(d);
+    }
+  } restore{ds.restore_to(e->cfg.device)};
   try {
     return f();
   } catch (DevError& de) {
@@ -895,5 +914,11 @@ int shp_restore(shp_engine* e, const void* buf, size_t len) {
 
 const char* shp_last_error(const shp_engine* e) { return e ? e->err.c_str() : "null engine"; }
 
-void shp_engine_destroy(shp_engine* e) { delete e; }
+void shp_engine_destroy(shp_engine* e) {
+  if (!e) return;
+  const DeviceScope ds(e->cfg.device);
+  const int back = ds.restore_to(e->cfg.device);
+  delete e;
+  if (back >= 0) (void)hipSetDevice(back);
+}
 }
