@@ -222,10 +222,14 @@ struct shp_engine {
   uint32_t *d_kcnt = nullptr, *d_kbeg = nullptr;
   void* d_tmp = nullptr;
   size_t tmp_bytes = 0;
-  int* d_err = nullptr;
+  int* d_err = nullptr;  // = d_status + 2
+  // per-push status block on the device (match counts [0..1], error bits [2]) and its
+  // page-locked host mirror (+ the engine clock [3]): one memset and two small DMA reads per push
+  unsigned long long* d_status = nullptr;
+  unsigned long long* h_status = nullptr;
   // match table
   int64_t mcap = 0, rcap = 0;
-  unsigned long long* d_mcount = nullptr;
+  unsigned long long* d_mcount = nullptr;  // = d_status
   int32_t* d_mkey = nullptr;
   int64_t *d_mts = nullptr, *d_mpos = nullptr, *d_moff = nullptr, *d_refs = nullptr;
   int8_t* d_mtype = nullptr;
@@ -270,8 +274,8 @@ struct shp_engine {
     F(d_kcnt);
     F(d_kbeg);
     F(d_tmp);
-    F(d_err);
-    F(d_mcount);
+    F(d_status);
+    if (h_status) (void)hipHostFree(h_status);
     F(d_mkey);
     F(d_mts);
     F(d_mpos);
@@ -356,10 +360,12 @@ struct shp_engine {
     alloc(d_perm, cap);
     alloc(d_kcnt, cfg.max_keys + 1);
     alloc(d_kbeg, cfg.max_keys + 1);
-    alloc(d_err, 1);
+    alloc(d_status, 4);
+    d_err = reinterpret_cast<int*>(d_status + 2);
+    d_mcount = d_status;
+    HIP_OK(hipHostMalloc((void**)&h_status, 4 * sizeof(unsigned long long), hipHostMallocDefault));
     mcap = cfg.max_matches;
     rcap = mcap * comp.P.nstates * 2 + 64;
-    alloc(d_mcount, 2);
     alloc(d_mkey, mcap);
     alloc(d_mts, mcap);
     alloc(d_mpos, mcap);
@@ -419,8 +425,7 @@ struct shp_engine {
       HIP_OK(hipMemsetAsync(d_stream, 0, n * 4, stream));
       x_stream = d_stream;
     }
-    HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), stream));
-    HIP_OK(hipMemsetAsync(d_mcount, 0, 2 * sizeof(unsigned long long), stream));
+    HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));  // counts + error bits
     kt.begin_push();
     HIP_OK(hipEventRecord(ev0, stream));
     BatchView B{};
@@ -437,7 +442,8 @@ struct shp_engine {
       B.nulls[c] = in ? (in->nulls ? in->nulls[c] : nullptr) : d_nulls[c];
     }
     MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs, d_magg};
-    int64_t tsmax = INT64_MIN;
+    int64_t* h_tsmax = reinterpret_cast<int64_t*>(h_status + 3);
+    *h_tsmax = INT64_MIN;  // the previous push has completed (stream synchronised)
     if (fast == 2) {
       // sweep: no clock scan, no global sort (the engine clock is the running max of ts)
       HIP_OK(hipEventRecord(ev1, stream));
@@ -449,7 +455,7 @@ struct shp_engine {
         sw.expand(B, x_key, O, stream, kt);
         expanded = true;
       }
-      HIP_OK(hipMemcpyAsync(&tsmax, sw.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipMemcpyAsync(h_tsmax, sw.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
     } else {
       int gb = (int)std::min<int64_t>((n + 255) / 256, 2048);
       if (gb < 1) gb = 1;
@@ -491,15 +497,16 @@ struct shp_engine {
         }
         kt.mark(nullptr, stream);
       }
-      if (n > 0) HIP_OK(hipMemcpyAsync(&tsmax, d_rmax + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+      if (n > 0) HIP_OK(hipMemcpyAsync(h_tsmax, d_rmax + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
     }
     HIP_OK(hipEventRecord(ev2, stream));
     HIP_OK(hipGetLastError());
-    int herr = 0;
-    unsigned long long cnt[2];
-    HIP_OK(hipMemcpyAsync(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipMemcpyAsync(cnt, d_mcount, sizeof(cnt), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
+    int herr = 0;
+    std::memcpy(&herr, h_status + 2, sizeof(int));
+    const unsigned long long cnt[2] = {h_status[0], h_status[1]};
+    const int64_t tsmax = *h_tsmax;
     float a = 0, b = 0;
     HIP_OK(hipEventElapsedTime(&a, ev0, ev1));
     HIP_OK(hipEventElapsedTime(&b, ev1, ev2));
