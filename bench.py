@@ -58,7 +58,10 @@ def parse():
     ap.add_argument("--events", type=int, default=100_000_000, help="events per GPU per step")
     ap.add_argument("--keys", type=int, default=0, help="keys (default: the config's, C2 = 10k)")
     ap.add_argument("--config", default="2", help="SURVEY §8d config: 2 (headline), 1, 3b, 4, 5")
-    ap.add_argument("--cpu-sample", type=int, default=2_500_000)
+    ap.add_argument("--cpu-sample", type=int, default=2_500_000, help="events per CPU thread")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the key-sharded CPU baseline (default: the box's CPU share, "
+                         "OMP_NUM_THREADS, else os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=["auto", "general", "scan"], default="auto",
                     help="auto = sweep path (default); scan = round-1 scan kernels; general = NFA lanes")
@@ -247,7 +250,9 @@ def main():
                 traffic = None
         cpu = None
         if not a.no_cpu_baseline and G == 1:
-            cpu = cpu_baseline(cq, a.cpu_sample, K, spec.config)
+            cpu = cpu_baseline(cq, a.cpu_sample, K, spec.config, a.cpu_threads)
+        step_ms = elapsed / a.steps * 1e3
+        step_achieved = alg_bytes / (step_ms * 1e-3) / 1e9
         line = {
             "metric": "input events/sec, keyed pattern query, 1/2/4/8 MI355X; p99 batch latency",
             "value": value,
@@ -284,7 +289,12 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": alg_bytes,
+                "bytes_per_event": BYTES_PER_EVENT,
+                "bytes_per_match": BYTES_PER_MATCH[layout],
                 "kernel_ms_per_launch": {k: v / a.steps for k, v in sorted(kernel_ms.items()) if v > 0},
+                # the same algorithmic bytes over the whole step (every kernel of the push, plus the
+                # host round trip), the fraction the headline `value` corresponds to
+                "step": {"achieved": step_achieved, "frac": step_achieved / HBM_PEAK_GBS, "ms": step_ms},
             },
             "cpu_baseline": cpu,
         }
@@ -354,19 +364,60 @@ def _sweep_shape(cq, device, keys):
         e.close()
 
 
-def cpu_baseline(cq, sample, keys, config=2):
-    """Oracle (C++ restatement of the reference semantics), one thread, first `sample` C2 events."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cq, sample, keys, config=2, threads=0):
+    """The oracle (C++ restatement of the reference semantics, oracle/liboracle.so) on the box's
+    host cores, two ways: one thread over the first `sample` events of the
+    stream, and key-sharded over T threads (one oracle engine per shard, keys k % T == t; each
+    ctypes call releases the GIL) over the first T * `sample` events.  The sharded rate is the
+    reported value; the single-thread run sits beside it."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from diff_util import run, small_stream
     from oracle.oracle import OracleEngine
-    g = small_stream(config, sample, keys)
+    if threads <= 0:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1, 64, keys))
+    g1 = small_stream(config, sample, keys)
     e = OracleEngine(cq.program_json(), 0)
     t = time.perf_counter()
-    mb = run(e, cq, g)
-    dt = time.perf_counter() - t
-    return {"value": sample / dt, "unit": "events/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample} events of the C{config} stream ({keys} keys), oracle/liboracle.so, "
-                      f"{len(mb['key'])} matches, {dt:.1f} s"}
+    mb = run(e, cq, g1)
+    dt1 = time.perf_counter() - t
+    single = {"value": sample / dt1, "cores": 1, "events": sample, "matches": int(len(mb["key"])), "s": dt1}
+    del e, mb, g1
+    total = sample * threads
+    g = small_stream(config, total, keys)
+    shard = g["key"] % threads
+    parts = [{k: v[shard == r] for k, v in g.items()} for r in range(threads)]
+    del g, shard
+    engines = [OracleEngine(cq.program_json(), 0) for _ in range(threads)]
+    out = [None] * threads
+
+    def work(r):
+        out[r] = run(engines[r], cq, parts[r])
+
+    ths = [threading.Thread(target=work, args=(r,)) for r in range(threads)]
+    t = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dtn = time.perf_counter() - t
+    nm = sum(len(o["key"]) for o in out)
+    return {"value": total / dtn, "unit": "events/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "cpus_visible": os.cpu_count(),
+            "sample": f"first {total} events of the C{config} stream ({keys} keys) key-sharded over {threads} "
+                      f"threads (one oracle/liboracle.so engine per shard, key % {threads}), {nm} matches, "
+                      f"{dtn:.1f} s; single thread: first {sample} events, {single['value']:.3e} events/s",
+            "single_thread": single}
 
 
 if __name__ == "__main__":

@@ -506,7 +506,11 @@ struct shp_engine {
     int herr = 0;
     std::memcpy(&herr, h_status + 2, sizeof(int));
     const unsigned long long cnt[2] = {h_status[0], h_status[1]};
-    const int64_t tsmax = *h_tsmax;
+    int64_t tsmax = *h_tsmax;
+    if (fast == 2) {  // the sweep's per-push max is kept as ts ^ 2^63 (0: no event)
+      const unsigned long long raw = h_status[3];
+      tsmax = raw ? (int64_t)(raw ^ (1ull << 63)) : INT64_MIN;
+    }
     float a = 0, b = 0;
     HIP_OK(hipEventElapsedTime(&a, ev0, ev1));
     HIP_OK(hipEventElapsedTime(&b, ev1, ev2));
@@ -514,15 +518,20 @@ struct shp_engine {
     last_ms_nfa = b;
     last_ms_total = a + b;
     kt.collect();
-    // carry the clock (running max of ts, playback)
-    if (tsmax != INT64_MIN && tsmax > clock) clock = tsmax;
-    if (!clock_only) seq += n;
     last_m = std::min<int64_t>((int64_t)cnt[0], mcap);
-    if (herr) {
+    if (!herr) {
+      // carry the clock (running max of ts, playback) and the sequence numbers: only a push that
+      // succeeded advances them (a failed push leaves the sweep path's state as it was)
+      if (tsmax != INT64_MIN && tsmax > clock) clock = tsmax;
+      if (!clock_only) seq += n;
+      if (fast == 2) sw.commit();
+    } else {
+      last_m = 0;
       if (herr & SWE_KEYS) return fail(SHP_ERR_KEYS, "partition key id >= max_keys");
       if (herr & E_OUT) return fail(SHP_ERR_OUTPUT, "match buffer too small for this batch (max_matches)");
-      if (herr & SWE_MONO) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state fast path");
-      if (herr & SWE_RANGE) return fail(SHP_ERR_UNSUPPORTED, "timestamps span more than 2^49 ms on the sweep path");
+      if (herr & SWE_MONO) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state scan kernels");
+      if (herr & SWE_RANGE)
+        return fail(SHP_ERR_UNSUPPORTED, "timestamps of one push (and the carried candidates) span 2^49 ms or more");
       if (herr & SWE_AGGNULL) return fail(SHP_ERR_UNSUPPORTED, "null value in the aggregated column (match_layout AGG)");
       if (herr & SWE_P32)
         return fail(SHP_ERR_UNSUPPORTED, "a match spans 2^32 or more events (match_layout PAIRS32; use PAIRS)");
@@ -543,17 +552,19 @@ struct shp_engine {
     if (fast == 2) {
       const SweepDev& D = sw.D;
       const int64_t no = D.nown, cc = (int64_t)no * SWS_CCAP;
-      v = {{D.c_n, (size_t)no * 4}, {D.c_ts, (size_t)cc * 8}, {D.c_seq, (size_t)cc * 8}, {D.c_v, (size_t)cc * 4},
-           {D.c_lk, (size_t)cc}, {D.c_null, (size_t)cc}, {D.lastts, (size_t)no * SW_LK * 8}, {D.tsmax, 8}};
+      const int c = D.cur;  // the committed copy
+      v = {{D.c_n[c], (size_t)no * 4}, {D.c_ts[c], (size_t)cc * 8}, {D.c_seq[c], (size_t)cc * 8},
+           {D.c_v[c], (size_t)cc * 4}, {D.c_lk[c], (size_t)cc}, {D.c_null[c], (size_t)cc},
+           {D.lastc[c], (size_t)no * SW_LK}};
       if (D.agg) {
-        v.push_back({D.agg_s, (size_t)no * SW_LK * 8});
-        v.push_back({D.agg_c, (size_t)no * SW_LK * 8});
+        v.push_back({D.agg_s[c], (size_t)no * SW_LK * 8});
+        v.push_back({D.agg_c[c], (size_t)no * SW_LK * 8});
       }
     } else if (fast == 1) {
       const FastDev& F = fs.F;
       v = {{F.c_seq, (size_t)nk * FCC * 8}, {F.c_ts, (size_t)nk * FCC * 8}, {F.c_val, (size_t)nk * FCC * 16},
            {F.c_null, (size_t)nk * FCC * 2}, {F.c_n, (size_t)nk * 4}, {F.c_match, (size_t)nk * FCC * 4},
-           {F.last_ts, (size_t)nk * 8}, {F.first_open, (size_t)nk * 4}};
+           {F.last_ts, (size_t)nk * 8}, {F.first_open, (size_t)nk * 4}, {F.last_cand, (size_t)nk}};
     } else {
       v = {{arena, (size_t)Y.bytes}};
     }
@@ -584,7 +595,7 @@ struct shp_engine {
     snap.assign(sizeof(SnapHeader) + payload, 0);
     SnapHeader h{};
     memcpy(h.magic, "SHPSNAP1", 8);
-    h.version = 1;
+    h.version = 2;
     h.path = fast;
     h.max_keys = cfg.max_keys;
     h.seq = seq;
@@ -610,7 +621,7 @@ struct shp_engine {
     SnapHeader h;
     if (!buf || len < sizeof h) return fail(SHP_ERR_ARG, "snapshot too short");
     memcpy(&h, buf, sizeof h);
-    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 1) return fail(SHP_ERR_ARG, "not a snapshot");
+    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 2) return fail(SHP_ERR_ARG, "not a snapshot (or of another version)");
     if (h.path != fast || h.max_keys != cfg.max_keys || h.program_hash != fnv1a(program))
       return fail(SHP_ERR_ARG, "snapshot is of a different query, path or key capacity");
     auto secs = state_sections();
@@ -776,6 +787,15 @@ extern "C" {
 
 int shp_engine_create(const char* json, const shp_config* cfg, shp_engine** out) {
   if (!json || !cfg || !out) return SHP_ERR_ARG;
+  // create binds the engine's device for its allocations; the caller's current device is restored
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  struct Restore {
+    int d;
+    ~Restore() {
+      if (d >= 0) (void)hipSetDevice(d);
+    }
+  } restore{prev};
   auto* e = new shp_engine();
   try {
     e->create(json, cfg);

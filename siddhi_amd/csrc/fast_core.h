@@ -9,6 +9,7 @@
 // Candidates are independent, so the work is data-parallel over events:
 //   gather  key-sorted SoA (ts, predicate columns) + per-key ts monotonicity check
 //   search  one item per candidate: forward scan to its closing event
+//   seq     keys whose ts decrease: the processor chain replayed exactly, one item per key
 //   emit    one item per closing event: backward scan writes (j, i) in order
 //   carry   per key: candidates still open at the batch end -> next batch
 // These bodies are SHP_HD so tests/hostcheck can run them under AddressSanitizer.
@@ -49,6 +50,8 @@ struct FastDev {
   int64_t within;
   int32_t nk;            // keys
   int32_t nv;            // predicate columns (<= 2)
+  int32_t fstream;       // the query's stream (program stream index)
+  int32_t pad_;
   // carry (per key)
   int64_t* c_seq;        // nk * FCC
   int64_t* c_ts;
@@ -57,6 +60,9 @@ struct FastDev {
   int32_t* c_n;          // nk
   int32_t* c_match;      // nk * FCC : matched sorted position, -1 dead, -2 open
   int64_t* last_ts;      // nk, INT64_MIN when unseen
+  uint8_t* slow;         // nk: the key's ts decrease in this batch -> exact replay (fast_seq_item)
+  uint8_t* last_cand;    // nk: the key's latest event opened a candidate (the last carried one; it
+                         // is on the new-and-every list when the next event arrives)
   // batch scratch
   int64_t* s_ts;         // n (key-sorted)
   int64_t* s_val;        // n * 2
@@ -137,8 +143,9 @@ SHP_HD inline void fast_gather_item(const DevProg& P, const BatchView& B, const 
   uint32_t k = skey[p];
   if (k < (uint32_t)F.nk) {
     int64_t prev = (p > 0 && skey[p - 1] == k) ? B.ts[perm[p - 1]] : F.last_ts[k];
-    if (t < prev) at_or_i32(err, 1 << 21);
+    if (t < prev) F.slow[k] = 1;  // the closed form needs non-decreasing ts: replay the key exactly
   }
+  (void)err;
 }
 
 // forward scan from `from` (sorted position) to `end` for the closing event of a candidate
@@ -159,8 +166,8 @@ SHP_HD inline int32_t fast_scan(const FastDev& F, const FVals& c, int64_t ti, in
 SHP_HD inline void fast_search_item(const BatchView& B, const FastDev& F, const uint32_t* perm, const uint32_t* skey,
                                     const uint32_t* kbeg, const uint32_t* kcnt, int64_t i, int fstream) {
   uint32_t k = skey[i];
-  if (k >= (uint32_t)F.nk || B.stream[perm[i]] != fstream) {
-    F.match[i] = -3;
+  if (k >= (uint32_t)F.nk || B.stream[perm[i]] != fstream || F.slow[k]) {
+    F.match[i] = -3;  // (a slow key's positions are set by fast_seq_item)
     return;
   }
   FVals c{F.s_val[2 * i], F.s_val[2 * i + 1], F.s_null[2 * i], F.s_null[2 * i + 1]};
@@ -180,7 +187,7 @@ SHP_HD inline void fast_search_carry_item(const BatchView& B, const FastDev& F, 
                                           const uint32_t* kbeg, const uint32_t* kcnt, int64_t c, int fstream) {
   int32_t k = (int32_t)(c / FCC);
   int32_t j = (int32_t)(c % FCC);
-  if (j >= F.c_n[k]) return;
+  if (j >= F.c_n[k] || F.slow[k]) return;
   if (kcnt[k] == 0) {
     F.c_match[c] = -2;
     return;
@@ -190,6 +197,71 @@ SHP_HD inline void fast_search_carry_item(const BatchView& B, const FastDev& F, 
   int32_t q = fast_scan(F, cv, F.c_ts[c], b, b + kcnt[k], fstream, B, perm);
   F.c_match[c] = q;
   if (q >= 0) at_add_u32(&F.nclose[q], 1u);
+}
+
+// Exact replay of one key whose timestamps decrease (the closed form above assumes they do not):
+// StreamPreStateProcessor.expireEvents (:326-361) expires the pending list from its head while
+// |ts - now| > within and stops at the first live partial; the new-and-every list (the candidate
+// the key's previous event opened) is expired whole; processAndReturn (:364-403) then tries every
+// pending partial in list order with no expiry test.  Writes the same match / c_match / nclose /
+// first_open the parallel items write for the other keys.
+SHP_HD inline void fast_seq_item(const FastDev& F, const BatchView& B, const uint32_t* perm, const uint32_t* kbeg,
+                                 const uint32_t* kcnt, int32_t k, int fstream) {
+  if (!F.slow[k]) return;
+  const int64_t b = kbeg[k], e = b + kcnt[k];
+  const int64_t cb = (int64_t)k * FCC;
+  const int cn = F.c_n[k];
+  for (int j = 0; j < cn; j++) F.c_match[cb + j] = -2;
+  for (int64_t i = b; i < e; i++) F.match[i] = -3;
+  // list entries: carried j as -(j + 1), batch positions as themselves
+  auto st = [&](int64_t x) -> int32_t& { return x < 0 ? F.c_match[cb + (-x - 1)] : F.match[x]; };
+  auto tsx = [&](int64_t x) -> int64_t { return x < 0 ? F.c_ts[cb + (-x - 1)] : F.s_ts[x]; };
+  auto valx = [&](int64_t x) -> FVals {
+    if (x < 0) {
+      const int64_t c = cb + (-x - 1);
+      return FVals{F.c_val[2 * c], F.c_val[2 * c + 1], F.c_null[2 * c], F.c_null[2 * c + 1]};
+    }
+    return FVals{F.s_val[2 * x], F.s_val[2 * x + 1], F.s_null[2 * x], F.s_null[2 * x + 1]};
+  };
+  auto nexte = [&](int64_t x) -> int64_t { return x < 0 ? (x == -(int64_t)cn ? b : x - 1) : x + 1; };
+  const int64_t first = cn > 0 ? -1 : b;
+  int64_t prevc = (cn > 0 && F.last_cand[k]) ? -(int64_t)cn : INT64_MIN;
+  uint32_t fo = 0xffffffffu;
+  for (int64_t q = b; q < e; q++) {
+    if (B.stream[perm[q]] != fstream) continue;  // other partition streams never reach the query
+    const int64_t tq = F.s_ts[q];
+    for (int64_t x = first; x != q; x = nexte(x)) {  // expireEvents: pending list from the head
+      if (st(x) != -2) continue;
+      if (x == prevc) break;
+      const int64_t d = tsx(x) - tq;
+      if (d > F.within || d < -F.within) st(x) = -1;
+      else break;
+    }
+    if (prevc != INT64_MIN && st(prevc) == -2) {  // ... and the new-and-every list, whole
+      const int64_t d = tsx(prevc) - tq;
+      if (d > F.within || d < -F.within) st(prevc) = -1;
+    }
+    const FVals ev{F.s_val[2 * q], F.s_val[2 * q + 1], F.s_null[2 * q], F.s_null[2 * q + 1]};
+    for (int64_t x = first; x != q; x = nexte(x)) {  // processAndReturn, list order
+      if (st(x) != -2) continue;
+      if (fast_pred(F.f2, valx(x), ev, true)) {
+        st(x) = (int32_t)q;
+        F.nclose[q] += 1;
+      }
+    }
+    if (fast_pred(F.f1, ev, ev, false)) {
+      F.match[q] = -2;
+      prevc = q;
+    } else {
+      prevc = INT64_MIN;
+    }
+  }
+  for (int64_t i = b; i < e; i++)
+    if (F.match[i] == -2) {
+      fo = (uint32_t)i;
+      break;
+    }
+  F.first_open[k] = fo;
 }
 
 SHP_HD inline void fast_emit_item(const FastDev& F, const BatchView& B, const MatchOut& O, const uint32_t* perm,
@@ -222,8 +294,9 @@ SHP_HD inline void fast_emit_item(const FastDev& F, const BatchView& B, const Ma
   // place forwards (ascending i)
   uint32_t nb = cnt - w;
   uint32_t placed = 0;
+  const bool slow = F.slow[k] != 0;  // no ts order to stop at
   for (int64_t i = q - 1; i >= (int64_t)kbeg[k] && placed < nb; i--) {
-    if (tq - F.s_ts[i] > F.within) break;
+    if (!slow && tq - F.s_ts[i] > F.within) break;
     if (F.match[i] == (int32_t)q) {
       put(B.seq0 + perm[i], w + nb - 1 - placed);
       placed++;
@@ -234,9 +307,15 @@ SHP_HD inline void fast_emit_item(const FastDev& F, const BatchView& B, const Ma
 SHP_HD inline void fast_carry_item(const FastDev& F, const BatchView& B, const uint32_t* perm, const uint32_t* kbeg,
                                    const uint32_t* kcnt, int32_t k, int* err) {
   uint32_t cnt = kcnt[k];
+  F.slow[k] = 0;
   if (cnt == 0) return;
   int64_t b = kbeg[k], e = b + cnt;
   F.last_ts[k] = F.s_ts[e - 1];
+  for (int64_t i = e - 1; i >= b; i--)  // the key's latest event of this query's stream
+    if (B.stream[perm[i]] == F.fstream) {
+      F.last_cand[k] = F.match[i] != -3 ? 1 : 0;
+      break;
+    }
   int64_t first_open = F.first_open[k] == 0xffffffffu ? e : (int64_t)F.first_open[k];
   F.first_open[k] = 0xffffffffu;
   int64_t base = (int64_t)k * FCC;

@@ -83,6 +83,12 @@ __global__ void k_fast_search(const DevProg* __restrict__ Pp, BatchView B, FastD
   for (int64_t c = p; c < (int64_t)F.nk * FCC; c += stride) fast_search_carry_item(B, F, perm, kbeg, kcnt, c, fstream);
 }
 
+__global__ void k_fast_seq(FastDev F, BatchView B, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ kbeg,
+                           const uint32_t* __restrict__ kcnt, int fstream) {
+  int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < F.nk) fast_seq_item(F, B, perm, kbeg, kcnt, k, fstream);
+}
+
 __global__ void k_fast_emit(FastDev F, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
                             const uint32_t* __restrict__ skey, const uint32_t* __restrict__ kbeg, int64_t n,
                             const unsigned long long* total, int* err) {
@@ -106,6 +112,8 @@ __global__ void k_fast_init(FastDev F) {
   if (k >= F.nk) return;
   F.c_n[k] = 0;
   F.last_ts[k] = INT64_MIN;
+  F.slow[k] = 0;
+  F.last_cand[k] = 0;
   F.first_open[k] = 0xffffffffu;
 }
 
@@ -119,7 +127,7 @@ struct FastState {
   unsigned long long* d_total = nullptr;
 
   void release() {
-    void* ps[] = {F.c_seq, F.c_ts, F.c_val, F.c_null, F.c_n, F.c_match, F.last_ts, F.s_ts,
+    void* ps[] = {F.c_seq, F.c_ts, F.c_val, F.c_null, F.c_n, F.c_match, F.last_ts, F.slow, F.last_cand, F.s_ts,
                   F.s_val, F.s_null, F.match, F.nclose, F.moff, F.first_open, d_total};
     for (void* p : ps)
       if (p) (void)hipFree(p);
@@ -180,6 +188,7 @@ struct FastState {
     F.nk = nk;
     F.nv = P.ncol;
     stream_ = fsh.stream;
+    F.fstream = fsh.stream;
     al(F.c_seq, (int64_t)nk * FCC);
     al(F.c_ts, (int64_t)nk * FCC);
     al(F.c_val, (int64_t)nk * FCC * 2);
@@ -187,6 +196,8 @@ struct FastState {
     al(F.c_n, nk);
     al(F.c_match, (int64_t)nk * FCC);
     al(F.last_ts, nk);
+    al(F.slow, nk);
+    al(F.last_cand, nk);
     al(F.s_ts, cap);
     al(F.s_val, cap * 2);
     al(F.s_null, cap * 2);
@@ -217,6 +228,8 @@ struct FastState {
     }
     kt.mark("fast_search", s);
     k_fast_search<<<gs, 256, 0, s>>>(dprog, B, F, perm, skey, kbeg, kcnt, n, stream_);
+    kt.mark("fast_seq", s);
+    k_fast_seq<<<(nk + 255) / 256, 256, 0, s>>>(F, B, perm, kbeg, kcnt, stream_);
     size_t tb = tmp_bytes;
     kt.mark("nclose_scan", s);
     (void)rocprim::exclusive_scan(tmp, tb, F.nclose, F.moff, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);

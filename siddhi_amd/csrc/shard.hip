@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -27,7 +28,7 @@ constexpr int SH_MAXG = 16;
 
 struct __attribute__((aligned(16))) ShRec {
   int64_t ts;
-  uint32_t key;
+  uint32_t key;  // packed form: stream << 24 | key / G; SoA form: key / G (full 32 bits)
   uint32_t v;
 };
 
@@ -76,6 +77,7 @@ __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __r
   __shared__ uint32_t lst[SH_MAXG + 1];  // this round's LDS start per destination
   __shared__ ShRec srec[SH_ROUND];
   __shared__ uint8_t sdst[SH_ROUND];
+  __shared__ int32_t sstp[SOA ? SH_ROUND : 1];   // SoA: stream id by destination-grouped slot
   const int t = blockIdx.x;
   const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -86,14 +88,17 @@ __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __r
     __syncthreads();
     ShRec rec[SH_SUB];
     uint32_t dst[SH_SUB], rk[SH_SUB];
+    int32_t sid[SH_SUB];
 #pragma unroll
     for (int s = 0; s < SH_SUB; s++) {  // wave w owns items [w*SEG, (w+1)*SEG) of the round
       const int64_t i = r0 + (int64_t)w * (SH_ROUND / NW) + s * 64 + lane;
       if (i < hi) {
         const uint32_t k = (uint32_t)key[i];
         rec[s].ts = ts[i];
-        rec[s].key = (k / (uint32_t)G) | (stream ? ((uint32_t)stream[i] << 24) : 0u);
+        // the SoA form carries the stream id in its own LDS column (no 24-bit packing)
+        rec[s].key = SOA ? k / (uint32_t)G : (k / (uint32_t)G) | (stream ? ((uint32_t)stream[i] << 24) : 0u);
         rec[s].v = val ? val[i] : 0u;
+        sid[s] = (SOA && stream) ? stream[i] : 0;
         dst[s] = k % (uint32_t)G;
       } else {
         dst[s] = SH_MAXG;
@@ -134,6 +139,7 @@ __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __r
       const uint32_t slot = wc[w][dst[s]] + rk[s];
       srec[slot] = rec[s];
       sdst[slot] = (uint8_t)dst[s];
+      if (SOA && stream) sstp[slot] = sid[s];
     }
     __syncthreads();
     const int nv = (int)lst[G];
@@ -143,8 +149,8 @@ __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __r
       const ShRec r = srec[x];
       if constexpr (SOA) {
         so.ts[o] = r.ts;
-        so.key[o] = (int32_t)(r.key & 0xffffffu);
-        if (so.stream) so.stream[o] = (int32_t)(r.key >> 24);
+        so.key[o] = (int32_t)r.key;
+        if (so.stream) so.stream[o] = sstp[x];
         if (so.val) so.val[o] = r.v;
       } else {
         out[o] = r;
@@ -152,6 +158,16 @@ __global__ __launch_bounds__(SH_THREADS) void k_shard_scatter(const int64_t* __r
     }
     __syncthreads();
   }
+}
+
+__global__ void k_shard_check(const int32_t* __restrict__ key, const int32_t* __restrict__ stream, int64_t n, int G,
+                              int* bad) {
+  int b = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if ((uint32_t)key[i] / (uint32_t)G >= (1u << 24)) b = 1;
+    if (stream && (stream[i] < 0 || stream[i] > 255)) b = 1;
+  }
+  if (b) atomicOr(bad, 1);
 }
 
 __global__ void k_shard_unpack(const ShRec* __restrict__ in, int64_t m, int64_t* ts, int32_t* key, uint32_t* val,
@@ -182,7 +198,8 @@ extern "C" int64_t shp_shard_workspace_bytes(int64_t n, int G) {
 }
 
 // n events (device SoA) -> out: n packed records grouped by destination rank key % G (stable);
-// counts[g] (host) = records for rank g.  Keys must be < 2^24 * G, stream ids < 256.
+// counts[g] (host) = records for rank g.  Packed form: keys must be < 2^24 * G and stream ids in
+// [0, 255] (shp_shard_partition checks both); the SoA form carries full 32-bit keys and streams.
 // ws: device workspace of shp_shard_workspace_bytes(n, G) bytes.
 static int shard_partition(int64_t n, const int64_t* ts, const int32_t* key, const void* value,
                            const int32_t* stream, int G, void* out, const ShSoa* so, int64_t* counts, void* ws,
@@ -222,6 +239,17 @@ extern "C" int shp_shard_partition(int64_t n, const int64_t* ts, const int32_t* 
                                    const int32_t* stream, int G, void* out, int64_t* counts, void* ws,
                                    void* hip_stream) {
   if (!out && n > 0) return -1;
+  if (n > 0 && G >= 1 && G <= SH_MAXG) {  // the packed record's limits: key / G < 2^24, stream in [0, 255]
+    int* bad = (int*)((char*)ws + shp_shard_workspace_bytes(n, G) - 256);
+    hipStream_t s = (hipStream_t)hip_stream;
+    if (hipMemsetAsync(bad, 0, 4, s) != hipSuccess) return -5;
+    int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    k_shard_check<<<blocks, 256, 0, s>>>(key, stream, n, G, bad);
+    int hb = 0;
+    if (hipMemcpyAsync(&hb, bad, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      return -5;
+    if (hb) return -1;
+  }
   return shard_partition(n, ts, key, value, stream, G, out, nullptr, counts, ws, hip_stream);
 }
 

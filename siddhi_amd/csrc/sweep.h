@@ -65,7 +65,7 @@ constexpr int SW_P2 = 8;     // probes per worklist round
 
 // error bits (engine.hip maps them to status codes)
 constexpr int SWE_KEYS = 1 << 20;   // key id outside [0, max_keys)
-constexpr int SWE_MONO = 1 << 21;   // ts decreases within a key
+constexpr int SWE_MONO = 1 << 21;   // ts decreases within a key (scan kernels only; the sweep is exact)
 constexpr int SWE_RANGE = 1 << 23;  // ts outside base +- 2^49 ms
 constexpr int SWE_AGGNULL = 1 << 24; // SHP_LAYOUT_AGG: a closing event's aggregated value is null
 constexpr int SWE_P32 = 1 << 25;     // SHP_LAYOUT_PAIRS32: e2 seq - e1 seq >= 2^32
@@ -131,27 +131,32 @@ struct SweepDev {
   int32_t lk_bits;       // bits of the largest local key id
   int32_t maybe_null;    // some pushed batch carried a null bitmap (sticky; the carry may hold nulls)
   int64_t st_len;
+  int32_t cur;           // which copy of the double-buffered per-owner state the next push reads
+  int32_t pad_;
   const uint8_t* lk8;    // key -> local key id within its owner (the owner is sw_owner(key))
   int32_t lk_lds;        // scatter stages lk8 in LDS (max_keys <= SW_LKTAB)
   uint32_t* cnt;         // nown * nst + 1: counts, scanned into off
   uint32_t* off;
   SwRec* recs;           // batch capacity
-  // per-owner carry across pushes
-  int32_t* c_n;          // nown
-  int64_t* c_ts;         // nown * SWS_CCAP, absolute ts
-  int64_t* c_seq;
-  uint32_t* c_v;
-  uint8_t* c_lk;
-  uint8_t* c_null;
-  int64_t* lastts;       // nown * SW_LK, absolute ts, INT64_MIN when unseen
-  int64_t* tsmax;        // running max of ts (engine clock)
+  // per-owner state carried across pushes, double-buffered: a push reads copy `cur` and writes
+  // copy cur ^ 1, and the engine flips `cur` only when the push succeeded (a failed push leaves
+  // the engine's state as it was)
+  int32_t* c_n[2];       // nown
+  int64_t* c_ts[2];      // nown * SWS_CCAP, absolute ts
+  int64_t* c_seq[2];
+  uint32_t* c_v[2];
+  uint8_t* c_lk[2];
+  uint8_t* c_null[2];
+  uint8_t* lastc[2];     // nown * SW_LK: the key's latest event opened a candidate (it is then the
+                         // key's last carried candidate, still on the new-and-every list)
+  unsigned long long* tsmax;  // max of ts over the push, as ts ^ 2^63 (0: no event); reset per push
   // SHP_LAYOUT_AGG: selector aggregate over e2's value (1 avg, 2 sum, 3 count; 0 off), its
   // running per-key state (sum, count as doubles: exact integers to 2^53) and the owner-local
   // key -> partition key map for the output rows
   int32_t agg;
   int32_t p32;           // SHP_LAYOUT_PAIRS32: (e2 index in the batch, e2 seq - e1 seq) as two u32
-  double* agg_s;         // nown * SW_LK
-  double* agg_c;
+  double* agg_s[2];      // nown * SW_LK
+  double* agg_c[2];
   int32_t* inv;          // nown * SW_LK
   unsigned long long* stamps;  // diagnostic build: nown * 8 phase cycle counts (else unused)
 };
@@ -514,7 +519,7 @@ __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchVie
   if (e) atomicOr(err, e);
   // running max of ts (the engine clock after the push)
   for (int d = 32; d > 0; d >>= 1) tmax = max(tmax, (int64_t)__shfl_xor((long long)tmax, d, 64));
-  if (lane == 0 && tmax != INT64_MIN) atomicMax((long long*)D.tsmax, (long long)tmax);
+  if (lane == 0 && tmax != INT64_MIN) atomicMax(D.tsmax, (unsigned long long)tmax ^ (1ull << 63));
 }
 
 // ------------------------------------------------------------------ pass 3: per-owner sweep
@@ -595,7 +600,9 @@ struct SwSolveSmem {
   uint64_t ckt[2][SWS_CCAP];          // carry: key | null | ts50 (batch-relative)
   uint32_t cv[2][SWS_CCAP];
   int64_t cseq[2][SWS_CCAP];
-  int64_t lastts[SW_LK];              // batch-relative ts of the key's latest event (INT64_MIN unseen)
+  uint8_t slow[SW_LK + 1];            // key solved by the exact sequential replay in this chunk
+  uint8_t lastc[SW_LK + 1];           // the key's latest event opened a candidate (SweepDev::lastc)
+  int32_t anyslow;
   uint32_t wtot[SWS_WAVES];
   unsigned long long gbase;
   union {
@@ -677,17 +684,103 @@ __device__ __forceinline__ uint32_t sw_block_scan_n(uint32_t v, uint32_t* wtot, 
   return pre + x - v;
 }
 
+// Exact replay of one key's run of the chunk (one thread), for keys whose timestamps are not
+// non-decreasing over [carried candidates..., events...] or lie beyond the chunk's 32-bit span.
+// There the closed form does not hold: StreamPreStateProcessor.expireEvents (:326-361) expires
+// the pending list only from its head while |ts - now| > within (it stops at the first live
+// partial, which may keep expired ones behind it) and the new-and-every list (the candidate the
+// previous event opened) whole; processAndReturn (:364-403) then tries every pending partial in
+// list order without any expiry test.  The results go to the same m(p) / close counts the
+// parallel probe produces (whose own results for the key are undone first), so the offsets,
+// carry and emission steps need no change.
+template <int NT2, int CT>
+__device__ __forceinline__ void sw_seq_key(SwSolveSmem& S, int b, int cur, const BatchView& B, int64_t base, int32_t W,
+                                        const SwPred& f2, bool vflt, bool vnull) {
+  const int beg = (int)S.binoff[b], fe = (int)S.fe[b], end = (int)S.binoff[b + 1];
+  for (int p = beg; p < end; p++) {
+    const int q = SWM(p);
+    if (q >= 0) atomicSub(&S.cnt2[q >> 1], 1u << ((q & 1) * 16));
+  }
+  auto ts_of = [&](int p) -> int64_t {  // exact, batch-relative
+    const uint32_t r = S.ref[p];
+    return (S.lkf[p] & SW_LKF_CAR) ? sw_ts(S.ckt[cur][r]) : B.ts[r] - base;
+  };
+  for (int p = beg; p < fe; p++) SWM(p) = -2;  // carried candidates: the pending list, in order
+  int head = beg;
+  int prevc = (fe > beg && S.lastc[b]) ? fe - 1 : -1;  // on the new-and-every list
+  for (int q = fe; q < end; q++) {
+    const int64_t tq = ts_of(q);
+    for (int p = head; p < q; p++) {  // expireEvents: pending list from the head
+      if (SWM(p) != -2) continue;
+      if (p == prevc) break;
+      const int64_t d = ts_of(p) - tq;
+      if (d > W || d < -W) SWM(p) = -1;
+      else break;
+    }
+    if (prevc >= 0 && SWM(prevc) == -2) {  // ... and the new-and-every list, whole
+      const int64_t d = ts_of(prevc) - tq;
+      if (d > W || d < -W) SWM(prevc) = -1;
+    }
+    const uint32_t fq = S.lkf[q];
+    const uint32_t ev = (uint32_t)S.tv[q].y;
+    double ef = 0, ei = 0;
+    if constexpr (CT == 0) sw_conv(ev, vflt, ef, ei);
+    const bool en = vnull || (fq & SW_LKF_NULL) != 0;
+    for (int p = head; p < q; p++) {  // processAndReturn: every pending partial, in list order
+      if (SWM(p) != -2) continue;
+      const uint32_t av = (uint32_t)S.tv[p].y;
+      double af = 0, ai = 0;
+      if constexpr (CT == 0) sw_conv(av, vflt, af, ai);
+      const bool an = vnull || (S.lkf[p] & SW_LKF_NULL) != 0;
+      const SwCand<CT> c = sw_cand<NT2, CT>(f2, av, af, ai, an);
+      if (sw_close<NT2, CT, 0>(f2, c, ev, ef, ei, en)) {
+        SWM(p) = (int16_t)q;
+        atomicAdd(&S.cnt2[q >> 1], 1u << ((q & 1) * 16));
+      }
+    }
+    if (fq & SW_LKF_F1) {  // e1 matched: a new partial on the new-and-every list
+      SWM(q) = -2;
+      prevc = q;
+    } else {
+      SWM(q) = -3;
+      prevc = -1;
+    }
+    while (head <= q && SWM(head) != -2) head++;
+  }
+}
+
 template <int NT1, int NT2, int CT>
-__global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView B, MatchOut O, int* err) {
+__global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchView B, MatchOut O, int* err) {
   __shared__ SwSolveSmem S;
   const int o = blockIdx.x;
   const uint32_t tid0 = threadIdx.x;
   const uint32_t tid = tid0, lane = __lane_id(), w = tid >> 6;
   const uint64_t lt = sw_lanemask_lt();
   const int64_t rb = D.off[(int64_t)o * D.nst], re = D.off[(int64_t)(o + 1) * D.nst];
-  if (rb == re) return;  // no events for this owner: carry and last ts unchanged
+  const int rd = D.cur, wr = D.cur ^ 1;  // double-buffered per-owner state: read rd, write wr
+  if (rb == re) {  // no events for this owner: its state passes through unchanged
+    const int n0 = D.c_n[rd][o];
+    for (int i = tid; i < n0; i += SWS_THREADS) {
+      const int64_t c = (int64_t)o * SWS_CCAP + i;
+      D.c_ts[wr][c] = D.c_ts[rd][c];
+      D.c_seq[wr][c] = D.c_seq[rd][c];
+      D.c_v[wr][c] = D.c_v[rd][c];
+      D.c_lk[wr][c] = D.c_lk[rd][c];
+      D.c_null[wr][c] = D.c_null[rd][c];
+    }
+    for (int i = tid; i < SW_LK; i += SWS_THREADS) {
+      const int64_t k = (int64_t)o * SW_LK + i;
+      D.lastc[wr][k] = D.lastc[rd][k];
+      if (D.agg) {
+        D.agg_s[wr][k] = D.agg_s[rd][k];
+        D.agg_c[wr][k] = D.agg_c[rd][k];
+      }
+    }
+    if (tid == 0) D.c_n[wr][o] = n0;
+    return;
+  }
   const int64_t base = B.ts[0];
-  const int32_t W = (int32_t)D.within;  // < 2^29 (SweepState::shape_ok)
+  const int32_t W = (int32_t)D.within;  // <= SW_TS_SPAN = 2^29 (SweepState::shape_ok)
   const SwPred f1 = D.f1, f2 = D.f2;
   const bool vnull = D.vtag == T_NULL;
   const bool vflt = D.vtag == T_FLOAT;
@@ -695,23 +788,27 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
   const int lkbits = D.lk_bits;
   const int opc = NT2 == 1 ? sw_opclass(f2.t[0].mask) : 0;
   int e = 0;
-  // carry and last ts from the previous push
-  int nc = D.c_n[o];
+  // carry from the previous push
+  int nc = D.c_n[rd][o];
   for (int i = tid; i <= SW_LK; i += SWS_THREADS) S.ncar[i] = 0;
   if (tid < 8) S.m_[tid] = -3;
   __syncthreads();
   for (int i = tid; i < nc; i += SWS_THREADS) {
     const int64_t c = (int64_t)o * SWS_CCAP + i;
-    const int64_t rel = D.c_ts[c] - base;
+    const int64_t rel = D.c_ts[rd][c] - base;
     if (!sw_rel_ok(rel)) e |= SWE_RANGE;
-    S.ckt[0][i] = sw_kt(D.c_lk[c], rel, D.c_null[c] ? SW_NULL : 0ull);
-    S.cv[0][i] = D.c_v[c];
-    S.cseq[0][i] = D.c_seq[c];
-    atomicAdd(&S.ncar[D.c_lk[c]], 1u);
+    S.ckt[0][i] = sw_kt(D.c_lk[rd][c], rel, D.c_null[rd][c] ? SW_NULL : 0ull);
+    S.cv[0][i] = D.c_v[rd][c];
+    S.cseq[0][i] = D.c_seq[rd][c];
+    atomicAdd(&S.ncar[D.c_lk[rd][c]], 1u);
   }
   for (int i = tid; i < SW_LK; i += SWS_THREADS) {
-    const int64_t t = D.lastts[(int64_t)o * SW_LK + i];
-    S.lastts[i] = t == INT64_MIN ? INT64_MIN : t - base;
+    const int64_t k = (int64_t)o * SW_LK + i;
+    S.lastc[i] = D.lastc[rd][k];
+    if (D.agg) {  // the chunks below read and update copy wr
+      D.agg_s[wr][k] = D.agg_s[rd][k];
+      D.agg_c[wr][k] = D.agg_c[rd][k];
+    }
   }
   if (D.agg)
     for (int i = tid; i < SW_LK; i += SWS_THREADS) S.ainv[i] = D.inv[(int64_t)o * SW_LK + i];
@@ -747,6 +844,8 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
 #endif
     // 1. rank the chunk's records by local key (stable: wave-major, then sub-round, then lane);
     //    S.wc was zeroed during the previous chunk's probe (or before the first chunk)
+    for (int i = tid; i <= SW_LK; i += SWS_THREADS) S.slow[i] = 0;
+    if (tid == 0) S.anyslow = 0;
     uint32_t rk[SWS_RPT], bin[SWS_RPT];
     const uint32_t nonebin = lkbits >= 8 ? SW_LKF_NONE : (1u << lkbits);
     const int rbits = lkbits >= 8 ? 8 : lkbits + 1;
@@ -798,8 +897,12 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     for (int s = 0; s < SWS_RPT; s++) {
       if (bin[s] == nonebin) continue;
       const uint32_t p = S.wc[w][bin[s]] + rk[s];
-      const int64_t rel = sw_ts(pf[s].kt) - tb;
-      if (rel >= SW_TS_SPAN || rel <= -SW_TS_SPAN) e |= SWE_RANGE;
+      int64_t rel = sw_ts(pf[s].kt) - tb;
+      if (rel >= SW_TS_SPAN || rel <= -SW_TS_SPAN) {  // beyond the 32-bit probe: exact replay
+        S.slow[bin[s]] = 1;
+        S.anyslow = 1;
+        rel = rel > 0 ? SW_TS_SPAN : -SW_TS_SPAN;
+      }
       S.tv[p] = make_int2((int32_t)rel, (int32_t)pf[s].v);
       S.lkf[p] = (uint16_t)(bin[s] | ((pf[s].kt & SW_NULL) ? SW_LKF_NULL : 0u) | ((pf[s].kt & SW_F1) ? SW_LKF_F1 : 0u));
       S.ref[p] = pf[s].ref;
@@ -809,7 +912,11 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       const uint32_t lk = sw_lk(kt);
       const uint32_t p = S.binoff[lk] + (uint32_t)x - S.cstart[lk];
       const int64_t rel = sw_ts(kt) - tb;
-      const int64_t crel = rel < SW_TS_FLOOR ? SW_TS_FLOOR : (rel > (1ll << 30) ? (1ll << 30) : rel);
+      if (rel > SW_TS_SPAN) {  // a carried candidate later than the chunk's span: exact replay
+        S.slow[lk] = 1;
+        S.anyslow = 1;
+      }
+      const int64_t crel = rel < SW_TS_FLOOR ? SW_TS_FLOOR : (rel > SW_TS_SPAN ? SW_TS_SPAN : rel);
       S.tv[p] = make_int2((int32_t)crel, (int32_t)S.cv[cur][x]);
       S.lkf[p] = (uint16_t)(lk | SW_LKF_CAR | ((kt & SW_NULL) ? SW_LKF_NULL : 0u));
       S.ref[p] = (uint32_t)x;
@@ -853,6 +960,11 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
         const bool cand = (f & (SW_LKF_CAR | SW_LKF_F1)) != 0;  // carried, or e1's filter (scatter)
         const uint32_t lk = f & 0xFFu;
         const int end = (int)S.binoff[lk + 1];
+        // the closed form needs non-decreasing ts over the key's [carried..., events...]
+        if (p > (int)S.binoff[lk] && S.tv[p - 1].x > a.x) {
+          S.slow[lk] = 1;
+          S.anyslow = 1;
+        }
         const int q0 = max(p + 1, (int)S.fe[lk]);  // carried candidates are not events
         const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
         res = cand ? -4 : -3;  // -4: unresolved
@@ -909,6 +1021,11 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
 #endif
     }
     __syncthreads();
+    if (S.anyslow) {  // rare: keys the closed form does not cover, replayed exactly
+      for (int b = tid; b < (int)min(nonebin, (uint32_t)SW_LK); b += SWS_THREADS)
+        if (S.slow[b]) sw_seq_key<NT2, CT>(S, b, cur, B, base, W, f2, vflt, vnull);
+      __syncthreads();
+    }
     SW_STAMP(1);
     // 4. one block scan gives both the output offsets (closes per closing event, counted by the
     //    probe; 16-bit, in place of the counts) and the carry slots of still-open candidates
@@ -927,8 +1044,8 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
       for (int i = tid; i <= SW_LK; i += SWS_THREADS) S.ncar[i] = 0;  // recounted below
       if (D.agg) {  // per-key aggregate state carried in (read before any run end rewrites it)
         for (int b = tid; b < (int)min(nonebin, (uint32_t)SW_LK); b += SWS_THREADS) {
-          S.ainit[b] = D.agg_s[(int64_t)o * SW_LK + b];
-          S.ainit[SW_LK + b] = D.agg_c[(int64_t)o * SW_LK + b];
+          S.ainit[b] = D.agg_s[wr][(int64_t)o * SW_LK + b];
+          S.ainit[SW_LK + b] = D.agg_c[wr][(int64_t)o * SW_LK + b];
         }
       }
       uint32_t total;
@@ -1004,36 +1121,17 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
             pn += (double)c;
             so += c;
             if ((uint32_t)q + 1 == S.binoff[lk + 1]) {  // run end: the key's state after this chunk
-              D.agg_s[(int64_t)o * SW_LK + lk] = ps;
-              D.agg_c[(int64_t)o * SW_LK + lk] = pn;
+              D.agg_s[wr][(int64_t)o * SW_LK + lk] = ps;
+              D.agg_c[wr][(int64_t)o * SW_LK + lk] = pn;
             }
           }
         }
       }
-      // 5. still-open candidates become the next carry (sorted order = key, then i)
-      // per-key timestamp order: consecutive events of a key (same key, neither carried) ...
-      {
-        uint32_t fq[SWS_PER + 1];
-        int32_t tq[SWS_PER + 1];
-#pragma unroll
-        for (int k = 0; k <= SWS_PER; k++) {
-          const int p = (int)tid * SWS_PER + k;
-          fq[k] = p < E ? (uint32_t)S.lkf[p] : SW_LKF_CAR;
-          tq[k] = p < E ? S.tv[p].x : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < SWS_PER; k++)
-          if (((fq[k] | fq[k + 1]) & SW_LKF_CAR) == 0 && ((fq[k] ^ fq[k + 1]) & 0xFFu) == 0 && tq[k + 1] < tq[k])
-            e |= SWE_MONO;
-      }
-      // ... and a key's first event against its latest ts so far, which then moves to its last
+      // 5. still-open candidates become the next carry (sorted order = key, then i); a key whose
+      //    latest event opened a candidate has it on the new-and-every list (sw_seq_key)
       for (int b = tid; b < (int)min(nonebin, (uint32_t)SW_LK); b += SWS_THREADS) {
         const int fe = (int)S.fe[b], end = (int)S.binoff[b + 1];
-        if (fe < end) {
-          const int64_t prev = S.lastts[b];
-          if (prev != INT64_MIN && tb + S.tv[fe].x < prev) e |= SWE_MONO;
-          S.lastts[b] = tb + S.tv[end - 1].x;
-        }
+        if (fe < end) S.lastc[b] = (S.lkf[end - 1] & SW_LKF_F1) ? 1 : 0;
       }
 #pragma unroll
       for (int k = 0; k < SWS_PER; k++) {
@@ -1119,21 +1217,18 @@ __global__ __launch_bounds__(SWS_THREADS) void k_sw_solve(SweepDev D, BatchView 
     D.stamps[(int64_t)o * 8 + 6] = (dbg_chunks << 40) | (dbg_nc & 0xffffffffffull);
   }
 #endif
-  // write back carry and last ts
+  // write back the carry and the per-key flags (copy wr)
   for (int i = tid; i < nc; i += SWS_THREADS) {
     const int64_t c = (int64_t)o * SWS_CCAP + i;
     const uint64_t kt = S.ckt[cur][i];
-    D.c_ts[c] = base + sw_ts(kt);
-    D.c_seq[c] = S.cseq[cur][i];
-    D.c_v[c] = S.cv[cur][i];
-    D.c_lk[c] = (uint8_t)sw_lk(kt);
-    D.c_null[c] = (kt & SW_NULL) ? 1 : 0;
+    D.c_ts[wr][c] = base + sw_ts(kt);
+    D.c_seq[wr][c] = S.cseq[cur][i];
+    D.c_v[wr][c] = S.cv[cur][i];
+    D.c_lk[wr][c] = (uint8_t)sw_lk(kt);
+    D.c_null[wr][c] = (kt & SW_NULL) ? 1 : 0;
   }
-  for (int i = tid; i < SW_LK; i += SWS_THREADS) {
-    const int64_t t = S.lastts[i];
-    D.lastts[(int64_t)o * SW_LK + i] = t == INT64_MIN ? INT64_MIN : base + t;
-  }
-  if (tid == 0) D.c_n[o] = nc;
+  for (int i = tid; i < SW_LK; i += SWS_THREADS) D.lastc[wr][(int64_t)o * SW_LK + i] = S.lastc[i];
+  if (tid == 0) D.c_n[wr][o] = nc;
   if (e) atomicOr(err, e);
 }
 
@@ -1166,9 +1261,8 @@ __global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchO
 
 __global__ void k_sw_init(SweepDev D) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < D.nown) D.c_n[i] = 0;
-  if (i < (int64_t)D.nown * SW_LK) D.lastts[i] = INT64_MIN;
-  if (i == 0) *D.tsmax = INT64_MIN;
+  if (i < D.nown) D.c_n[0][i] = D.c_n[1][i] = 0;
+  if (i < (int64_t)D.nown * SW_LK) D.lastc[0][i] = D.lastc[1][i] = 0;
 }
 
 }  // namespace shp
@@ -1196,7 +1290,9 @@ struct SweepState {
   // Is the program a sweep shape? One 4-byte predicate column (int / float / string id) or none,
   // filters over slot 0/1 attributes of that column only, lowerable to SwPred.
   static bool shape_ok(const DevProg& P, const FastShape& f) {
-    if (!f.ok || P.ncol > 1) return false;
+    // `within` must fit the probe's 32-bit chunk-relative timestamps (and the carried-candidate
+    // floor, SW_TS_FLOOR): longer windows take the scan kernels (64-bit timestamps)
+    if (!f.ok || P.ncol > 1 || f.within > SW_TS_SPAN) return false;
     if (P.ncol == 1 && !(P.colTag[0] == T_INT || P.colTag[0] == T_FLOAT || P.colTag[0] == T_STR)) return false;
     SwPred a, b;
     int8_t vt = P.ncol == 1 ? P.colTag[0] : T_NULL;
@@ -1393,14 +1489,17 @@ struct SweepState {
     al(D.cnt, nc);
     al(D.off, nc);
     al(D.recs, cap);
-    al(D.c_n, nown);
-    al(D.c_ts, (int64_t)nown * SWS_CCAP);
-    al(D.c_seq, (int64_t)nown * SWS_CCAP);
-    al(D.c_v, (int64_t)nown * SWS_CCAP);
-    al(D.c_lk, (int64_t)nown * SWS_CCAP);
-    al(D.c_null, (int64_t)nown * SWS_CCAP);
-    al(D.lastts, (int64_t)nown * SW_LK);
+    for (int c = 0; c < 2; c++) {
+      al(D.c_n[c], nown);
+      al(D.c_ts[c], (int64_t)nown * SWS_CCAP);
+      al(D.c_seq[c], (int64_t)nown * SWS_CCAP);
+      al(D.c_v[c], (int64_t)nown * SWS_CCAP);
+      al(D.c_lk[c], (int64_t)nown * SWS_CCAP);
+      al(D.c_null[c], (int64_t)nown * SWS_CCAP);
+      al(D.lastc[c], (int64_t)nown * SW_LK);
+    }
     al(D.tsmax, 1);
+    D.cur = 0;
     (void)rocprim::exclusive_scan(nullptr, tmp_bytes, D.cnt, D.off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s);
     if (hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)) != hipSuccess)
       throw std::runtime_error("hipMalloc failed (sweep scan scratch)");
@@ -1413,20 +1512,30 @@ struct SweepState {
     const int64_t nk = (int64_t)D.nown * SW_LK;
     std::vector<int32_t> inv(nk, -1);
     for (int32_t k = 0; k < max_keys; k++) inv[(int64_t)(kmap[k] & 0xffffu) * SW_LK + (kmap[k] >> 16)] = k;
-    al(D.agg_s, nk);
-    al(D.agg_c, nk);
     al(D.inv, nk);
-    if (hipMemcpy(D.inv, inv.data(), nk * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemsetAsync(D.agg_s, 0, nk * 8, s) != hipSuccess || hipMemsetAsync(D.agg_c, 0, nk * 8, s) != hipSuccess)
+    if (hipMemcpy(D.inv, inv.data(), nk * 4, hipMemcpyHostToDevice) != hipSuccess)
       throw std::runtime_error("sweep: aggregate state");
+    for (int c = 0; c < 2; c++) {
+      al(D.agg_s[c], nk);
+      al(D.agg_c[c], nk);
+      if (hipMemsetAsync(D.agg_s[c], 0, nk * 8, s) != hipSuccess || hipMemsetAsync(D.agg_c[c], 0, nk * 8, s) != hipSuccess)
+        throw std::runtime_error("sweep: aggregate state");
+    }
     D.agg = fn;
   }
 
+  // the push succeeded: the state it wrote becomes the state the next push reads
+  void commit() { D.cur ^= 1; }
+
   void release() {
-    void* ps[] = {(void*)D.lk8, D.agg_s, D.agg_c, D.inv, D.cnt, D.off, D.recs, D.c_n, D.c_ts, D.c_seq, D.c_v, D.c_lk, D.c_null,
-                  D.lastts, D.tsmax, tmp};
+    void* ps[] = {(void*)D.lk8, D.inv, D.cnt, D.off, D.recs, D.tsmax, tmp};
     for (void* p : ps)
       if (p) (void)hipFree(p);
+    for (int c = 0; c < 2; c++) {
+      void* qs[] = {D.agg_s[c], D.agg_c[c], D.c_n[c], D.c_ts[c], D.c_seq[c], D.c_v[c], D.c_lk[c], D.c_null[c], D.lastc[c]};
+      for (void* q : qs)
+        if (q) (void)hipFree(q);
+    }
     D = SweepDev{};
     tmp = nullptr;
   }
@@ -1436,6 +1545,7 @@ struct SweepState {
     if (B.n <= 0) return;
     if (B.nulls[0]) D.maybe_null = 1;
     D.nst = (int32_t)((B.n + st_len - 1) / st_len);
+    (void)hipMemsetAsync(D.tsmax, 0, sizeof(unsigned long long), s);
     size_t nc = (size_t)D.nown * D.nst + 1;
     kt.mark("sw_count", s);
     k_sw_count<<<D.nst, SW_THREADS, 0, s>>>(D, B, key, err);

@@ -63,6 +63,8 @@ class DeviceExchange:
         self.L = native.lib()
         self.G, self.dist = world, dist
         vd = value_dtype or torch.float32
+        if torch.empty(0, dtype=vd).element_size() != 4:
+            raise ValueError("DeviceExchange moves 4-byte value columns (int, float, string id) only")
         self.s_ts = torch.empty(capacity, dtype=torch.int64, device=device)
         self.s_key = torch.empty(capacity, dtype=torch.int32, device=device)
         self.s_val = torch.empty(capacity, dtype=vd, device=device)

@@ -16,7 +16,7 @@ struct FH {
   int nk;
   int64_t cap, mcap;
   std::vector<int64_t> c_seq, c_ts, c_val, last_ts, s_ts, s_val;
-  std::vector<uint8_t> c_null, s_null;
+  std::vector<uint8_t> c_null, s_null, slow, last_cand;
   std::vector<int32_t> c_n, c_match, match;
   std::vector<uint32_t> nclose, moff, first_open;
   FastDev F{};
@@ -46,6 +46,7 @@ void* fh_create(const char* json, int max_keys, int64_t max_batch, int64_t max_m
   h->c_seq.assign(nk * FCC, 0); h->c_ts.assign(nk * FCC, 0); h->c_val.assign(nk * FCC * 2, 0);
   h->c_null.assign(nk * FCC * 2, 0); h->c_n.assign(nk, 0); h->c_match.assign(nk * FCC, 0);
   h->last_ts.assign(nk, INT64_MIN); h->first_open.assign(nk, 0xffffffffu);
+  h->slow.assign(nk, 0); h->last_cand.assign(nk, 0);
   h->s_ts.assign(cap, 0); h->s_val.assign(cap * 2, 0); h->s_null.assign(cap * 2, 0);
   h->match.assign(cap, 0); h->nclose.assign(cap, 0); h->moff.assign(cap + 1, 0);
   FastDev& F = h->F;
@@ -54,6 +55,7 @@ void* fh_create(const char* json, int max_keys, int64_t max_batch, int64_t max_m
   F.c_n = h->c_n.data(); F.c_match = h->c_match.data(); F.last_ts = h->last_ts.data(); F.s_ts = h->s_ts.data();
   F.s_val = h->s_val.data(); F.s_null = h->s_null.data(); F.match = h->match.data(); F.nclose = h->nclose.data();
   F.moff = h->moff.data(); F.first_open = h->first_open.data();
+  F.slow = h->slow.data(); F.last_cand = h->last_cand.data(); F.fstream = h->comp.fast.stream;
   return h;
 }
 
@@ -79,6 +81,7 @@ int fh_push(void* hp, int64_t n, const int64_t* ts, const int32_t* key, const in
   for (int64_t i = 0; i < n; i++) fast_search_item(B, h->F, perm.data(), skey.data(), kbeg.data(), kcnt.data(), i, fstream);
   for (int64_t c = 0; c < (int64_t)h->nk * FCC; c++)
     fast_search_carry_item(B, h->F, perm.data(), kbeg.data(), kcnt.data(), c, fstream);
+  for (int k = 0; k < h->nk; k++) fast_seq_item(h->F, B, perm.data(), kbeg.data(), kcnt.data(), k, fstream);
   uint32_t acc = 0;
   for (int64_t p = 0; p < n; p++) { h->moff[p] = acc; acc += h->nclose[p]; }
   int64_t total = acc;

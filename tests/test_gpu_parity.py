@@ -143,15 +143,17 @@ def test_key_out_of_range_fails_loudly():
         run(eng, cq, g)
 
 
-def test_decreasing_ts_on_fast_path_fails_loudly():
-    from siddhi_amd.native import HipEngine, ShpError
+def test_decreasing_ts_on_sweep_matches_oracle():
+    """A fully reversed stream (every key's ts decreasing): the sweep replays the keys exactly
+    (see tests/test_unordered_ts.py) instead of refusing the push."""
     cq = program_for(2)
-    eng = HipEngine(cq.program_json(), 0, max_keys=4, max_batch=1024, force_general=3)
+    eng = hip(3, max_keys=4, max_batch=1024)(cq.program_json(), 0)
     assert eng.path == 2
     g = small_stream(2, 200, 4)
     g["ts"] = g["ts"][::-1].copy()
-    with pytest.raises(ShpError, match="SHP_ERR_UNSUPPORTED"):
-        run(eng, cq, g)
+    a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    b = per_key(run(eng, cq, g))
+    assert compare(a, b) is None, compare(a, b)
 
 
 @pytest.mark.parametrize("q,keys,general", [(2, 300, 0), (2, 64, 2), (2, 64, 1), ("3b", 64, 0), (4, 200, 0),
@@ -441,3 +443,127 @@ def test_pairs32_device_pairs_decode_to_pairs():
         assert (p64[o64] == p32[o32]).all()
     for eng in engs.values():
         eng.close()
+
+
+@pytest.mark.parametrize("q", [3, "3b"], ids=["c3", "c3b"])
+def test_hbm_lanes_many_keys_vs_oracle(q):
+    """k_nfa_lanes with its state arena in HBM (more than LDS_LANES_MAX_KEYS = 8192 keys; the
+    LDS variant serves fewer): C3 / C3' at 20k keys, split pushes, against the oracle."""
+    cq = program_for(q)
+    g = small_stream(q, 400_000, 20_000)
+    a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    eng = hip(1, max_keys=20_000, max_batch=1 << 17)(cq.program_json(), 0)
+    assert eng.path == 0
+    b = per_key(run(eng, cq, g, 131_071))
+    assert compare(a, b) is None, compare(a, b)
+    if q == "3b":
+        assert sum(len(v) for v in a.values()) > 10_000
+
+
+def test_hbm_lanes_forced_by_env_vs_oracle(monkeypatch):
+    """SHP_NO_LDS_LANES forces the HBM arena at a few keys too (C4's logical/absent shape)."""
+    monkeypatch.setenv("SHP_NO_LDS_LANES", "1")
+    cq = program_for(4)
+    g = small_stream(4, 60_000, 200)
+    a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    b = per_key(run(hip(1, max_keys=200, max_batch=1 << 15)(cq.program_json(), 0), cq, g, 17_011))
+    assert compare(a, b) is None, compare(a, b)
+    assert sum(len(v) for v in a.values()) > 100
+
+
+def test_c5_aggregate_at_100k_keys():
+    """C5 as configured (100k keys): SHP_LAYOUT_AGG on the device against the oracle's matches
+    folded by AvgAttributeAggregatorExecutor's arithmetic; 2M events in three pushes."""
+    from siddhi_amd.native import LAYOUT_AGG
+    cq = program_for(5)
+    g = small_stream(5, 2_000_000, 100_000)
+    a = run(OracleEngine(cq.program_json(), 0), cq, g)
+    want = _expected_agg(a, columns_for(cq, g)[0], "avg")
+    eng = hip(0, max_keys=100_000, max_batch=1 << 20, match_layout=LAYOUT_AGG)(cq.program_json(), 0)
+    assert eng.path == 2
+    b = run(eng, cq, g, 700_001)
+    got = {}
+    for k, v in zip(b["key"], b["agg"]):
+        got.setdefault(int(k), []).append(float(v))
+    assert set(got) == set(want)
+    for k in want:
+        assert len(got[k]) == len(want[k]), k
+        np.testing.assert_allclose(got[k], want[k], rtol=1e-9, atol=0)
+    assert sum(len(v) for v in want.values()) > 500_000
+
+
+@pytest.mark.parametrize("within", ["6 days", "30 days"])
+def test_long_within_at_many_keys_vs_oracle(within):
+    """`within` longer than the sweep's 2^29 ms probe span (30 days) must not take the sweep
+    (it would truncate W to 32 bits): the engine picks the scan kernels; 6 days still sweeps."""
+    from siddhi_amd.query.compiler import compile_app
+    app = ("define stream S (k string, v float); partition with (k of S) begin @info(name='q') "
+           f"from every e1=S[v > 20] -> e2=S[v > e1.v] within {within} select e1.v as a, e2.v as b "
+           "insert into Out; end;")
+    cq = compile_app(app)[1][0]
+    rng = np.random.default_rng(5)
+    n, keys = 50_000, 300
+    ts = 1_000_000 + np.cumsum(rng.integers(0, 400_000, n)).astype(np.int64)  # ~0.7 days per key
+    key = rng.integers(0, keys, n).astype(np.int32)
+    price = (rng.integers(0, 10000, n) / 100.0).astype(np.float32)
+    outs = []
+    eng = hip(0, max_keys=keys, max_batch=1 << 14)(cq.program_json(), 0)
+    assert eng.path == (1 if within == "30 days" else 2)
+    for e in (OracleEngine(cq.program_json(), 0), eng):
+        for lo in range(0, n, 9_001):
+            hi = min(n, lo + 9_001)
+            e.push(ts[lo:hi], key[lo:hi], np.zeros(hi - lo, np.int32), [price[lo:hi]], [None])
+        outs.append(per_key(e.fetch()))
+    assert compare(*outs) is None, compare(*outs)
+    assert sum(len(v) for v in outs[0].values()) > 1000
+
+
+def test_sweep_failed_push_leaves_state_unchanged():
+    """The sweep's per-owner state is double-buffered: a push that fails (here: more matches than
+    max_matches) leaves the engine as it was, so the caller can push the same events again in
+    smaller pieces and get the oracle's matches."""
+    from siddhi_amd.native import HipEngine, ShpError
+    cq = program_for(2)
+    g = small_stream(2, 120_000, 300)
+    ref = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    eng = HipEngine(cq.program_json(), 0, max_keys=300, max_batch=1 << 16, max_matches=20_000, force_general=3)
+    cols = columns_for(cq, g)
+    lo, step, failures = 0, 60_000, 0
+    while lo < len(g["ts"]):
+        hi = min(len(g["ts"]), lo + step)
+        try:
+            eng.push(g["ts"][lo:hi], g["key"][lo:hi], g["stream"][lo:hi], [c[lo:hi] for c in cols], [None])
+            lo = hi
+        except ShpError as ex:  # too many matches for the buffer: the same events again, in smaller pushes
+            assert "SHP_ERR_OUTPUT" in str(ex)
+            failures += 1
+            step //= 2
+    assert failures > 0
+    got = per_key(eng.fetch())
+    assert compare(ref, got) is None, compare(ref, got)
+
+
+@pytest.mark.parametrize("general", [1, 2], ids=["lanes", "scan"])
+def test_restore_after_failed_push(general):
+    """Lanes / scan kernels update state in place: after a failed push the engine must be
+    restored from a snapshot (include/siddhi_hip.h); restore + smaller pushes = the oracle."""
+    from siddhi_amd.native import HipEngine, ShpError
+    cq = program_for(2)
+    g = small_stream(2, 60_000, 64)
+    ref = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    eng = HipEngine(cq.program_json(), 0, max_keys=64, max_batch=1 << 16, max_matches=12_000, force_general=general)
+    cols = columns_for(cq, g)
+    first = 10_000
+    eng.push(g["ts"][:first], g["key"][:first], g["stream"][:first], [c[:first] for c in cols], [None])
+    blob = eng.snapshot()
+    head = eng.fetch()
+    with pytest.raises(ShpError, match="SHP_ERR_OUTPUT"):
+        eng.push(g["ts"][first:], g["key"][first:], g["stream"][first:], [c[first:] for c in cols], [None])
+    eng.fetch()
+    eng.restore(blob)
+    for lo in range(first, len(g["ts"]), 10_000):
+        hi = min(len(g["ts"]), lo + 10_000)
+        eng.push(g["ts"][lo:hi], g["key"][lo:hi], g["stream"][lo:hi], [c[lo:hi] for c in cols], [None])
+    from siddhi_amd.native import _concat
+    got = per_key(_concat([head, eng.fetch()], None, eng.S))
+    assert compare(ref, got) is None, compare(ref, got)
