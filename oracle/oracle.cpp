@@ -1235,6 +1235,10 @@ struct Engine {
       liveTimersUpTo(ts);
       if (ts > clock) clock = ts;
     }
+    int stream = ev_stream[seq];
+    // a clock-only event (stream -1: a send on a stream this query does not read) sets the
+    // playback clock above and reaches no receiver, so no partition is created for it
+    if (stream < 0 || stream >= (int)receivers.size()) return;
     KeyCtx* k;
     if (partitioned) {
       bool created;
@@ -1244,8 +1248,6 @@ struct Engine {
       k = keys[0].get();
     }
     cur = k;
-    int stream = ev_stream[seq];
-    if (stream < 0 || stream >= (int)receivers.size()) return;
     Receiver& r = receivers[stream];
     if (r.forStream.empty()) return;
     // stabilizeStates (state/receiver/*.java)

@@ -168,7 +168,13 @@ class SiddhiAppRuntime:
         self._pending = []
         stream_names = list(self.app.streams.keys())
         for qr in self.queries.values():
-            sel = [i for i in ids if stream_names[self._events[i][0]] in qr.streams]
+            if self.app.playback:
+                # the playback clock is the app's: a send on any stream sets it before anything
+                # else (InputHandler.java:59-64), so a stream this query does not read still
+                # fires its timers -- pushed as clock-only events (stream -1)
+                sel = list(ids)
+            else:
+                sel = [i for i in ids if stream_names[self._events[i][0]] in qr.streams]
             if not sel:
                 continue
             self._push(qr, sel, stream_names)
@@ -190,6 +196,11 @@ class SiddhiAppRuntime:
             ts[j] = t
             stream[j] = s
             sname = stream_names[s]
+            if sname not in qr.streams:  # clock-only (playback): no key, no values
+                stream[j] = -1
+                for c in range(len(cols)):
+                    nulls[c][j] = 1
+                continue
             if pk is not None:
                 attr = pk[sname]
                 ai = [x[0] for x in self.app.streams[sname].attrs].index(attr)

@@ -73,6 +73,10 @@ def run_fixture(fx, engine_factory):
         elif "advance" in op:
             now = op["advance"]
             rt.advance_time(now)
+        elif "expect_count" in op:  # an intermediate count assert of the reference test
+            rt.flush()
+            if len(rows) != op["expect_count"]:
+                return False, f"count {len(rows)} != expected {op['expect_count']} at op {fx['ops'].index(op)}", rows
         elif "wait_in_events" in op:
             w = op["wait_in_events"]
             for i in range(w["retry"]):
