@@ -77,7 +77,9 @@ typedef struct shp_config {
 
 /* One batch of events in SoA form. Column c follows program["columns"][c]:
  * int->int32, long->int64, float->float32, double->float64, bool->uint8,
- * string->int32 (dictionary id, host owns the strings). nulls[c] may be NULL. */
+ * string->int32 (dictionary id, host owns the strings). nulls[c] may be NULL.
+ * stream -1 marks a clock-only event: a send on a stream this query does not read, which in
+ * playback still sets the app's clock (InputHandler.java:59-64) and so fires timers. */
 typedef struct shp_batch {
   int64_t n;
   const int64_t* ts;
@@ -85,6 +87,17 @@ typedef struct shp_batch {
   const int32_t* stream;   /* stream index per event (program["streams"] order); NULL = all 0 */
   const void* const* cols;
   const uint8_t* const* nulls;
+  /* optional (NULL = derived): the playback clock each event hands
+   * TimestampGeneratorImpl.setCurrentTimestamp (core/util/timestamp/TimestampGeneratorImpl.java:
+   * 105-121), the events' own ts when NULL.  A key-sharded rank sees only its keys' events, so it
+   * is given the global clock here (AbsentStreamPreStateProcessor.java:216-223 reads it as
+   * actualCurrentTime).  Used by the general NFA lanes (absent-state timers); the 2-state paths
+   * have no timers and ignore it. */
+  const int64_t* clock;
+  /* optional: the events' sequence numbers (NULL = the engine's running count); match records
+   * then refer to events by these numbers (a key-sharded rank passes global ones).  Not with
+   * SHP_LAYOUT_PAIRS (its records must map back to batch positions). */
+  const int64_t* seq;
 } shp_batch;
 
 /* Engine-owned match records (valid until the next call on the engine).
@@ -124,6 +137,39 @@ int shp_engine_num_states(const shp_engine* e);
 /* Which kernels the engine runs: 2 = sweep (owner partition + LDS sweep), 1 = specialised 2-state
  * scan kernel, 0 = general NFA lanes. */
 int shp_engine_path(const shp_engine* e);
+/* ---- Key-sharded multi-GPU (SURVEY.md §8b "Multi-GPU is internal to the engine", §8e) ----
+ * A partitioned query's keys are split over `world` engines: key k on rank k % world (the dense
+ * id k / world there).  One push hands every rank one slice of the global stream (consecutive
+ * pieces in rank order, device pointers on that rank's GPU); the group splits each slice by key
+ * owner on the GPU, exchanges it (RCCL ncclSend/ncclRecv over xGMI between processes, device
+ * copies within one process), and every rank's engine runs the keys it owns.  Per-key emission
+ * order is the reference's (a key lives on one rank; received events keep global order).  The
+ * group's cfg.max_keys is the global key count; cfg.max_batch bounds the events one rank may
+ * receive per push.  Absent-state timers get the global playback clock (shp_batch.clock);
+ * SHP_LAYOUT_FULL records name events by global sequence number.  Replaces, for the sharded
+ * deployment, PartitionStreamReceiver.receive/send (core/partition/PartitionStreamReceiver.java:
+ * 82-283) routing each event to its key's state. */
+typedef struct shp_group shp_group;
+#define SHP_COMM_ID_BYTES 128
+/* One process driving `world` GPUs (e.g. one JVM): rank r on devices[r] (repeats allowed). */
+int shp_group_create(const char* nfa_program_json, const shp_config* cfg, int32_t world, const int32_t* devices,
+                     shp_group** out);
+/* One process per GPU: rank 0 makes the RCCL id, the host broadcasts its SHP_COMM_ID_BYTES bytes,
+ * every rank then creates its member on cfg.device (a collective call). */
+int shp_comm_id(void* id, size_t len);
+int shp_group_create_rank(const char* nfa_program_json, const shp_config* cfg, int32_t world, int32_t rank,
+                          const void* comm_id, shp_group** out);
+/* One push (collective: every rank pushes once per step).  slices: one shp_batch per local rank
+ * (in-process group: world of them; per-rank member: its own).  matches (may be NULL): per local
+ * rank, the matches of this push (they stay in HBM until shp_group_fetch_matches). */
+int shp_group_push(shp_group* g, const shp_batch* slices, int64_t* matches);
+/* The local ranks' matches of the last push in host memory, global key ids, per-key emission order. */
+int shp_group_fetch_matches(shp_group* g, shp_matches* out);
+int shp_group_local_engines(const shp_group* g);
+shp_engine* shp_group_engine(shp_group* g, int32_t i);  /* local rank i's engine (timings, snapshots) */
+const char* shp_group_last_error(const shp_group* g);
+void shp_group_destroy(shp_group* g);
+
 /* Bench/test utility (not part of the reference boundary): fill device buffers with events
  * start..start+count-1 of the SURVEY.md §8d synthetic stream (PCG32, bit-identical to
  * siddhi_amd/synth.py). Any output pointer may be NULL. hip_stream: a hipStream_t or NULL. */

@@ -253,6 +253,8 @@ struct Engine {
   int64_t clock = 0;
   int64_t nevents = 0;
   vector<int64_t> ev_ts;
+  vector<int64_t> ev_clk;   // value handed to setCurrentTimestamp (the caller's clock column, else ts)
+  vector<int64_t> ev_gseq;  // the caller's sequence numbers (seq column, else the running count)
   std::unordered_map<int32_t, size_t> keyIndex;
   vector<std::unique_ptr<KeyCtx>> keys;
   KeyCtx* cur = nullptr;
@@ -1224,7 +1226,7 @@ struct Engine {
 
   // one InputHandler.send(ts, data) on stream `stream` for partition key `key`
   void sendEvent(int64_t seq) {
-    int64_t ts = ev_ts[seq];
+    int64_t ts = ev_clk[seq];  // the clock this send sets (= the event's ts unless given)
     emit_pos = seq;
     if (playback) {
       if (ts >= clock) {  // TimestampGeneratorImpl.setCurrentTimestamp :105-121
@@ -1539,9 +1541,12 @@ struct Engine {
   }
 
   void push(int64_t n, const int64_t* ts, const int32_t* key, const int32_t* stream,
-            const void* const* colp, const uint8_t* const* nulls) {
+            const void* const* colp, const uint8_t* const* nulls, const int64_t* clk = nullptr,
+            const int64_t* gseq = nullptr) {
     int64_t base = nevents;
     ev_ts.insert(ev_ts.end(), ts, ts + n);
+    ev_clk.insert(ev_clk.end(), clk ? clk : ts, (clk ? clk : ts) + n);
+    for (int64_t i = 0; i < n; i++) ev_gseq.push_back(gseq ? gseq[i] : base + i);
     ev_key.insert(ev_key.end(), key, key + n);
     ev_stream.insert(ev_stream.end(), stream, stream + n);
     for (size_t c = 0; c < cols.size(); c++) {
@@ -1634,6 +1639,15 @@ int oracle_push(void* hp, int64_t n, const int64_t* ts, const int32_t* key, cons
   return 0;
 }
 
+// the same with the optional columns of shp_batch: clock (setCurrentTimestamp value per event)
+// and seq (sequence numbers the match records use); either may be NULL
+int oracle_push2(void* hp, int64_t n, const int64_t* ts, const int32_t* key, const int32_t* stream,
+                 const void* const* cols, const uint8_t* const* nulls, const int64_t* clock, const int64_t* seq) {
+  auto* h = (OracleHandle*)hp;
+  h->e.push(n, ts, key, stream, cols, nulls, clock, seq);
+  return 0;
+}
+
 int oracle_advance(void* hp, int64_t now) {
   ((OracleHandle*)hp)->e.advance(now);
   return 0;
@@ -1655,15 +1669,23 @@ int oracle_fetch(void* hp, int32_t* key, int64_t* ts, int8_t* type, int64_t* pos
                  int64_t* refs) {
   Engine& e = ((OracleHandle*)hp)->e;
   int64_t r = 0;
+  const int64_t ne = (int64_t)e.ev_gseq.size();
+  // internal event numbers -> the caller's sequence numbers (an emission after the last event,
+  // e.g. from an advance, sits one past the last event's number)
+  auto g = [&](int64_t x) -> int64_t {
+    if (x < 0) return x;
+    if (x < ne) return e.ev_gseq[x];
+    return ne > 0 ? e.ev_gseq[ne - 1] + (x - ne + 1) : x;
+  };
   for (size_t i = 0; i < e.out.size(); i++) {
     auto& m = e.out[i];
     key[i] = m.key;
     ts[i] = m.ts;
     type[i] = m.type;
-    pos[i] = m.pos;
+    pos[i] = g(m.pos);
     for (int s = 0; s < e.nstates; s++) {
       slot_len[i * e.nstates + s] = (int32_t)m.slots[s].size();
-      for (int64_t x : m.slots[s]) refs[r++] = x;
+      for (int64_t x : m.slots[s]) refs[r++] = g(x);
     }
   }
   e.out.clear();

@@ -31,6 +31,7 @@ def lib():
         L.oracle_create.restype = ctypes.c_void_p
         L.oracle_create.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int]
         L.oracle_push.argtypes = [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 5
+        L.oracle_push2.argtypes = [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 7
         L.oracle_advance.argtypes = [ctypes.c_void_p, ctypes.c_int64]
         for f in ("oracle_num_matches", "oracle_num_refs", "oracle_timer_ties", "oracle_dropped_returns"):
             getattr(L, f).restype = ctypes.c_int64
@@ -58,7 +59,7 @@ class OracleEngine:
         self.S = L.oracle_num_states(self.h)
         self._keep = []
 
-    def push(self, ts, key, stream, cols, nulls):
+    def push(self, ts, key, stream, cols, nulls, clock=None, seq=None):
         L = lib()
         n = len(ts)
         ts = np.ascontiguousarray(ts, np.int64)
@@ -68,8 +69,10 @@ class OracleEngine:
         colp = (ctypes.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
         nul = [None if m is None else np.ascontiguousarray(m, np.uint8) for m in nulls]
         nulp = (ctypes.c_void_p * max(1, len(nul)))(*[None if m is None else m.ctypes.data for m in nul])
-        L.oracle_push(self.h, n, _ptr(ts), _ptr(key), _ptr(stream),
-                      ctypes.cast(colp, ctypes.c_void_p), ctypes.cast(nulp, ctypes.c_void_p))
+        clock = None if clock is None else np.ascontiguousarray(clock, np.int64)
+        seq = None if seq is None else np.ascontiguousarray(seq, np.int64)
+        L.oracle_push2(self.h, n, _ptr(ts), _ptr(key), _ptr(stream), ctypes.cast(colp, ctypes.c_void_p),
+                       ctypes.cast(nulp, ctypes.c_void_p), _ptr(clock), _ptr(seq))
 
     def advance(self, now):
         lib().oracle_advance(self.h, int(now))

@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libsiddhi_hip.so")
 SRC = os.path.join(HERE, "csrc")
-DEPS = ["engine.hip", "synth.hip", "shard.hip", "nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h", "sweep.h"]
+DEPS = ["engine.hip", "synth.hip", "shard.hip", "group.hip", "nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h", "sweep.h"]
 
 
 def _stale(lib: str = LIB) -> bool:
@@ -31,7 +31,7 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-o", lib + ".tmp", os.path.join(SRC, "engine.hip"), os.path.join(SRC, "synth.hip"),
-           os.path.join(SRC, "shard.hip")]
+           os.path.join(SRC, "shard.hip"), os.path.join(SRC, "group.hip"), "-lrccl"]
     if stamps:
         cmd.insert(3, "-DSHP_SW_STAMPS")
     if verbose:

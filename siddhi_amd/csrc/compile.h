@@ -27,7 +27,7 @@ class ProgramCompiler {
  public:
   DevProg P{};
   FastShape fast{};
-  // select-side aggregate over the matches (SHP_LAYOUT_AGG): 0 none, 1 avg, 2 sum, 3 count;
+  // select-side aggregate over the matches (SHP_LAYOUT_AGG): 0 none, 1 avg, 2 sum, 3 count, 4 min, 5 max;
   // over the value of state agg_state in predicate column agg_col (count: no argument)
   int agg_fn = 0, agg_state = -1, agg_col = -1;
 
@@ -36,8 +36,8 @@ class ProgramCompiler {
     if (root.present("aggregate")) {
       const JV& a = root.get("aggregate");
       const std::string& fn = a.get("fn").sv;
-      agg_fn = fn == "avg" ? 1 : fn == "sum" ? 2 : fn == "count" ? 3 : 0;
-      if (!agg_fn) throw CompileError(-2, "aggregate: avg, sum or count");
+      agg_fn = fn == "avg" ? 1 : fn == "sum" ? 2 : fn == "count" ? 3 : fn == "min" ? 4 : fn == "max" ? 5 : 0;
+      if (!agg_fn) throw CompileError(-2, "aggregate: avg, sum, count, min or max");
       agg_state = a.present("state") ? (int)a.get("state").i() : -1;
       agg_col = a.present("column") ? (int)a.get("column").i() : -1;
     }

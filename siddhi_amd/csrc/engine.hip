@@ -213,6 +213,7 @@ struct shp_engine {
   // batch buffers
   int64_t cap = 0;
   int64_t* d_ts = nullptr;
+  int64_t *d_clk = nullptr, *d_seq = nullptr;  // staged optional columns (host pushes)
   int32_t* d_key = nullptr;
   int32_t* d_stream = nullptr;
   void* d_cols[MAXCOL] = {};
@@ -260,6 +261,8 @@ struct shp_engine {
     F(dprog);
     F(arena);
     F(d_ts);
+    F(d_clk);
+    F(d_seq);
     F(d_key);
     F(d_stream);
     for (int c = 0; c < MAXCOL; c++) {
@@ -347,6 +350,8 @@ struct shp_engine {
     kt.enabled = cfg.profile_kernels != 0;
     cap = cfg.max_batch + 1;
     alloc(d_ts, cap);
+    alloc(d_clk, cap);
+    alloc(d_seq, cap);
     alloc(d_key, cap);
     alloc(d_stream, cap);
     for (int i = 0; i < comp.P.ncol; i++) {
@@ -415,9 +420,14 @@ struct shp_engine {
 
   // runs the pipeline over n events at device pointers `in` (engine buffers after stage(), or
   // the caller's HBM columns for shp_push_batch_device); leaves matches in HBM
-  int run(int64_t n, bool clock_only = false, const shp_batch* in = nullptr) {
+  int run(int64_t n, bool clock_only = false, const shp_batch* in = nullptr, bool staged_clk = false,
+          bool staged_seq = false) {
     const DevProg& P = comp.P;
     const int64_t* x_ts = in ? in->ts : d_ts;
+    const int64_t* x_clk = in ? in->clock : (staged_clk ? d_clk : nullptr);
+    const int64_t* x_seq = in ? in->seq : (staged_seq ? d_seq : nullptr);
+    if (x_seq && cfg.match_layout == SHP_LAYOUT_PAIRS)
+      return fail(SHP_ERR_ARG, "a seq column needs match layout FULL, PAIRS32 or AGG");
     const int32_t* x_key = in ? (P.partitioned ? in->key : d_key) : d_key;
     const int32_t* x_stream = in ? in->stream : d_stream;
     if (in && !P.partitioned && fast != 2) HIP_OK(hipMemsetAsync(d_key, 0, n * 4, stream));
@@ -435,6 +445,8 @@ struct shp_engine {
     B.init_clock = cfg.start_clock;
     B.partitioned = P.partitioned;
     B.ts = x_ts;
+    B.tclk = x_clk ? x_clk : x_ts;
+    B.seq = x_seq;
     B.stream = x_stream;
     B.rmax = d_rmax;
     for (int c = 0; c < P.ncol; c++) {
@@ -462,7 +474,7 @@ struct shp_engine {
       // 1. clock
       size_t tb = tmp_bytes;
       kt.mark("clock_scan", stream);
-      HIP_OK(rocprim::inclusive_scan(d_tmp, tb, x_ts, d_rmax, (size_t)n, rocprim::maximum<int64_t>(), stream));
+      HIP_OK(rocprim::inclusive_scan(d_tmp, tb, B.tclk, d_rmax, (size_t)n, rocprim::maximum<int64_t>(), stream));
       kt.mark("clamp_clock", stream);
       k_clamp_clock<<<gb, 256, 0, stream>>>(d_rmax, n, clock);
       // 2. partition by key (stable)
@@ -666,6 +678,8 @@ struct shp_engine {
     const DevProg& P = comp.P;
     int64_t n = in->n;
     HIP_OK(hipMemcpyAsync(d_ts, in->ts, n * 8, kind, stream));
+    if (in->clock) HIP_OK(hipMemcpyAsync(d_clk, in->clock, n * 8, kind, stream));
+    if (in->seq) HIP_OK(hipMemcpyAsync(d_seq, in->seq, n * 8, kind, stream));
     if (P.partitioned) HIP_OK(hipMemcpyAsync(d_key, in->key, n * 4, kind, stream));
     else HIP_OK(hipMemsetAsync(d_key, 0, n * 4, stream));
     if (in->stream) HIP_OK(hipMemcpyAsync(d_stream, in->stream, n * 4, kind, stream));
@@ -859,7 +873,7 @@ int shp_push_batch(shp_engine* e, const shp_batch* in, shp_matches* out) {
     int64_t n = in->n;
     if (n > e->cfg.max_batch) return e->fail(SHP_ERR_ARG, "batch larger than max_batch");
     e->stage(in, hipMemcpyHostToDevice);
-    int rc = e->run(n);
+    int rc = e->run(n, false, nullptr, in->clock != nullptr, in->seq != nullptr);
     if (rc != SHP_OK) return rc;
     e->fetch(out);
     (void)done;

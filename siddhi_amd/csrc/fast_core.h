@@ -272,7 +272,7 @@ SHP_HD inline void fast_emit_item(const FastDev& F, const BatchView& B, const Ma
   int64_t base = F.moff[q];
   if (base + cnt > O.cap) return;
   int64_t tq = F.s_ts[q];
-  int64_t seqq = B.seq0 + perm[q];
+  int64_t seqq = bseq(B, perm[q]);
   uint32_t w = 0;
   auto put = [&](int64_t seqi, uint32_t slot) {
     int64_t m = base + slot;
@@ -298,7 +298,7 @@ SHP_HD inline void fast_emit_item(const FastDev& F, const BatchView& B, const Ma
   for (int64_t i = q - 1; i >= (int64_t)kbeg[k] && placed < nb; i--) {
     if (!slow && tq - F.s_ts[i] > F.within) break;
     if (F.match[i] == (int32_t)q) {
-      put(B.seq0 + perm[i], w + nb - 1 - placed);
+      put(bseq(B, perm[i]), w + nb - 1 - placed);
       placed++;
     }
   }
@@ -342,7 +342,7 @@ SHP_HD inline void fast_carry_item(const FastDev& F, const BatchView& B, const u
       break;
     }
     int64_t c = base + w;
-    F.c_seq[c] = B.seq0 + perm[i];
+    F.c_seq[c] = bseq(B, perm[i]);
     F.c_ts[c] = F.s_ts[i];
     F.c_val[2 * c] = F.s_val[2 * i];
     F.c_val[2 * c + 1] = F.s_val[2 * i + 1];

@@ -1,0 +1,715 @@
+// siddhi-hip: key-sharded engine groups — multi-GPU behind the C-ABI ("Multi-GPU
+// is internal to the engine, which owns the RCCL communicator"; §8e).
+//
+// A partitioned query's per-key state is isolated (PartitionStateHolder.java:43-48), so `world`
+// engines split the keys: key k lives on rank k % world, as the dense id k / world there (the
+// reference's own precedent for spreading by key is PartitionedDistributionStrategy.java:99-110).
+// A push hands every rank one slice of the global stream (consecutive pieces, in rank order).
+// Per push:
+//   1. split   each rank splits its slice by destination rank, stable (HIP, k_gs_count +
+//              k_gs_scatter below), into destination-grouped columns: ts, key / world, the
+//              predicate columns, stream, and when the query needs them the global playback
+//              clock (absent-state timers) and the events' global sequence numbers (match
+//              records that name events);
+//   2. counts  every rank learns every rank's counts, slice length and largest ts (the global
+//              clock seed and sequence base): RCCL all-gather between processes, a host read
+//              within one process;
+//   3. exchange the columns go to their owners: grouped ncclSend / ncclRecv over xGMI between
+//              processes, device-to-device copies within one process.  A rank receives its
+//              events ordered by source rank, then arrival, i.e. in global order, so each key
+//              sees its events in the reference's order;
+//   4. run     each rank's engine processes what it received (shp_push_batch_device), plus one
+//              clock-only event at the push's global clock so timers due before the end of the
+//              global batch fire in this push as they do in one process.
+// Clock-only events of the slices (stream -1) are not moved: the global clock column carries
+// their effect.  Sharded absent-state timers are exact when every rank sees one of its own events
+// at least every `waitingTime` of global clock (true for SURVEY §8d C4's dense stream): a timer
+// then fires late on a rank by less than waitingTime, which leaves lastScheduledTime as in one
+// process (AbsentStreamPreStateProcessor.java:216-223).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <rocprim/rocprim.hpp>
+
+#include "../../include/siddhi_hip.h"
+#include "compile.h"
+
+namespace {
+
+constexpr int GS_THREADS = 256;
+constexpr int GS_TILE = 65536;  // events per split workgroup
+constexpr int GS_MAXG = 16;
+constexpr int GS_MAXCOL = 12;
+
+// columns moved by the split: in[c] (4 or 8 bytes per event) -> out[c] grouped by destination
+struct GsCols {
+  int32_t n;
+  int32_t sz[GS_MAXCOL];
+  const void* in[GS_MAXCOL];
+  void* out[GS_MAXCOL];
+};
+
+// per tile: events per destination (clock-only events go nowhere) and the tile's largest ts
+__global__ __launch_bounds__(GS_THREADS) void k_gs_count(const int32_t* __restrict__ key,
+                                                         const int32_t* __restrict__ stream,
+                                                         const int64_t* __restrict__ ts, int64_t n, int G,
+                                                         int ntiles, uint32_t* cnt, unsigned long long* tsmax) {
+  __shared__ uint32_t h[GS_MAXG];
+  if (threadIdx.x < GS_MAXG) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int t = blockIdx.x;
+  const int64_t lo = (int64_t)t * GS_TILE, hi = min(n, lo + GS_TILE);
+  uint32_t c[GS_MAXG] = {};
+  int64_t mx = INT64_MIN;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += GS_THREADS) {
+    mx = max(mx, ts[i]);
+    if (stream && stream[i] < 0) continue;
+    const uint32_t d = (uint32_t)key[i] % (uint32_t)G;
+#pragma unroll
+    for (int g = 0; g < GS_MAXG; g++) c[g] += d == (uint32_t)g ? 1u : 0u;
+  }
+  for (int g = 0; g < G; g++)
+    if (c[g]) atomicAdd(&h[g], c[g]);
+  for (int d = 32; d > 0; d >>= 1) mx = max(mx, (int64_t)__shfl_xor((long long)mx, d, 64));
+  if (__lane_id() == 0 && mx != INT64_MIN) atomicMax(tsmax, (unsigned long long)mx ^ (1ull << 63));
+  __syncthreads();
+  if (threadIdx.x < G) cnt[(int64_t)threadIdx.x * ntiles + t] = h[threadIdx.x];
+}
+
+// exclusive scan of the G x ntiles counts (destination-major), one workgroup; total per
+// destination to tot[g]
+__global__ __launch_bounds__(1024) void k_gs_scan(const uint32_t* cnt, uint32_t* off, int64_t m, int G, int ntiles,
+                                                  int64_t* tot) {
+  __shared__ uint32_t part[1024];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t b = 0; b < m; b += 1024) {
+    const int64_t i = b + threadIdx.x;
+    const uint32_t v = i < m ? cnt[i] : 0u;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+      const uint32_t y = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0u;
+      __syncthreads();
+      part[threadIdx.x] += y;
+      __syncthreads();
+    }
+    if (i < m) off[i] = carry + part[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) off[m] = carry;
+  __syncthreads();
+  if (threadIdx.x < G) tot[threadIdx.x] = (int64_t)off[(int64_t)(threadIdx.x + 1) * ntiles] - off[(int64_t)threadIdx.x * ntiles];
+}
+
+// stable split: per tile, rounds of 64 * SUB events per wave ranked by destination with wave
+// ballots; per-wave running cursors.  Columns are written at their destination-grouped slot.
+// Derived columns: key -> key / G; gclk -> max(seed, running max of ts) (the global clock);
+// gseq -> seq_base + index.
+template <int SUB>
+__global__ __launch_bounds__(GS_THREADS) void k_gs_scatter(const int32_t* __restrict__ key,
+                                                           const int32_t* __restrict__ stream,
+                                                           const int64_t* __restrict__ ts,
+                                                           const int64_t* __restrict__ rmax, int64_t n, int G,
+                                                           int gbits, int ntiles, const uint32_t* __restrict__ off,
+                                                           GsCols cols, int32_t* okey, int64_t* oclk, int64_t seed,
+                                                           int64_t* oseq, int64_t seq_base) {
+  constexpr int NW = GS_THREADS / 64;
+  __shared__ uint32_t wc[NW][GS_MAXG];
+  __shared__ uint32_t run[GS_MAXG];
+  const int t = blockIdx.x;
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  if (threadIdx.x < G) run[threadIdx.x] = off[(int64_t)threadIdx.x * ntiles + t];
+  const int64_t lo = (int64_t)t * GS_TILE, hi = min(n, lo + GS_TILE);
+  constexpr int ROUND = GS_THREADS * SUB;
+  for (int64_t r0 = lo; r0 < hi; r0 += ROUND) {
+    if (threadIdx.x < NW * GS_MAXG) (&wc[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t dst[SUB], rk[SUB];
+#pragma unroll
+    for (int s = 0; s < SUB; s++) {
+      const int64_t i = r0 + (int64_t)w * (64 * SUB) + s * 64 + lane;
+      dst[s] = GS_MAXG;
+      if (i < hi && !(stream && stream[i] < 0)) dst[s] = (uint32_t)key[i] % (uint32_t)G;
+    }
+#pragma unroll
+    for (int s = 0; s < SUB; s++) {
+      const bool valid = dst[s] < GS_MAXG;
+      uint64_t peers = __ballot(valid);
+      for (int b = 0; b < gbits; b++) {
+        const bool bit = (dst[s] >> b) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      const uint32_t before = valid ? wc[w][dst[s]] : 0u;
+      rk[s] = before + (uint32_t)__popcll(peers & lt);
+      if (valid && (peers & lt) == 0) wc[w][dst[s]] = before + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // wave cursors: destinations x waves, in order
+      for (int d = 0; d < G; d++) {
+        uint32_t g = run[d];
+        for (int ww = 0; ww < NW; ww++) {
+          const uint32_t c = wc[ww][d];
+          wc[ww][d] = g;
+          g += c;
+        }
+        run[d] = g;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < SUB; s++) {
+      if (dst[s] >= GS_MAXG) continue;
+      const int64_t i = r0 + (int64_t)w * (64 * SUB) + s * 64 + lane;
+      const uint32_t o = wc[w][dst[s]] + rk[s];
+      okey[o] = (int32_t)((uint32_t)key[i] / (uint32_t)G);
+      for (int c = 0; c < cols.n; c++) {
+        if (cols.sz[c] == 8) ((int64_t*)cols.out[c])[o] = ((const int64_t*)cols.in[c])[i];
+        else ((int32_t*)cols.out[c])[o] = ((const int32_t*)cols.in[c])[i];
+      }
+      if (oclk) oclk[o] = max(seed, rmax[i]);
+      if (oseq) oseq[o] = seq_base + i;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_gs_fill_tail(int64_t* ts, int32_t* key, int32_t* stream, int64_t* clk, int64_t* seq, int64_t at,
+                               int64_t clock, int64_t seqv) {
+  ts[at] = clock;
+  key[at] = 0;
+  stream[at] = -1;
+  if (clk) clk[at] = clock;
+  if (seq) seq[at] = seqv;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(b, 256)) != hipSuccess) throw std::runtime_error("hipMalloc failed (group)");
+    bytes = std::max<size_t>(b, 256);
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+int col_bytes(int8_t tag) { return (tag == shp::T_LONG || tag == shp::T_DOUBLE) ? 8 : (tag == shp::T_BOOL ? 1 : 4); }
+
+}  // namespace
+
+struct shp_group {
+  int world = 1;
+  int rank0 = 0;  // rank of local slot 0
+  int nlocal = 1;
+  bool rccl = false;
+  ncclComm_t comm = nullptr;
+  shp_config cfg{};
+  shp::ProgramCompiler comp;
+  bool need_clock = false, need_seq = false, has_stream_col = false;
+  int ncol = 0;
+  std::vector<int8_t> ctag;
+  struct Local {
+    int dev = 0;
+    int rank = 0;
+    shp_engine* eng = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t split_done = nullptr;
+    // split workspace
+    DevBuf cnt, off, tot, tsmax, rmax, scan_tmp;
+    // send (destination-grouped) and receive columns: ts, key, stream, clock, seq, predicate columns
+    DevBuf s_ts, s_key, s_stream, s_clk, s_seq, r_ts, r_key, r_stream, r_clk, r_seq;
+    DevBuf s_col[shp::MAXCOL], r_col[shp::MAXCOL];
+    int64_t n_slice = 0;
+    int64_t max_ts = INT64_MIN;
+    std::vector<int64_t> send_cnt;  // per destination
+    std::vector<int64_t> recv_cnt;  // per source
+    int64_t n_recv = 0;
+    int64_t last_m = 0;
+  };
+  std::vector<Local> L;
+  int64_t seq = 0;              // global sequence number of the next push's first event
+  int64_t clock = INT64_MIN;    // global playback clock
+  std::string err;
+  // host copies of the last fetch
+  std::vector<int32_t> h_key;
+  std::vector<int64_t> h_ts, h_pos, h_off, h_refs;
+  std::vector<int8_t> h_type;
+  std::vector<int16_t> h_slot;
+  std::vector<double> h_agg;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+};
+
+namespace {
+
+#define GH(x)                                                                               \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define GN(x)                                                                                \
+  do {                                                                                       \
+    ncclResult_t r_ = (x);                                                                   \
+    if (r_ != ncclSuccess) throw std::runtime_error(std::string(#x) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+// step 1a: per-destination counts, slice length and largest ts (device -> host)
+void split_count(shp_group& g, shp_group::Local& l, const shp_batch& b) {
+  GH(hipSetDevice(l.dev));
+  const int G = g.world;
+  const int64_t n = b.n;
+  const int ntiles = (int)std::max<int64_t>(1, (n + GS_TILE - 1) / GS_TILE);
+  l.cnt.ensure((size_t)G * ntiles * 4 + 4);
+  l.off.ensure(((size_t)G * ntiles + 1) * 4);
+  l.tot.ensure(GS_MAXG * 8);
+  l.tsmax.ensure(8);
+  GH(hipMemsetAsync(l.tsmax.p, 0, 8, l.s));
+  GH(hipMemsetAsync(l.cnt.p, 0, (size_t)G * ntiles * 4, l.s));
+  if (n > 0)
+    k_gs_count<<<ntiles, GS_THREADS, 0, l.s>>>(b.key, b.stream, b.ts, n, G, ntiles, (uint32_t*)l.cnt.p,
+                                               (unsigned long long*)l.tsmax.p);
+  k_gs_scan<<<1, 1024, 0, l.s>>>((const uint32_t*)l.cnt.p, (uint32_t*)l.off.p, (int64_t)G * ntiles, G, ntiles,
+                                 (int64_t*)l.tot.p);
+  GH(hipGetLastError());
+  std::vector<int64_t> tot(GS_MAXG);
+  unsigned long long mx = 0;
+  GH(hipMemcpyAsync(tot.data(), l.tot.p, GS_MAXG * 8, hipMemcpyDeviceToHost, l.s));
+  GH(hipMemcpyAsync(&mx, l.tsmax.p, 8, hipMemcpyDeviceToHost, l.s));
+  GH(hipStreamSynchronize(l.s));
+  l.send_cnt.assign(tot.begin(), tot.begin() + G);
+  l.n_slice = n;
+  l.max_ts = mx ? (int64_t)(mx ^ (1ull << 63)) : INT64_MIN;
+}
+
+// step 1b: the scatter into destination-grouped send columns
+void split_scatter(shp_group& g, shp_group::Local& l, const shp_batch& b, int64_t clock_seed, int64_t seq_base) {
+  GH(hipSetDevice(l.dev));
+  const int G = g.world;
+  const int64_t n = b.n;
+  const int ntiles = (int)std::max<int64_t>(1, (n + GS_TILE - 1) / GS_TILE);
+  const size_t cap = (size_t)std::max<int64_t>(n, 1);
+  l.s_ts.ensure(cap * 8);
+  l.s_key.ensure(cap * 4);
+  GsCols cols{};
+  cols.n = 0;
+  auto add = [&](const void* in, DevBuf& out, int sz) {
+    out.ensure(cap * sz);
+    cols.in[cols.n] = in;
+    cols.out[cols.n] = out.p;
+    cols.sz[cols.n] = sz;
+    cols.n++;
+  };
+  add(b.ts, l.s_ts, 8);
+  if (g.has_stream_col) add(b.stream, l.s_stream, 4);
+  for (int c = 0; c < g.ncol; c++) {
+    const int sz = col_bytes(g.ctag[c]);
+    if (sz == 1) throw std::runtime_error("group: bool columns are not exchanged");
+    add(b.cols[c], l.s_col[c], sz);
+  }
+  int64_t* oclk = nullptr;
+  if (g.need_clock && n > 0) {  // the global clock after each event: running max of ts, seeded
+    l.rmax.ensure(cap * 8);
+    size_t tb = 0;
+    GH(rocprim::inclusive_scan(nullptr, tb, b.ts, (int64_t*)l.rmax.p, (size_t)n, rocprim::maximum<int64_t>(), l.s));
+    l.scan_tmp.ensure(tb);
+    GH(rocprim::inclusive_scan(l.scan_tmp.p, tb, b.ts, (int64_t*)l.rmax.p, (size_t)n, rocprim::maximum<int64_t>(),
+                               l.s));
+    l.s_clk.ensure(cap * 8);
+    oclk = (int64_t*)l.s_clk.p;
+  }
+  int64_t* oseq = nullptr;
+  if (g.need_seq) {
+    l.s_seq.ensure(cap * 8);
+    oseq = (int64_t*)l.s_seq.p;
+  }
+  int gbits = 0;
+  while ((1 << gbits) < G) gbits++;
+  if (n > 0)
+    k_gs_scatter<8><<<ntiles, GS_THREADS, 0, l.s>>>(b.key, b.stream, b.ts, (const int64_t*)l.rmax.p, n, G, gbits,
+                                                   ntiles, (const uint32_t*)l.off.p, cols, (int32_t*)l.s_key.p, oclk,
+                                                   clock_seed, oseq, seq_base);
+  GH(hipGetLastError());
+  GH(hipEventRecord(l.split_done, l.s));
+}
+
+void ensure_recv(shp_group& g, shp_group::Local& l, int64_t n) {
+  const size_t cap = (size_t)n + 1;  // + the end-of-push clock event
+  l.r_ts.ensure(cap * 8);
+  l.r_key.ensure(cap * 4);
+  l.r_stream.ensure(cap * 4);
+  if (g.need_clock) l.r_clk.ensure(cap * 8);
+  if (g.need_seq) l.r_seq.ensure(cap * 8);
+  for (int c = 0; c < g.ncol; c++) l.r_col[c].ensure(cap * col_bytes(g.ctag[c]));
+}
+
+// the columns exchanged, as (send buffer, receive buffer, bytes per event)
+std::vector<std::tuple<void*, void*, int>> column_pairs(shp_group& g, shp_group::Local& src, shp_group::Local& dst) {
+  std::vector<std::tuple<void*, void*, int>> v = {{src.s_ts.p, dst.r_ts.p, 8}, {src.s_key.p, dst.r_key.p, 4}};
+  if (g.has_stream_col) v.emplace_back(src.s_stream.p, dst.r_stream.p, 4);
+  if (g.need_clock) v.emplace_back(src.s_clk.p, dst.r_clk.p, 8);
+  if (g.need_seq) v.emplace_back(src.s_seq.p, dst.r_seq.p, 8);
+  for (int c = 0; c < g.ncol; c++) v.emplace_back(src.s_col[c].p, dst.r_col[c].p, col_bytes(g.ctag[c]));
+  return v;
+}
+
+// step 4: one engine push of what a rank received, plus the end-of-push clock event
+int run_local(shp_group& g, shp_group::Local& l, int64_t push_clock, int64_t next_seq) {
+  GH(hipSetDevice(l.dev));
+  const int64_t m = l.n_recv;
+  const bool tail = g.need_clock && push_clock != INT64_MIN;
+  if (!g.has_stream_col) GH(hipMemsetAsync(l.r_stream.p, 0, (size_t)m * 4, l.s));
+  if (tail)
+    k_gs_fill_tail<<<1, 1, 0, l.s>>>((int64_t*)l.r_ts.p, (int32_t*)l.r_key.p, (int32_t*)l.r_stream.p,
+                                     g.need_clock ? (int64_t*)l.r_clk.p : nullptr,
+                                     g.need_seq ? (int64_t*)l.r_seq.p : nullptr, m, push_clock, next_seq);
+  GH(hipStreamSynchronize(l.s));
+  std::vector<const void*> colp(std::max(1, g.ncol));
+  for (int c = 0; c < g.ncol; c++) colp[c] = l.r_col[c].p;
+  shp_batch b{};
+  b.n = m + (tail ? 1 : 0);
+  b.ts = (const int64_t*)l.r_ts.p;
+  b.key = (const int32_t*)l.r_key.p;
+  b.stream = (const int32_t*)l.r_stream.p;
+  b.cols = colp.data();
+  b.nulls = nullptr;
+  b.clock = g.need_clock ? (const int64_t*)l.r_clk.p : nullptr;
+  b.seq = g.need_seq ? (const int64_t*)l.r_seq.p : nullptr;
+  if (b.n == 0) {
+    l.last_m = 0;
+    return SHP_OK;
+  }
+  shp_matches mt{};
+  const int rc = shp_push_batch_device(l.eng, &b, &mt);
+  if (rc != SHP_OK) {
+    g.err = std::string("rank ") + std::to_string(l.rank) + ": " + shp_last_error(l.eng);
+    return rc;
+  }
+  l.last_m = mt.m;
+  return SHP_OK;
+}
+
+int push_impl(shp_group& g, const shp_batch* slices, int64_t* counts) {
+  const int G = g.world;
+  // 1a + 2: counts, slice lengths, largest ts of every rank
+  for (int i = 0; i < g.nlocal; i++) split_count(g, g.L[i], slices[i]);
+  std::vector<int64_t> all((size_t)G * (G + 2));  // per rank: counts[G], n, maxts
+  if (g.rccl) {
+    shp_group::Local& l = g.L[0];
+    DevBuf mine, gath;
+    mine.ensure((G + 2) * 8);
+    gath.ensure((size_t)G * (G + 2) * 8);
+    std::vector<int64_t> v(l.send_cnt);
+    v.push_back(l.n_slice);
+    v.push_back(l.max_ts);
+    GH(hipMemcpyAsync(mine.p, v.data(), (G + 2) * 8, hipMemcpyHostToDevice, l.s));
+    GN(ncclAllGather(mine.p, gath.p, (size_t)(G + 2), ncclInt64, g.comm, l.s));
+    GH(hipMemcpyAsync(all.data(), gath.p, all.size() * 8, hipMemcpyDeviceToHost, l.s));
+    GH(hipStreamSynchronize(l.s));
+  } else {
+    for (int i = 0; i < g.nlocal; i++) {
+      shp_group::Local& l = g.L[i];
+      for (int d = 0; d < G; d++) all[(size_t)l.rank * (G + 2) + d] = l.send_cnt[d];
+      all[(size_t)l.rank * (G + 2) + G] = l.n_slice;
+      all[(size_t)l.rank * (G + 2) + G + 1] = l.max_ts;
+    }
+  }
+  auto cnt = [&](int s, int d) { return all[(size_t)s * (G + 2) + d]; };
+  std::vector<int64_t> base(G + 1, g.seq), seed(G + 1, g.clock);
+  for (int r = 0; r < G; r++) {
+    base[r + 1] = base[r] + all[(size_t)r * (G + 2) + G];
+    seed[r + 1] = std::max(seed[r], all[(size_t)r * (G + 2) + G + 1]);
+  }
+  const int64_t push_clock = seed[G];
+  for (int i = 0; i < g.nlocal; i++) {
+    shp_group::Local& l = g.L[i];
+    l.recv_cnt.assign(G, 0);
+    l.n_recv = 0;
+    for (int s = 0; s < G; s++) {
+      l.recv_cnt[s] = cnt(s, l.rank);
+      l.n_recv += l.recv_cnt[s];
+    }
+    if (l.n_recv + 1 > g.cfg.max_batch)
+      return g.fail(SHP_ERR_CAPACITY, "rank " + std::to_string(l.rank) + " would receive " +
+                                          std::to_string(l.n_recv) + " events (> max_batch)");
+  }
+  // 1b: scatter
+  for (int i = 0; i < g.nlocal; i++) split_scatter(g, g.L[i], slices[i], seed[g.L[i].rank], base[g.L[i].rank]);
+  for (int i = 0; i < g.nlocal; i++) ensure_recv(g, g.L[i], g.L[i].n_recv);
+  // 3: exchange
+  if (g.rccl) {
+    shp_group::Local& l = g.L[0];
+    GH(hipSetDevice(l.dev));
+    auto cols = column_pairs(g, l, l);
+    GN(ncclGroupStart());
+    for (auto& c : cols) {
+      void* sb = std::get<0>(c);
+      void* rb = std::get<1>(c);
+      const int sz = std::get<2>(c);
+      int64_t so = 0, ro = 0;
+      for (int p = 0; p < G; p++) {
+        const int64_t sn = l.send_cnt[p], rn = l.recv_cnt[p];
+        if (sn) GN(ncclSend((char*)sb + so * sz, (size_t)sn * sz, ncclChar, p, g.comm, l.s));
+        if (rn) GN(ncclRecv((char*)rb + ro * sz, (size_t)rn * sz, ncclChar, p, g.comm, l.s));
+        so += sn;
+        ro += rn;
+      }
+    }
+    GN(ncclGroupEnd());
+  } else {
+    for (int di = 0; di < g.nlocal; di++) {
+      shp_group::Local& dst = g.L[di];
+      GH(hipSetDevice(dst.dev));
+      int64_t ro = 0;
+      for (int si = 0; si < g.nlocal; si++) {
+        shp_group::Local& src = g.L[si];
+        GH(hipStreamWaitEvent(dst.s, src.split_done, 0));
+        int64_t so = 0;
+        for (int d = 0; d < dst.rank; d++) so += src.send_cnt[d];
+        const int64_t k = src.send_cnt[dst.rank];
+        if (k)
+          for (auto& c : column_pairs(g, src, dst)) {
+            const int sz = std::get<2>(c);
+            GH(hipMemcpyPeerAsync((char*)std::get<1>(c) + ro * sz, dst.dev, (char*)std::get<0>(c) + so * sz, src.dev,
+                                  (size_t)k * sz, dst.s));
+          }
+        ro += k;
+      }
+    }
+  }
+  // 4: every local engine runs what it received (one host thread per engine: GPUs overlap)
+  const int64_t next_seq = base[G];
+  std::vector<int> rcs(g.nlocal, SHP_OK);
+  std::vector<std::string> errs(g.nlocal);
+  if (g.nlocal == 1) {
+    rcs[0] = run_local(g, g.L[0], push_clock, next_seq);
+  } else {
+    std::vector<std::thread> th;
+    for (int i = 0; i < g.nlocal; i++)
+      th.emplace_back([&, i]() {
+        try {
+          rcs[i] = run_local(g, g.L[i], push_clock, next_seq);
+        } catch (std::exception& ex) {
+          errs[i] = ex.what();
+          rcs[i] = SHP_ERR_DEVICE;
+        }
+      });
+    for (auto& t : th) t.join();
+  }
+  for (int i = 0; i < g.nlocal; i++) {
+    if (!errs[i].empty()) return g.fail(rcs[i], errs[i]);
+    if (rcs[i] != SHP_OK) return rcs[i];
+  }
+  g.seq = next_seq;
+  if (push_clock != INT64_MIN) g.clock = std::max(g.clock, push_clock);
+  if (counts)
+    for (int i = 0; i < g.nlocal; i++) counts[i] = g.L[i].last_m;
+  return SHP_OK;
+}
+
+int create_impl(shp_group* g, const char* json, const shp_config* cfg, int world, const int32_t* devices, int rank,
+                const void* comm_id) {
+  if (world < 1 || world > GS_MAXG) return g->fail(SHP_ERR_ARG, "world must be in [1, 16]");
+  g->world = world;
+  g->cfg = *cfg;
+  g->comp.compile(json);
+  const shp::DevProg& P = g->comp.P;
+  if (!P.partitioned && world > 1) return g->fail(SHP_ERR_UNSUPPORTED, "only partitioned queries shard by key");
+  g->need_clock = P.nsched > 0 && P.playback;  // absent-state timers read the playback clock
+  g->need_seq = cfg->match_layout == SHP_LAYOUT_FULL;
+  g->has_stream_col = P.nstream > 1;
+  g->ncol = P.ncol;
+  g->ctag.assign(P.colTag, P.colTag + P.ncol);
+  shp_config ec = *cfg;
+  ec.max_keys = (int32_t)((cfg->max_keys + world - 1) / world);
+  g->nlocal = comm_id ? 1 : world;
+  g->rank0 = comm_id ? rank : 0;
+  g->L.resize(g->nlocal);
+  g->clock = cfg->start_clock;
+  for (int i = 0; i < g->nlocal; i++) {
+    shp_group::Local& l = g->L[i];
+    l.rank = g->rank0 + i;
+    l.dev = comm_id ? cfg->device : devices[i];
+    ec.device = l.dev;
+    GH(hipSetDevice(l.dev));
+    GH(hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking));
+    GH(hipEventCreateWithFlags(&l.split_done, hipEventDisableTiming));
+    const int rc = shp_engine_create(json, &ec, &l.eng);
+    if (rc != SHP_OK) return g->fail(rc, "engine creation failed on rank " + std::to_string(l.rank));
+  }
+  if (comm_id && world > 1) {
+    g->rccl = true;
+    ncclUniqueId id;
+    std::memcpy(&id, comm_id, sizeof id);
+    GH(hipSetDevice(g->L[0].dev));
+    GN(ncclCommInitRank(&g->comm, world, id, rank));
+  }
+  return SHP_OK;
+}
+
+void destroy_impl(shp_group* g) {
+  if (g->comm) (void)ncclCommDestroy(g->comm);
+  for (auto& l : g->L) {
+    (void)hipSetDevice(l.dev);
+    if (l.eng) shp_engine_destroy(l.eng);
+    if (l.split_done) (void)hipEventDestroy(l.split_done);
+    if (l.s) (void)hipStreamDestroy(l.s);
+  }
+}
+
+template <class F>
+int guarded(shp_group* g, F&& f) {
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  int rc;
+  try {
+    rc = f();
+  } catch (shp::CompileError& ce) {
+    g->err = ce.what();
+    rc = ce.code == -2 ? SHP_ERR_UNSUPPORTED : SHP_ERR_ARG;
+  } catch (std::exception& ex) {
+    g->err = ex.what();
+    rc = SHP_ERR_DEVICE;
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int shp_comm_id(void* id, size_t len) {
+  if (!id || len < sizeof(ncclUniqueId)) return SHP_ERR_ARG;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return SHP_ERR_DEVICE;
+  std::memcpy(id, &u, sizeof u);
+  return SHP_OK;
+}
+
+int shp_group_create(const char* json, const shp_config* cfg, int32_t world, const int32_t* devices,
+                     shp_group** out) {
+  if (!json || !cfg || !devices || !out) return SHP_ERR_ARG;
+  auto* g = new shp_group();
+  const int rc = guarded(g, [&]() { return create_impl(g, json, cfg, world, devices, 0, nullptr); });
+  if (rc != SHP_OK) {
+    fprintf(stderr, "shp_group_create: %s\n", g->err.c_str());
+    destroy_impl(g);
+    delete g;
+    *out = nullptr;
+    return rc;
+  }
+  *out = g;
+  return SHP_OK;
+}
+
+int shp_group_create_rank(const char* json, const shp_config* cfg, int32_t world, int32_t rank, const void* comm_id,
+                          shp_group** out) {
+  if (!json || !cfg || !comm_id || !out || rank < 0 || rank >= world) return SHP_ERR_ARG;
+  auto* g = new shp_group();
+  const int rc = guarded(g, [&]() { return create_impl(g, json, cfg, world, nullptr, rank, comm_id); });
+  if (rc != SHP_OK) {
+    fprintf(stderr, "shp_group_create_rank: %s\n", g->err.c_str());
+    destroy_impl(g);
+    delete g;
+    *out = nullptr;
+    return rc;
+  }
+  *out = g;
+  return SHP_OK;
+}
+
+int shp_group_push(shp_group* g, const shp_batch* slices, int64_t* matches) {
+  if (!g || !slices) return SHP_ERR_ARG;
+  return guarded(g, [&]() { return push_impl(*g, slices, matches); });
+}
+
+int shp_group_local_engines(const shp_group* g) { return g ? g->nlocal : 0; }
+
+shp_engine* shp_group_engine(shp_group* g, int32_t i) {
+  return (g && i >= 0 && i < g->nlocal) ? g->L[i].eng : nullptr;
+}
+
+int shp_group_fetch_matches(shp_group* g, shp_matches* out) {
+  if (!g || !out) return SHP_ERR_ARG;
+  return guarded(g, [&]() {
+    g->h_key.clear();
+    g->h_ts.clear();
+    g->h_pos.clear();
+    g->h_off.clear();
+    g->h_refs.clear();
+    g->h_type.clear();
+    g->h_slot.clear();
+    g->h_agg.clear();
+    int layout = SHP_LAYOUT_FULL, S = shp_engine_num_states(g->L[0].eng);
+    for (auto& l : g->L) {
+      shp_matches m{};
+      const int rc = shp_fetch_matches(l.eng, &m);
+      if (rc != SHP_OK) return g->fail(rc, std::string("rank ") + std::to_string(l.rank) + ": " + shp_last_error(l.eng));
+      layout = m.layout;
+      for (int64_t i = 0; i < m.m; i++)  // rank-local dense key ids -> the global ones
+        g->h_key.push_back((int32_t)((int64_t)m.key[i] * g->world + l.rank));
+      if (m.layout == SHP_LAYOUT_AGG) {
+        g->h_agg.insert(g->h_agg.end(), m.agg, m.agg + m.m);
+        continue;
+      }
+      const int64_t r0 = (int64_t)g->h_refs.size();
+      int64_t nr = 0;
+      for (int64_t i = 0; i < m.m * S; i++) nr += m.slot_len[i];
+      g->h_ts.insert(g->h_ts.end(), m.ts, m.ts + m.m);
+      g->h_pos.insert(g->h_pos.end(), m.pos, m.pos + m.m);
+      g->h_type.insert(g->h_type.end(), m.type, m.type + m.m);
+      g->h_slot.insert(g->h_slot.end(), m.slot_len, m.slot_len + m.m * S);
+      for (int64_t i = 0; i < m.m; i++) g->h_off.push_back(r0 + m.ref_off[i]);
+      g->h_refs.insert(g->h_refs.end(), m.refs, m.refs + nr);
+    }
+    *out = shp_matches{};
+    out->m = (int64_t)g->h_key.size();
+    out->num_states = S;
+    out->layout = layout;
+    out->key = g->h_key.data();
+    if (layout == SHP_LAYOUT_AGG) {
+      out->agg = g->h_agg.data();
+      return SHP_OK;
+    }
+    out->ts = g->h_ts.data();
+    out->type = g->h_type.data();
+    out->pos = g->h_pos.data();
+    out->ref_off = g->h_off.data();
+    out->slot_len = g->h_slot.data();
+    out->refs = g->h_refs.data();
+    return SHP_OK;
+  });
+}
+
+const char* shp_group_last_error(const shp_group* g) { return g ? g->err.c_str() : "null group"; }
+
+void shp_group_destroy(shp_group* g) {
+  if (!g) return;
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  destroy_impl(g);
+  delete g;
+  if (prev >= 0) (void)hipSetDevice(prev);
+}
+}

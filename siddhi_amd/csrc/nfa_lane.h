@@ -86,10 +86,18 @@ struct BatchView {
   int32_t pad;
   const int64_t* ts;
   const int32_t* stream;
-  const int64_t* rmax;   // clock after event g (running max of ts, seeded with clock0)
+  const int64_t* rmax;   // clock after event g (running max of tclk, seeded with clock0)
   const void* cols[MAXCOL];
   const uint8_t* nulls[MAXCOL];
+  // optional columns (shp_batch.seq / .clock): the events' sequence numbers (NULL: seq0 + g) and
+  // the value each event hands TimestampGenerator.setCurrentTimestamp (= ts when the caller gives
+  // no clock column; a key-sharded rank gets the global playback clock here)
+  const int64_t* seq;
+  const int64_t* tclk;
 };
+
+// sequence number of batch event g
+SHP_HD inline int64_t bseq(const BatchView& B, int64_t g) { return B.seq ? B.seq[g] : B.seq0 + g; }
 
 // Match sink: records are appended with atomics, per-lane order preserved.
 struct MatchOut {
@@ -450,7 +458,7 @@ struct LaneT {
   SHP_HD int node_of_event(int64_t g) {
     int nd = alloc_bit(Y.o_nd_used, NN / 64, E_ND);
     if (nd < 0) return -1;
-    nseq(nd) = B.seq0 + g;
+    nseq(nd) = bseq(B, g);
     nts(nd) = B.ts[g];
     nnext(nd) = -1;
     int st = B.stream[g];
@@ -1316,7 +1324,7 @@ struct LaneT {
   }
 
   SHP_HD int64_t clock_before(int64_t g) const { return g == 0 ? B.clock0 : B.rmax[g - 1]; }
-  SHP_HD bool is_call(int64_t g) const { return !P.playback || B.ts[g] >= clock_before(g); }
+  SHP_HD bool is_call(int64_t g) const { return !P.playback || B.tclk[g] >= clock_before(g); }
 
   // first global event index c in [lo, hi] at which a timer due at `due` fires:
   // playback: a call point whose clock (= ts[c]) >= due; live: first event with ts >= due.
@@ -1374,8 +1382,8 @@ struct LaneT {
           if (c >= 0 && (best < 0 || c < best)) best = c;
         }
         if (best < 0) return;
-        clock = B.ts[best];
-        emit_pos = B.seq0 + best;
+        clock = B.tclk[best];
+        emit_pos = bseq(B, best);
         for (int s = 0; s < P.nsched; s++) {
           int64_t h;
           while (q_head(s, &h) && h <= clock) {
@@ -1401,7 +1409,7 @@ struct LaneT {
         if (c < 0) return;
         int64_t cb = clock_before(c);
         clock = cb > bh ? cb : bh;
-        emit_pos = B.seq0 + c;
+        emit_pos = bseq(B, c);
         // Scheduler.sendTimerEvents for (bs, this key): drain every head <= clock
         int64_t h;
         while (q_head(bs, &h) && h <= clock) {
@@ -1417,7 +1425,7 @@ struct LaneT {
   // One InputHandler.send of batch event g on this key (after its timers).
   SHP_HD void on_event(int64_t g) {
     clock = B.rmax[g];
-    emit_pos = B.seq0 + g;
+    emit_pos = bseq(B, g);
     if (!at<uint8_t>(Y.o_kinit, 0)) init_partition();
     int st = B.stream[g];
     if (st < 0 || st >= P.nstream || P.recvCount[st] == 0) return;

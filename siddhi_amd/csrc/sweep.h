@@ -40,12 +40,24 @@
 
 namespace shp {
 
+#ifndef SWS_THREADS_CFG
+#define SWS_THREADS_CFG 512
+#endif
+#ifndef SWS_CHUNK_CFG
+#define SWS_CHUNK_CFG 1984
+#endif
+#ifndef SWS_CCAP_CFG
+#define SWS_CCAP_CFG 512
+#endif
+#ifndef SWS_OWN_MIN
+#define SWS_OWN_MIN 512
+#endif
 constexpr int SW_THREADS = 256;
 constexpr int SW_WAVES = SW_THREADS / 64;
 constexpr int SW_LK = 255;          // local keys per owner; bin 255 = "no item"
 constexpr int SW_MAXOWN = 2048;     // owners (partition bins)
 constexpr int SW_PREF_OWN = 1024;   // owner count the map stops at unless keys would crowd them
-constexpr int SW_MIN_OWN = 512;     // owner count the map grows to while owners keep ~2 keys (fill the CUs)
+constexpr int SW_MIN_OWN = SWS_OWN_MIN;     // owner count the map grows to while owners keep ~2 keys (fill the CUs)
 constexpr int SW_LKTAB = 65536;     // scatter LDS bound: its counters + the key -> local key table
 // partition
 constexpr int SWP_THREADS = 512;  // scatter workgroup
@@ -54,8 +66,8 @@ constexpr int SWP_ROUND = 4096;  // events ranked per round: 8 per lane
 constexpr int SWP_SEG = SWP_ROUND / SWP_WAVES;
 constexpr int SWP_SUB = SWP_SEG / 64;
 // solve
-constexpr int SWS_CHUNK = 1984;  // records per chunk: with ~<64 carried, E <= 2048 = 4 per thread
-constexpr int SWS_CCAP = 512;  // carried open candidates per owner
+constexpr int SWS_CHUNK = SWS_CHUNK_CFG;  // records per chunk: with ~<64 carried, E <= 2048 = 4 per thread
+constexpr int SWS_CCAP = SWS_CCAP_CFG;  // carried open candidates per owner
 constexpr int SWS_EMAX = SWS_CHUNK + SWS_CCAP;
 constexpr int SWS_SEG = SWS_EMAX / SW_WAVES;
 constexpr int SWS_SUB = SWS_SEG / 64;
@@ -150,7 +162,7 @@ struct SweepDev {
   uint8_t* lastc[2];     // nown * SW_LK: the key's latest event opened a candidate (it is then the
                          // key's last carried candidate, still on the new-and-every list)
   unsigned long long* tsmax;  // max of ts over the push, as ts ^ 2^63 (0: no event); reset per push
-  // SHP_LAYOUT_AGG: selector aggregate over e2's value (1 avg, 2 sum, 3 count; 0 off), its
+  // SHP_LAYOUT_AGG: selector aggregate over e2's value (1 avg, 2 sum, 3 count, 4 min, 5 max; 0 off), its
   // running per-key state (sum, count as doubles: exact integers to 2^53) and the owner-local
   // key -> partition key map for the output rows
   int32_t agg;
@@ -534,7 +546,7 @@ __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchVie
 //            the output offsets, (e1 seq, e2 seq) pairs are written in (key, j, i) order
 //   carry    still-open candidates (key order) become the next chunk's carry
 #define SWM(p) S.m_[8 + (p)]
-constexpr int SWS_THREADS = 512;
+constexpr int SWS_THREADS = SWS_THREADS_CFG;
 constexpr int SWS_WAVES = SWS_THREADS / 64;
 constexpr int SWS_RPT = (SWS_CHUNK + SWS_THREADS - 1) / SWS_THREADS;  // prefetch slots per thread
 constexpr int SWS_PER = (SWS_EMAX + SWS_THREADS - 1) / SWS_THREADS;
@@ -659,6 +671,150 @@ __device__ __forceinline__ void sw_block_segscan(double& s, double& n, bool f, d
   }
   s = ef ? es : as + es;
   n = ef ? en : an + en;
+}
+
+// min / max aggregates (MinAttributeAggregatorExecutor / MaxAttributeAggregatorExecutor,
+// core/query/selector/attribute/aggregator/, non-sliding: no deque): value = first value, then
+// `if (value > x) value = x` (min; `<` for max).  A NaN first value therefore stays, and a NaN
+// later one never replaces.  Fold state: the best non-NaN value (keeps the earlier one on ties),
+// the count, and whether the first value was NaN; combining two folds is associative.
+template <bool MAX>
+__device__ __forceinline__ double sw_mm_best(double a, double b) {  // a folded first
+  if constexpr (MAX) return a < b ? b : a;
+  else return a > b ? b : a;
+}
+template <bool MAX>
+__device__ __forceinline__ double sw_mm_ident() {
+  return MAX ? -INFINITY : INFINITY;
+}
+// exclusive segmented block scan of one (best, count, first-NaN) fold per thread (see
+// sw_block_segscan): out = the fold the thread's first position continues from
+template <bool MAX>
+__device__ __forceinline__ void sw_block_segscan_mm(double& m, double& n, bool& fn, bool f, double* wm, double* wn,
+                                                    uint32_t* wf) {
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  double im = m, in = n;
+  int ifn = fn, inf = f;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double ym = __shfl_up(im, d, 64), yn = __shfl_up(in, d, 64);
+    const int yfn = __shfl_up(ifn, d, 64), yf = __shfl_up(inf, d, 64);
+    if (lane >= (uint32_t)d) {
+      if (!inf) {
+        im = sw_mm_best<MAX>(ym, im);
+        ifn = yn > 0 ? yfn : ifn;
+        in = yn + in;
+      }
+      inf = inf || yf;
+    }
+  }
+  double em = __shfl_up(im, 1, 64), en = __shfl_up(in, 1, 64);
+  int efn = __shfl_up(ifn, 1, 64), ef = __shfl_up(inf, 1, 64);
+  if (lane == 0) {
+    em = sw_mm_ident<MAX>();
+    en = 0;
+    efn = 0;
+    ef = 0;
+  }
+  if (lane == 63) {
+    wm[w] = im;
+    wn[w] = in;
+    wf[w] = (inf ? 1u : 0u) | (ifn ? 2u : 0u);
+  }
+  __syncthreads();
+  double am = sw_mm_ident<MAX>(), an = 0;
+  int afn = 0;
+  for (uint32_t i = 0; i < w; i++) {
+    if (wf[i] & 1u) {
+      am = wm[i];
+      an = wn[i];
+      afn = (wf[i] & 2u) != 0;
+    } else {
+      am = sw_mm_best<MAX>(am, wm[i]);
+      afn = an > 0 ? afn : ((wf[i] & 2u) != 0);
+      an += wn[i];
+    }
+  }
+  if (ef) {
+    m = em;
+    n = en;
+    fn = efn != 0;
+  } else {
+    m = sw_mm_best<MAX>(am, em);
+    fn = (an > 0 ? afn : efn) != 0;
+    n = an + en;
+  }
+}
+
+// SHP_LAYOUT_AGG with min / max: every match a closing event q makes outputs the fold after q's
+// value (adding the same value again does not change a min / max); the key's state (value: NaN
+// when the first value was NaN, count) is seeded from the carry and written at each run end.
+template <bool MAX>
+__device__ __forceinline__ void sw_agg_minmax(SwSolveSmem& S, const SweepDev& D, const MatchOut& O, int E,
+                                              const uint32_t* cq, uint32_t so, bool vflt, int o, int wr) {
+  const uint32_t tid = threadIdx.x;
+  auto seed = [&](uint32_t lk, double& m, double& n, bool& fn) {
+    const double v = S.ainit[lk];
+    n = S.ainit[SW_LK + lk];
+    fn = n > 0 && v != v;
+    m = (n > 0 && !fn) ? v : sw_mm_ident<MAX>();
+  };
+  auto fold = [&](double v, double& m, double& n, bool& fn) {
+    if (n == 0) {
+      fn = v != v;
+      m = fn ? sw_mm_ident<MAX>() : v;
+    } else if (v == v) {
+      m = sw_mm_best<MAX>(m, v);
+    }
+  };
+  double m = sw_mm_ident<MAX>(), n = 0;
+  bool fn = false, tf = false;
+#pragma unroll
+  for (int k = 0; k < SWS_PER; k++) {
+    const int q = (int)tid * SWS_PER + k;
+    if (q < E) {
+      const uint32_t lk = S.lkf[q] & 0xFFu;
+      if ((uint32_t)q == S.binoff[lk]) {
+        seed(lk, m, n, fn);
+        tf = true;
+      }
+      if (cq[k]) {
+        const double v = vflt ? (double)__uint_as_float((uint32_t)S.tv[q].y) : (double)S.tv[q].y;
+        fold(v, m, n, fn);
+        n += (double)cq[k];
+      }
+    }
+  }
+  sw_block_segscan_mm<MAX>(m, n, fn, tf, S.aws, S.awn, S.awf);
+  const unsigned long long gb = S.gbase;
+#pragma unroll
+  for (int k = 0; k < SWS_PER; k++) {
+    const int q = (int)tid * SWS_PER + k;
+    if (q < E) {
+      const uint32_t lk = S.lkf[q] & 0xFFu;
+      if ((uint32_t)q == S.binoff[lk]) seed(lk, m, n, fn);
+      const uint32_t c = cq[k];
+      if (c) {
+        const double v = vflt ? (double)__uint_as_float((uint32_t)S.tv[q].y) : (double)S.tv[q].y;
+        fold(v, m, n, fn);
+        n += (double)c;
+        const double val = fn ? __longlong_as_double(0x7ff8000000000000ll) : m;
+        const int32_t kid = S.ainv[lk];
+        for (uint32_t r = 0; r < c; r++) {
+          const uint64_t slot = gb + so + r;
+          if (slot < (uint64_t)O.cap) {
+            O.key[slot] = kid;
+            O.agg[slot] = val;
+          }
+        }
+      }
+      so += c;
+      if ((uint32_t)q + 1 == S.binoff[lk + 1]) {  // run end: the key's state after this chunk
+        D.agg_s[wr][(int64_t)o * SW_LK + lk] = n == 0 ? 0.0 : (fn ? __longlong_as_double(0x7ff8000000000000ll) : m);
+        D.agg_c[wr][(int64_t)o * SW_LK + lk] = n;
+      }
+    }
+  }
 }
 
 template <int NW>
@@ -1065,7 +1221,14 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
         if (g + ctot > (unsigned long long)O.cap) e |= E_OUT;
         S.gbase = g;
       }
-      if (D.agg) {
+      if (D.agg >= 4) {
+        if (D.agg == 4) sw_agg_minmax<false>(S, D, O, E, cq, pk >> 16, vflt, o, wr);
+        else sw_agg_minmax<true>(S, D, O, E, cq, pk >> 16, vflt, o, wr);
+        for (int k = 0; k < SWS_PER; k++) {
+          const int q = (int)tid * SWS_PER + k;
+          if (q < E && cq[k] && ((S.lkf[q] & SW_LKF_NULL) || vnull)) e |= SWE_AGGNULL;
+        }
+      } else if (D.agg) {
         // SHP_LAYOUT_AGG: the selector's running aggregate per match, in place of the pairs.
         // Per closing event q (c closes, value v): the r-th match adds v once more, so its
         // output is (S + (r+1) v) / (N + r + 1) for avg, where (S, N) is the key's state before
@@ -1148,7 +1311,7 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
             } else {
               S.ckt[nx][pre] = sw_kt(lk, tb + S.tv[p].x, (f & SW_LKF_NULL) ? SW_NULL : 0ull);
               S.cv[nx][pre] = (uint32_t)S.tv[p].y;
-              S.cseq[nx][pre] = B.seq0 + r;
+              S.cseq[nx][pre] = bseq(B, r);
             }
             atomicAdd(&S.ncar[lk], 1u);
           }
@@ -1185,14 +1348,16 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
         for (int d = 0; d < SW_PROBE; d++) later += ((p + 1 + d < q) & (mm[d] == q)) ? 1u : 0u;
         for (int p2 = p + SW_PROBE + 1; p2 < q; p2++) later += SWM(p2) == q ? 1u : 0u;
         const uint32_t r = S.ref[p];
-        const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : B.seq0 + r;
-        const int64_t sq = B.seq0 + S.ref[q];
+        const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : bseq(B, r);
+        const int64_t sq = bseq(B, S.ref[q]);
         const uint64_t slot = gb + off16[q] + (c - 1 - later);
         if (slot < (uint64_t)O.cap) {
           if (D.p32) {
             const int64_t dq = sq - si;  // >= 1
             if (dq >= (1ll << 32)) e |= SWE_P32;
             reinterpret_cast<uint2*>(O.refs)[slot] = make_uint2(S.ref[q], (uint32_t)dq);
+          } else if (B.seq) {  // a seq column: keep e2's batch index for k_sw_expand (FULL layout)
+            *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, (int64_t)S.ref[q]);
           } else {
             *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
           }
@@ -1239,16 +1404,21 @@ __global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchO
   const int64_t m = min((int64_t)*O.count, O.cap);
   if (blockIdx.x == 0 && threadIdx.x == 0) O.count[1] = 2ull * (unsigned long long)m;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t j;
-    if (p32) {
+    int64_t j, g;
+    if (p32) {  // (e2's batch index, e2 seq - e1 seq)
       const uint2 pr = reinterpret_cast<const uint2*>(O.pos)[i];
-      j = B.seq0 + (int64_t)pr.x;
+      g = (int64_t)pr.x;
+      j = bseq(B, g);
       O.refs[2 * i] = j - (int64_t)pr.y;
       O.refs[2 * i + 1] = j;
-    } else {
+    } else if (B.seq) {  // (e1 seq, e2's batch index): the FULL layout with a seq column
+      g = O.refs[2 * i + 1];
+      j = B.seq[g];
+      O.refs[2 * i + 1] = j;
+    } else {  // (e1 seq, e2 seq)
       j = O.refs[2 * i + 1];
+      g = j - B.seq0;
     }
-    int64_t g = j - B.seq0;
     O.key[i] = B.partitioned ? key[g] : 0;
     O.ts[i] = B.ts[g];
     O.type[i] = 0;

@@ -26,7 +26,9 @@ SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
            "shp_dev_to_host", "shp_host_alloc", "shp_host_free", "shp_host_register",
            "shp_host_unregister", "shp_snapshot", "shp_restore", "shp_shard_workspace_bytes",
-           "shp_shard_partition", "shp_shard_unpack", "shp_shard_partition_soa"]
+           "shp_shard_partition", "shp_shard_unpack", "shp_shard_partition_soa", "shp_comm_id",
+           "shp_group_create", "shp_group_create_rank", "shp_group_push", "shp_group_fetch_matches",
+           "shp_group_local_engines", "shp_group_engine", "shp_group_last_error", "shp_group_destroy"]
 
 
 class ShpConfig(ctypes.Structure):
@@ -40,7 +42,8 @@ LAYOUT_FULL, LAYOUT_PAIRS, LAYOUT_AGG, LAYOUT_PAIRS32 = 0, 1, 2, 3
 
 class ShpBatch(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("ts", ctypes.c_void_p), ("key", ctypes.c_void_p),
-                ("stream", ctypes.c_void_p), ("cols", ctypes.c_void_p), ("nulls", ctypes.c_void_p)]
+                ("stream", ctypes.c_void_p), ("cols", ctypes.c_void_p), ("nulls", ctypes.c_void_p),
+                ("clock", ctypes.c_void_p), ("seq", ctypes.c_void_p)]
 
 
 class ShpMatches(ctypes.Structure):
@@ -100,6 +103,19 @@ def lib():
         L.shp_shard_unpack.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 6
         L.shp_shard_partition_soa.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int] + \
             [ctypes.c_void_p] * 7
+        L.shp_comm_id.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.shp_group_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(ShpConfig), ctypes.c_int32, ctypes.c_void_p,
+                                       ctypes.POINTER(ctypes.c_void_p)]
+        L.shp_group_create_rank.argtypes = [ctypes.c_char_p, ctypes.POINTER(ShpConfig), ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+        L.shp_group_push.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.shp_group_fetch_matches.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpMatches)]
+        L.shp_group_local_engines.argtypes = [ctypes.c_void_p]
+        L.shp_group_engine.restype = ctypes.c_void_p
+        L.shp_group_engine.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        L.shp_group_last_error.restype = ctypes.c_char_p
+        L.shp_group_last_error.argtypes = [ctypes.c_void_p]
+        L.shp_group_destroy.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -151,7 +167,8 @@ class HipEngine:
         if rc != 0:
             raise ShpError(rc, lib().shp_last_error(self.h).decode())
 
-    def push(self, ts, key, stream, cols, nulls):
+    def push(self, ts, key, stream, cols, nulls, clock=None, seq=None):
+        """Host arrays; clock / seq: the optional shp_batch columns (global playback clock, sequence numbers)."""
         L = lib()
         n = len(ts)
         out_all = []
@@ -166,8 +183,11 @@ class HipEngine:
             ns = [None if m is None else np.ascontiguousarray(m[lo:hi], np.uint8) for m in nulls]
             colp = (ctypes.c_void_p * max(1, len(cs)))(*[c.ctypes.data for c in cs])
             nulp = (ctypes.c_void_p * max(1, len(ns)))(*[0 if m is None else m.ctypes.data for m in ns])
+            ck = None if clock is None else np.ascontiguousarray(clock[lo:hi], np.int64)
+            sq = None if seq is None else np.ascontiguousarray(seq[lo:hi], np.int64)
             b = ShpBatch(hi - lo, t.ctypes.data, k.ctypes.data, s.ctypes.data,
-                         ctypes.cast(colp, ctypes.c_void_p), ctypes.cast(nulp, ctypes.c_void_p))
+                         ctypes.cast(colp, ctypes.c_void_p), ctypes.cast(nulp, ctypes.c_void_p),
+                         None if ck is None else ck.ctypes.data, None if sq is None else sq.ctypes.data)
             mt = ShpMatches()
             self._check(L.shp_push_batch(self.h, ctypes.byref(b), ctypes.byref(mt)))
             out_all.append(matches_to_numpy(mt))
@@ -218,3 +238,79 @@ def _concat(parts, prev, S, layout=LAYOUT_FULL):
                 "pos": np.zeros(0, np.int64), "slot_len": np.zeros((0, S), np.int32),
                 "refs": np.zeros(0, np.int64)}
     return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_id() -> bytes:
+    """RCCL unique id for a per-process group (rank 0 makes it; broadcast it to the other ranks)."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    rc = lib().shp_comm_id(buf, COMM_ID_BYTES)
+    if rc != 0:
+        raise ShpError(rc, "shp_comm_id failed")
+    return buf.raw
+
+
+class HipGroup:
+    """Key-sharded engines (shp_group_*): in one process over `devices`, or one member per process
+    (rank, comm id).  push() takes one slice per local rank as device tensors (torch) or host arrays."""
+
+    def __init__(self, program_json: str, start_clock: int = 0, max_keys: int = 1 << 16, max_batch: int = 1 << 20,
+                 max_matches: int = 0, devices=None, world: int = 0, rank: int = 0, comm: bytes = None,
+                 device: int = 0, force_general: int = 0, profile_kernels: bool = False,
+                 match_layout: int = LAYOUT_FULL):
+        L = lib()
+        cfg = ShpConfig(device, max_keys, max_batch, max_matches, int(start_clock), int(force_general),
+                        int(profile_kernels), int(match_layout))
+        h = ctypes.c_void_p()
+        if comm is None:
+            devs = list(devices or [0])
+            arr = (ctypes.c_int32 * len(devs))(*devs)
+            rc = L.shp_group_create(program_json.encode(), ctypes.byref(cfg), len(devs), arr, ctypes.byref(h))
+            self.world = len(devs)
+        else:
+            rc = L.shp_group_create_rank(program_json.encode(), ctypes.byref(cfg), world, rank, comm, ctypes.byref(h))
+            self.world = world
+        if rc != 0:
+            raise ShpError(rc, "shp_group_create failed (see stderr)")
+        self.h = h
+        self.nlocal = L.shp_group_local_engines(h)
+        self.layout = int(match_layout)
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ShpError(rc, lib().shp_group_last_error(self.h).decode())
+
+    def push_device(self, slices):
+        """slices: per local rank, (ts, key, stream-or-None, [cols]) torch tensors on that rank's device."""
+        arr = (ShpBatch * self.nlocal)()
+        keep = []
+        for i, (ts, key, stream, cols) in enumerate(slices):
+            colp = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
+            keep.append(colp)
+            arr[i] = ShpBatch(ts.numel(), ts.data_ptr(), key.data_ptr(), None if stream is None else stream.data_ptr(),
+                              ctypes.cast(colp, ctypes.c_void_p), None)
+        counts = (ctypes.c_int64 * self.nlocal)()
+        self._check(lib().shp_group_push(self.h, arr, counts))
+        return list(counts)
+
+    def fetch(self):
+        mt = ShpMatches()
+        self._check(lib().shp_group_fetch_matches(self.h, ctypes.byref(mt)))
+        return matches_to_numpy(mt)
+
+    def engine_ms(self, i, which="total"):
+        e = lib().shp_group_engine(self.h, i)
+        return lib().shp_last_kernel_ms(e, which.encode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().shp_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -356,10 +356,10 @@ class QueryCompiler:
 
     def _device_aggregate(self, sel):
         """The select's aggregate, when the engine can run it (SHP_LAYOUT_AGG): exactly one
-        avg/sum/count whose argument is a filter column of one state; the other items must not
-        aggregate.  Mirrors the selector's aggregator (QuerySelector.java:271-313)."""
+        avg/sum/count/min/max whose argument is a filter column of one state; the other items
+        must not aggregate.  Mirrors the selector's aggregator (QuerySelector.java:271-313)."""
         funcs = [it for it in sel if it["op"] == "func"]
-        if len(funcs) != 1 or funcs[0]["name"] not in ("avg", "sum", "count"):
+        if len(funcs) != 1 or funcs[0]["name"] not in ("avg", "sum", "count", "min", "max"):
             return None
         f = funcs[0]
         if f["name"] == "count":

@@ -75,14 +75,21 @@ class Aggregator:
                 self.value = int(self.value) + (-int(x) if remove else int(x))
             return self.value
         if n in ("max", "min"):
-            if remove:
+            if remove:  # sliding windows only (the deque of Min/MaxAttributeAggregatorExecutor)
                 if x in self.items:
                     self.items.remove(x)
-            else:
-                self.items.append(x)
-            if not self.items:
-                return None
-            return max(self.items) if n == "max" else min(self.items)
+                if not self.items:
+                    self.mm = None
+                else:
+                    self.mm = max(self.items) if n == "max" else min(self.items)
+                return self.mm
+            self.items.append(x)
+            # MinAttributeAggregatorExecutor.processAdd: `if (minValue == null || minValue > value)`
+            # (max: `<`): a NaN first value stays, a later NaN never replaces
+            m = getattr(self, "mm", None)
+            if m is None or (m > x if n == "min" else m < x):
+                self.mm = x
+            return self.mm
         raise ValueError(f"unsupported aggregate {n}")
 
     def current(self):
@@ -92,9 +99,7 @@ class Aggregator:
             return self.count
         if self.name == "sum":
             return self.value
-        if not self.items:
-            return None
-        return max(self.items) if self.name == "max" else min(self.items)
+        return getattr(self, "mm", None)
 
 
 class Selector:

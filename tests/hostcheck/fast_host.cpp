@@ -73,7 +73,7 @@ int fh_push(void* hp, int64_t n, const int64_t* ts, const int32_t* key, const in
   for (int64_t i = 0; i < n; i++) if (kof(i) < (uint32_t)h->nk) kcnt[kof(i)]++;
   for (int k = 1; k <= h->nk; k++) kbeg[k] = kbeg[k - 1] + kcnt[k - 1];
   BatchView B{};
-  B.n = n; B.seq0 = h->seq; B.ts = ts; B.stream = stream; B.partitioned = P.partitioned;
+  B.n = n; B.seq0 = h->seq; B.ts = ts; B.tclk = ts; B.stream = stream; B.partitioned = P.partitioned;
   for (int i = 0; i < P.ncol; i++) { B.cols[i] = cols[i]; B.nulls[i] = nulls ? nulls[i] : nullptr; }
   int err = 0;
   int fstream = h->comp.fast.stream;

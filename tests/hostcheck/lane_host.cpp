@@ -64,7 +64,7 @@ int hc_push(void* hp, int64_t n, const int64_t* ts, const int32_t* key, const in
   for (int k = 1; k <= h->nk; k++) kbeg[k] = kbeg[k - 1] + kcnt[k - 1];
   BatchView B{};
   B.n = n; B.seq0 = h->seq; B.clock0 = h->clock; B.init_clock = h->start; B.partitioned = P.partitioned;
-  B.ts = ts; B.stream = stream; B.rmax = rmax.data();
+  B.ts = ts; B.tclk = ts; B.stream = stream; B.rmax = rmax.data();
   for (int i = 0; i < P.ncol; i++) { B.cols[i] = cols[i]; B.nulls[i] = nulls ? nulls[i] : nullptr; }
   int64_t cap = 1 << 20;
   std::vector<int32_t> mk(cap); std::vector<int64_t> mts(cap), mpos(cap), moff(cap), mrefs(cap * 4);

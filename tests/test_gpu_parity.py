@@ -271,7 +271,9 @@ def _agg_app(fn, typ="float"):
 
 def _expected_agg(oracle_mb, price, fn):
     """Per key, the selector's running aggregate over the oracle's matches in emission order
-    (AvgAttributeAggregatorExecutor: double sum += (double)x, count++, sum / count)."""
+    (AvgAttributeAggregatorExecutor: double sum += (double)x, count++, sum / count;
+    Min/MaxAttributeAggregatorExecutor: value = first x, then `if (value > x) value = x` (min),
+    `<` for max)."""
     out = {}
     state = {}
     S = oracle_mb["slot_len"].shape[1]
@@ -281,15 +283,23 @@ def _expected_agg(oracle_mb, price, fn):
         lens = [int(x) for x in oracle_mb["slot_len"][i]]
         e2 = int(oracle_mb["refs"][off + lens[0]])
         off += sum(lens)
+        x = float(price[e2])
+        if fn in ("min", "max"):
+            m = state.get(k)
+            if m is None or (m > x if fn == "min" else m < x):
+                m = x
+            state[k] = m
+            out.setdefault(k, []).append(m)
+            continue
         s, c = state.get(k, (0.0, 0))
-        s += float(price[e2])
+        s += x
         c += 1
         state[k] = (s, c)
         out.setdefault(k, []).append(s / c if fn == "avg" else (s if fn == "sum" else float(c)))
     return out
 
 
-@pytest.mark.parametrize("fn", ["avg", "sum", "count"])
+@pytest.mark.parametrize("fn", ["avg", "sum", "count", "min", "max"])
 @pytest.mark.parametrize("typ", ["float", "int"])
 def test_device_aggregate_vs_oracle_selector(fn, typ):
     """SHP_LAYOUT_AGG (row 18 / §8f-1): the running per-key avg/sum/count over the matches,
@@ -567,3 +577,37 @@ def test_restore_after_failed_push(general):
     from siddhi_amd.native import _concat
     got = per_key(_concat([head, eng.fetch()], None, eng.S))
     assert compare(ref, got) is None, compare(ref, got)
+
+
+@pytest.mark.parametrize("fn", ["min", "max"])
+def test_device_minmax_java_nan_and_signed_zero(fn):
+    """min / max on the device with NaN (first value of a key and later ones) and -0.0 / 0.0 ties:
+    the reference's `if (value > x) value = x` fold, bit for bit (not IEEE fmin / fmax)."""
+    from siddhi_amd.native import LAYOUT_AGG
+    from siddhi_amd.query.compiler import compile_app
+    app = ("define stream StockStream (symbol string, price float, volume long); "
+           "partition with (symbol of StockStream) begin @info(name='q') "
+           "from every e1=StockStream[price>20] -> e2=StockStream[price != e1.price] within 1 sec "
+           f"select e1.symbol as symbol, {fn}(e2.price) as a insert into Out; end;")  # e2 may be NaN / +-0
+    cq = compile_app(app)[1][0]
+    rng = np.random.default_rng(17)
+    n, keys = 60_000, 300
+    ts = np.cumsum(rng.integers(0, 3, n)).astype(np.int64) + 1_000
+    key = rng.integers(0, keys, n).astype(np.int32)
+    v = rng.choice(np.array([0.0, -0.0, 25.0, 30.5, 99.0, np.nan], np.float32), n, p=[.2, .2, .2, .2, .15, .05])
+    v = v.astype(np.float32)
+    g = {"ts": ts, "key": key, "stream": np.zeros(n, np.int32), "price": v}
+    a = run(OracleEngine(cq.program_json(), 0), cq, g)
+    want = _expected_agg(a, v, fn)
+    eng = hip(3, max_keys=keys, max_batch=1 << 14, match_layout=LAYOUT_AGG)(cq.program_json(), 0)
+    b = run(eng, cq, g, 7_001)
+    got = {}
+    for k, x in zip(b["key"], b["agg"]):
+        got.setdefault(int(k), []).append(float(x))
+    assert set(got) == set(want)
+    for k in want:
+        w, h = np.array(want[k]), np.array(got[k])
+        assert len(w) == len(h), k
+        assert (np.isnan(w) == np.isnan(h)).all(), k
+        ok = ~np.isnan(w)
+        assert (w[ok].view(np.uint64) == h[ok].view(np.uint64)).all(), k  # bitwise: -0.0 != 0.0

@@ -1,0 +1,118 @@
+"""Multi-GPU behind the C-ABI (shp_group_*): the library splits each rank's slice by key owner,
+exchanges it and runs every rank's engine.  On the one-GPU box every rank of
+an in-process group sits on cuda:0 (device-to-device copies stand in for RCCL; the split, the
+counts, the global clock / sequence columns and the per-rank engines are the same code).
+
+Parity: the union of the ranks' matches equals the single-process oracle run per key, bit-exact
+(global key ids and global event sequence numbers).  For absent-state timers (C4) the emission
+position of a timer match is the rank's next event rather than the global one, so `pos` is left
+out of that comparison (include/siddhi_hip.h, group.hip header)."""
+import numpy as np
+import pytest
+
+from diff_util import columns_for, compare, per_key, program_for, run, small_stream
+from oracle.oracle import OracleEngine
+
+pytestmark = pytest.mark.gpu
+
+
+def _slices(g, cols, lo, hi, world, with_stream):
+    import torch
+    out = []
+    for r in range(world):
+        a = lo + r * (hi - lo) // world
+        b = lo + (r + 1) * (hi - lo) // world
+        t = lambda x: torch.from_numpy(np.ascontiguousarray(x[a:b])).to("cuda:0")  # noqa: E731
+        out.append((t(g["ts"]), t(g["key"]), t(g["stream"]) if with_stream else None, [t(c) for c in cols]))
+    return out
+
+
+def _run_group(cq, g, world, keys, pushes, layout, max_batch=1 << 18, **kw):
+    import torch
+    from siddhi_amd.native import HipGroup
+    grp = HipGroup(cq.program_json(), 0, max_keys=keys, max_batch=max_batch, max_matches=max_batch,
+                   devices=[0] * world, match_layout=layout, **kw)
+    cols = columns_for(cq, g)
+    n = len(g["ts"])
+    bounds = np.linspace(0, n, pushes + 1).astype(np.int64)
+    parts = []
+    for p in range(pushes):
+        grp.push_device(_slices(g, cols, bounds[p], bounds[p + 1], world, len(cq.program["streams"]) > 1))
+        parts.append(grp.fetch())
+        torch.cuda.synchronize()
+    grp.close()
+    return parts
+
+
+def _concat(parts):
+    return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+
+
+def _drop_pos(pk):
+    return {k: [(t, ty, sl) for (t, ty, _, sl) in v] for k, v in pk.items()}
+
+
+@pytest.mark.parametrize("world,keys", [(2, 600), (3, 900), (4, 64)])
+def test_group_c2_matches_single_process(world, keys):
+    """C2 through an in-process group (sweep per rank at >= 256 keys per rank, scan kernels below)."""
+    from siddhi_amd.native import LAYOUT_FULL
+    cq = program_for(2)
+    g = small_stream(2, 150_000, keys)
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    got = per_key(_concat(_run_group(cq, g, world, keys, 3, LAYOUT_FULL)))
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(v) for v in want.values()) > 10_000
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_c4_absent_timers_with_global_clock(world):
+    """C4 (logical + absent, playback timers) sharded: every rank gets the global playback clock
+    column, so its timers fire as in one process."""
+    from siddhi_amd.native import LAYOUT_FULL
+    cq = program_for(4)
+    keys = 200
+    g = small_stream(4, 120_000, keys)
+    want = _drop_pos(per_key(run(OracleEngine(cq.program_json(), 0), cq, g)))
+    got = _drop_pos(per_key(_concat(_run_group(cq, g, world, keys, 4, LAYOUT_FULL))))
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(v) for v in want.values()) > 1000
+
+
+def test_group_c3b_count_lanes():
+    from siddhi_amd.native import LAYOUT_FULL
+    cq = program_for("3b")
+    keys = 2000
+    g = small_stream(3, 100_000, keys)
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    got = per_key(_concat(_run_group(cq, g, 2, keys, 2, LAYOUT_FULL)))
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(v) for v in want.values()) > 1000
+
+
+def test_group_c5_device_aggregate():
+    """C5's running avg on the device (SHP_LAYOUT_AGG) per rank: per key the same values as the
+    reference arithmetic over the single-process matches."""
+    from siddhi_amd.native import LAYOUT_AGG
+    from test_gpu_parity import _expected_agg
+    cq = program_for(5)
+    keys = 1200
+    g = small_stream(5, 200_000, keys)
+    want = _expected_agg(run(OracleEngine(cq.program_json(), 0), cq, g), columns_for(cq, g)[0], "avg")
+    parts = _run_group(cq, g, 2, keys, 2, LAYOUT_AGG)
+    got = {}
+    for p in parts:
+        for k, v in zip(p["key"], p["agg"]):
+            got.setdefault(int(k), []).append(float(v))
+    assert set(got) == set(want)
+    for k in want:
+        np.testing.assert_allclose(got[k], want[k], rtol=1e-9, atol=0)
+
+
+def test_group_rank_overflow_is_refused():
+    """A rank that would receive more than max_batch events fails the push before any engine runs."""
+    from siddhi_amd.native import LAYOUT_FULL, ShpError
+    cq = program_for(2)
+    g = small_stream(2, 40_000, 600)
+    g["key"] = (g["key"] // 2) * 2  # every key even: all events to rank 0
+    with pytest.raises(ShpError, match="SHP_ERR_CAPACITY"):
+        _run_group(cq, g, 2, 600, 1, LAYOUT_FULL, max_batch=30_000)
