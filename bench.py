@@ -6,10 +6,11 @@ e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec ... end`
 100M synthetic events per GPU per step (PCG32 stream, generated in HBM before the timed region).
 A step = one shp_push_batch_device of the next 100M events of the stream through the engine
 (partition by key + NFA + match compaction into HBM), per-key state carried across steps.
-N>1: one process per GPU; each rank ingests its slice of the global stream and the events are
-redistributed by key owner (key % N): a HIP stable split into destination-grouped SoA columns,
-then one RCCL all-to-all per column (torch.distributed nccl) whose receive buffers are the owner's
-engine input as they stand, so per-GPU work is fixed (weak scaling).
+N>1: one process per GPU; each rank ingests its slice of the global stream and the library's
+key-sharded group (shp_group_*, multi-GPU behind the C-ABI) redistributes the events by key owner
+(key % N): a HIP stable split into destination-grouped columns, then RCCL ncclSend/ncclRecv over
+xGMI from the engine's own communicator; per-GPU work is fixed (weak scaling).  torch.distributed
+(gloo) is the control plane only: barriers, the RCCL id broadcast, max-over-ranks timing.
 
 Prints ONE JSON line (rank 0) with roofline (dominant kernel, HIP events on the engine stream)
 and cpu_baseline (the oracle, single-threaded, on a bounded sample of the same stream).
@@ -66,7 +67,8 @@ def parse():
     ap.add_argument("--path", choices=["auto", "general", "scan"], default="auto",
                     help="auto = sweep path (default); scan = round-1 scan kernels; general = NFA lanes")
     ap.add_argument("--same-device", action="store_true",
-                    help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, collectives over gloo")
+                    help="N>1 rehearsal on a one-GPU box without torchrun: one process, an in-process group of "
+                         "--gpus ranks all on cuda:0 (device copies stand in for RCCL)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
     ap.add_argument("--latency-batches", type=int, default=200,
                     help="§8d latency: batches of --latency-events, push + D2H of the match payload (0: skip)")
@@ -83,20 +85,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.same_device:  # rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0
-        local = 0
+    G = a.gpus if a.same_device else world
+    if a.same_device:  # rehearsal of the N>1 path on a one-GPU box: an in-process group, every rank on cuda:0
+        local, world, rank = 0, 1, 0
     torch.cuda.set_device(local)
     dist = None
-    backend = "gloo" if a.same_device else "nccl"  # nccl = RCCL over xGMI on ROCm
-    coll_dev = "cpu" if backend == "gloo" else "cuda"
     if world > 1:
+        # control plane only (barriers, the RCCL id broadcast, max-over-ranks timing): the data-path
+        # exchange is the engine's own RCCL communicator inside libsiddhi_hip.so (shp_group_*)
         import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("gloo")
 
-    from siddhi_amd import native, shard, synth
+    from siddhi_amd import native, synth
     from siddhi_amd.query.compiler import compile_app
 
     cfg_id = int(a.config) if a.config.isdigit() else a.config
@@ -104,23 +104,42 @@ def main():
     _, qs, _ = compile_app(synth.QUERIES[cfg_id])
     cq = qs[0]
     assert all(c[1] == 1 and c[2] == "float" for c in cq.columns), "bench configs read price only"
-    N, G = a.events, world
+    N = a.events
     K = a.keys if a.keys else spec.keys
     K_local = -(-K // G)  # each rank's engine holds a dense dictionary of the keys it owns
     cap = int(N * 1.08) + 4096 if G > 1 else N
     force = {"auto": 0, "general": 1, "scan": 2}[a.path]
     sweep = force == 0 and _sweep_shape(cq, local, K_local)
     layout = ("agg" if "aggregate" in cq.program else a.pairs_layout) if sweep else "full"
-    eng = native.HipEngine(cq.program_json(), 0, max_keys=K_local, max_batch=cap, max_matches=cap,
-                           device=local, force_general=force, profile_kernels=True,
-                           match_layout={"agg": native.LAYOUT_AGG, "pairs": native.LAYOUT_PAIRS,
-                                         "pairs32": native.LAYOUT_PAIRS32, "full": native.LAYOUT_FULL}[layout])
+    mlay = {"agg": native.LAYOUT_AGG, "pairs": native.LAYOUT_PAIRS, "pairs32": native.LAYOUT_PAIRS32,
+            "full": native.LAYOUT_FULL}[layout]
     L = native.lib()
+    grp = None
+    if G == 1:
+        eng = native.HipEngine(cq.program_json(), 0, max_keys=K_local, max_batch=cap, max_matches=cap,
+                               device=local, force_general=force, profile_kernels=True, match_layout=mlay)
+        engines = [eng]
+    else:
+        if a.same_device:
+            grp = native.HipGroup(cq.program_json(), 0, max_keys=K, max_batch=cap, max_matches=cap,
+                                  devices=[0] * G, force_general=force, profile_kernels=True, match_layout=mlay)
+        else:
+            cid = torch.zeros(native.COMM_ID_BYTES, dtype=torch.uint8)
+            if rank == 0:
+                cid = torch.frombuffer(bytearray(native.comm_id()), dtype=torch.uint8)
+            dist.broadcast(cid, 0)
+            grp = native.HipGroup(cq.program_json(), 0, max_keys=K, max_batch=cap, max_matches=cap, world=G,
+                                  rank=rank, comm=bytes(cid.numpy().tobytes()), device=local, force_general=force,
+                                  profile_kernels=True, match_layout=mlay)
+        engines = [_EngineView(grp, i) for i in range(grp.nlocal)]
+    eng = engines[0]
     steps = a.warmup + a.steps
+    my_ranks = list(range(G)) if a.same_device else [rank]
 
-    # synthetic input for every step, resident in HBM before timing
-    def gen(step):
-        start = (step * G + rank) * N
+    # synthetic input for every step, resident in HBM before timing: step s of the global stream is
+    # G consecutive slices of N events, slice r ingested by rank r
+    def gen(step, r):
+        start = (step * G + r) * N
         ts = torch.empty(N, dtype=torch.int64, device="cuda")
         key = torch.empty(N, dtype=torch.int32, device="cuda")
         price = torch.empty(N, dtype=torch.float32, device="cuda")
@@ -131,18 +150,14 @@ def main():
         assert rc == 0
         return ts, key, price, stream
 
-    # N>1: two batches beyond the timed ones, so every timed step also exchanges a later batch
-    batches = [gen(s) for s in range(steps + (2 if G > 1 else 0))]
+    batches = [[gen(s, r) for r in my_ranks] for s in range(steps)]
     torch.cuda.synchronize()
-    xch = shard.DeviceExchange(N, G, dist, torch.device("cuda", local), spec.n_streams > 1,
-                               cpu_collectives=backend == "gloo") if G > 1 else None
-    ready, pending = {}, {}
+    ncol = max(1, len(cq.columns))
 
     def push(ts, key, price, stream):
         n = ts.numel()
         # one pointer per program column (cq.columns: (stream, attr, type)); every stream's
         # predicate attribute is the synthetic price column
-        ncol = max(1, len(cq.columns))
         colp = (ctypes.c_void_p * ncol)(*([price.data_ptr()] * ncol))
         b = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), stream.data_ptr() if stream is not None else None,
                             ctypes.cast(colp, ctypes.c_void_p), None)
@@ -152,45 +167,40 @@ def main():
             raise native.ShpError(rc, L.shp_last_error(eng.h).decode())
         return n, mt.m
 
-    def exchange_ahead(i):
-        """Main thread, while batch i is in the engine: land batch i+1 (its all-to-alls were
-        started one step earlier) and start batch i+2's split + all-to-alls."""
-        if i + 1 in pending:
-            ready[i + 1] = xch.finish(pending.pop(i + 1))
-            torch.cuda.current_stream().synchronize()  # the engine runs on its own HIP stream
-        if i + 2 < len(batches):
-            pending[i + 2] = xch.start(*batches[i + 2])
+    def slices(i):
+        return [(ts, key, stream, [price] * ncol) for (ts, key, price, stream) in batches[i]]
 
-    if G > 1:  # fill the pipeline (untimed)
-        ready[0] = xch(*batches[0])
-        torch.cuda.current_stream().synchronize()
-        pending[1] = xch.start(*batches[1])
+    staged = []
 
     def step(i):
-        """One batch through the hot path.  N>1: the engine runs batch i (already exchanged by key
-        owner) on a worker thread -- the blocking C call releases the GIL -- while this thread
-        lands batch i+1 and starts the HIP split and RCCL all-to-alls of batch i+2, so the
-        exchange overlaps the engine instead of adding to it."""
+        """One batch through the hot path.  N>1: shp_group_run runs batch i (split, exchanged by key
+        owner and landed in a receive slot earlier) on a worker thread -- the blocking C call
+        releases the GIL -- while this thread stages batch i + 2 (HIP split + RCCL exchange inside
+        the library), so the exchange overlaps the engines instead of adding to them."""
         if G == 1:
-            return push(*batches[i])
+            return push(*batches[i][0])
         out = {}
 
         def work():
             try:
-                out["r"] = push(*ready.pop(i))
+                out["r"] = grp.run()
             except BaseException as ex:  # re-raised on the main thread
                 out["e"] = ex
 
         th = threading.Thread(target=work)
         th.start()
         try:
-            exchange_ahead(i)
+            if i + 2 < steps:
+                staged.append(grp.stage_device(slices(i + 2)))
         finally:
             th.join()
         if "e" in out:
             raise out["e"]
-        return out["r"]
+        return N * len(my_ranks), sum(out["r"])
 
+    if G > 1:  # fill the pipeline (untimed)
+        for i in range(min(2, steps)):
+            staged.append(grp.stage_device(slices(i)))
     for i in range(a.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -213,14 +223,11 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    for p in list(pending.values()):  # drain the exchange started past the last step (untimed)
-        xch.finish(p)
-    pending.clear()
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        cnt = torch.tensor([ev_local, m_local], dtype=torch.int64, device=coll_dev)
+        cnt = torch.tensor([ev_local, m_local], dtype=torch.int64)
         dist.all_reduce(cnt)
         ev_total, m_total = int(cnt[0]), int(cnt[1])
     else:
@@ -235,8 +242,9 @@ def main():
         value = ev_total / elapsed
         dom = max(kernel_ms, key=lambda k: kernel_ms[k])
         dom_ms = kernel_ms[dom] / a.steps
-        ev_per_launch = ev_local / a.steps
-        m_per_launch = m_local / a.steps
+        # per launch of the dominant kernel on rank 0's (first local) engine: the events it received
+        ev_per_launch = ev_total / G / a.steps
+        m_per_launch = m_total / G / a.steps
         alg_bytes = BYTES_PER_EVENT * ev_per_launch + BYTES_PER_MATCH[layout] * m_per_launch
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
         traffic = None
@@ -244,7 +252,7 @@ def main():
             try:
                 pm = json.load(open(a.pmc))
                 # PMC passes are of one bench command (tools/pmc_run.sh): its config only
-                if str(pm.get("config", "2")) == str(cfg_id) and int(pm.get("keys", K)) == K:
+                if str(pm.get("config", "2")) == str(cfg_id) and int(pm.get("keys", K)) == K and G == 1:
                     traffic = pm.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -253,6 +261,12 @@ def main():
             cpu = cpu_baseline(cq, a.cpu_sample, K, spec.config, a.cpu_threads)
         step_ms = elapsed / a.steps * 1e3
         step_achieved = alg_bytes / (step_ms * 1e-3) / 1e9
+        par = f"key-sharded x{G}"
+        if G > 1:
+            par += (" (shp_group: HIP split by key owner + " +
+                    ("device copies, every rank on cuda:0 (rehearsal)" if a.same_device else
+                     "RCCL ncclSend/ncclRecv over xGMI") +
+                    " inside libsiddhi_hip.so, batch i+2 exchanged while the engines run batch i)")
         line = {
             "metric": "input events/sec, keyed pattern query, 1/2/4/8 MI355X; p99 batch latency",
             "value": value,
@@ -260,7 +274,7 @@ def main():
             "n_gpus": G,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
+            "ms_per_step": step_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -270,8 +284,7 @@ def main():
                 "workload": WORKLOADS.get(str(cfg_id), f"C{cfg_id}") + f"; {K} keys",
                 "events_per_gpu_per_step": N,
                 "keys": K,
-                "parallelism": f"key-sharded x{G}" + (" (RCCL all-to-all of the batch's SoA columns by key "
-                                                      "owner, overlapped with the previous batch)" if G > 1 else ""),
+                "parallelism": par,
                 "engine_path": PATHS.get(eng.path, str(eng.path)),
                 "matches_per_s": m_total / elapsed,
                 "matches_per_step_gpu0": m_per_launch,
@@ -299,8 +312,27 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if grp is not None:
+        grp.close()
     if dist:
         dist.destroy_process_group()
+
+
+class _EngineView:
+    """A group member's engine, for the per-kernel timings and the path (shp_group_engine)."""
+
+    def __init__(self, grp, i):
+        from siddhi_amd import native
+        self.h = ctypes.c_void_p(native.lib().shp_group_engine(grp.h, i))
+
+    @property
+    def path(self):
+        from siddhi_amd import native
+        return native.lib().shp_engine_path(self.h)
+
+    def kernel_ms(self, which="total"):
+        from siddhi_amd import native
+        return native.lib().shp_last_kernel_ms(self.h, which.encode())
 
 
 def batch_latency(eng, L, native, spec, K, layout, n, batches, start):

@@ -163,6 +163,13 @@ int shp_group_create_rank(const char* nfa_program_json, const shp_config* cfg, i
  * (in-process group: world of them; per-rank member: its own).  matches (may be NULL): per local
  * rank, the matches of this push (they stay in HBM until shp_group_fetch_matches). */
 int shp_group_push(shp_group* g, const shp_batch* slices, int64_t* matches);
+/* shp_group_push in two halves, so the exchange of later batches overlaps the engines' run of
+ * this one: stage = split + exchange into one of three receive slots (returns once the exchange
+ * is enqueued; the slices must stay valid until that batch's run returns); run = the engines on
+ * the oldest staged batch.  At most three batches staged ahead; one thread may stage while
+ * another runs (and nothing else calls into the group meanwhile). */
+int shp_group_stage(shp_group* g, const shp_batch* slices);
+int shp_group_run(shp_group* g, int64_t* matches);
 /* The local ranks' matches of the last push in host memory, global key ids, per-key emission order. */
 int shp_group_fetch_matches(shp_group* g, shp_matches* out);
 int shp_group_local_engines(const shp_group* g);

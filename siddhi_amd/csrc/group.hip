@@ -30,6 +30,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -234,16 +235,24 @@ struct shp_group {
     hipEvent_t split_done = nullptr;
     // split workspace
     DevBuf cnt, off, tot, tsmax, rmax, scan_tmp;
-    // send (destination-grouped) and receive columns: ts, key, stream, clock, seq, predicate columns
-    DevBuf s_ts, s_key, s_stream, s_clk, s_seq, r_ts, r_key, r_stream, r_clk, r_seq;
-    DevBuf s_col[shp::MAXCOL], r_col[shp::MAXCOL];
+    // send (destination-grouped) columns: ts, key, stream, clock, seq, predicate columns
+    DevBuf s_ts, s_key, s_stream, s_clk, s_seq;
+    DevBuf s_col[shp::MAXCOL];
     int64_t n_slice = 0;
     int64_t max_ts = INT64_MIN;
     std::vector<int64_t> send_cnt;  // per destination
-    std::vector<int64_t> recv_cnt;  // per source
-    int64_t n_recv = 0;
+    // three receive slots: batch i + 2 can be exchanged while the engines run batch i
+    struct Slot {
+      DevBuf r_ts, r_key, r_stream, r_clk, r_seq;
+      DevBuf r_col[shp::MAXCOL];
+      std::vector<int64_t> recv_cnt;  // per source
+      int64_t n_recv = 0;
+      int64_t push_clock = INT64_MIN, next_seq = 0;
+      hipEvent_t done = nullptr;      // the exchange into this slot has landed
+    } slot[3];
     int64_t last_m = 0;
   };
+  std::atomic<int64_t> staged{0}, ran{0};  // batches exchanged / run (at most three staged ahead)
   std::vector<Local> L;
   int64_t seq = 0;              // global sequence number of the next push's first event
   int64_t clock = INT64_MIN;    // global playback clock
@@ -353,18 +362,19 @@ void split_scatter(shp_group& g, shp_group::Local& l, const shp_batch& b, int64_
   GH(hipEventRecord(l.split_done, l.s));
 }
 
-void ensure_recv(shp_group& g, shp_group::Local& l, int64_t n) {
+void ensure_recv(shp_group& g, shp_group::Local::Slot& r, int64_t n) {
   const size_t cap = (size_t)n + 1;  // + the end-of-push clock event
-  l.r_ts.ensure(cap * 8);
-  l.r_key.ensure(cap * 4);
-  l.r_stream.ensure(cap * 4);
-  if (g.need_clock) l.r_clk.ensure(cap * 8);
-  if (g.need_seq) l.r_seq.ensure(cap * 8);
-  for (int c = 0; c < g.ncol; c++) l.r_col[c].ensure(cap * col_bytes(g.ctag[c]));
+  r.r_ts.ensure(cap * 8);
+  r.r_key.ensure(cap * 4);
+  r.r_stream.ensure(cap * 4);
+  if (g.need_clock) r.r_clk.ensure(cap * 8);
+  if (g.need_seq) r.r_seq.ensure(cap * 8);
+  for (int c = 0; c < g.ncol; c++) r.r_col[c].ensure(cap * col_bytes(g.ctag[c]));
 }
 
 // the columns exchanged, as (send buffer, receive buffer, bytes per event)
-std::vector<std::tuple<void*, void*, int>> column_pairs(shp_group& g, shp_group::Local& src, shp_group::Local& dst) {
+std::vector<std::tuple<void*, void*, int>> column_pairs(shp_group& g, shp_group::Local& src,
+                                                        shp_group::Local::Slot& dst) {
   std::vector<std::tuple<void*, void*, int>> v = {{src.s_ts.p, dst.r_ts.p, 8}, {src.s_key.p, dst.r_key.p, 4}};
   if (g.has_stream_col) v.emplace_back(src.s_stream.p, dst.r_stream.p, 4);
   if (g.need_clock) v.emplace_back(src.s_clk.p, dst.r_clk.p, 8);
@@ -373,28 +383,25 @@ std::vector<std::tuple<void*, void*, int>> column_pairs(shp_group& g, shp_group:
   return v;
 }
 
-// step 4: one engine push of what a rank received, plus the end-of-push clock event
-int run_local(shp_group& g, shp_group::Local& l, int64_t push_clock, int64_t next_seq) {
+// step 4: one engine push of what a rank received (slot r), plus the end-of-push clock event
+int run_local(shp_group& g, shp_group::Local& l, shp_group::Local::Slot& r) {
   GH(hipSetDevice(l.dev));
-  const int64_t m = l.n_recv;
+  GH(hipEventSynchronize(r.done));
+  const int64_t push_clock = r.push_clock, next_seq = r.next_seq;
+  const int64_t m = r.n_recv;
   const bool tail = g.need_clock && push_clock != INT64_MIN;
-  if (!g.has_stream_col) GH(hipMemsetAsync(l.r_stream.p, 0, (size_t)m * 4, l.s));
-  if (tail)
-    k_gs_fill_tail<<<1, 1, 0, l.s>>>((int64_t*)l.r_ts.p, (int32_t*)l.r_key.p, (int32_t*)l.r_stream.p,
-                                     g.need_clock ? (int64_t*)l.r_clk.p : nullptr,
-                                     g.need_seq ? (int64_t*)l.r_seq.p : nullptr, m, push_clock, next_seq);
-  GH(hipStreamSynchronize(l.s));
   std::vector<const void*> colp(std::max(1, g.ncol));
-  for (int c = 0; c < g.ncol; c++) colp[c] = l.r_col[c].p;
+  for (int c = 0; c < g.ncol; c++) colp[c] = r.r_col[c].p;
   shp_batch b{};
   b.n = m + (tail ? 1 : 0);
-  b.ts = (const int64_t*)l.r_ts.p;
-  b.key = (const int32_t*)l.r_key.p;
-  b.stream = (const int32_t*)l.r_stream.p;
+  b.ts = (const int64_t*)r.r_ts.p;
+  b.key = (const int32_t*)r.r_key.p;
+  b.stream = (const int32_t*)r.r_stream.p;
   b.cols = colp.data();
   b.nulls = nullptr;
-  b.clock = g.need_clock ? (const int64_t*)l.r_clk.p : nullptr;
-  b.seq = g.need_seq ? (const int64_t*)l.r_seq.p : nullptr;
+  b.clock = g.need_clock ? (const int64_t*)r.r_clk.p : nullptr;
+  b.seq = g.need_seq ? (const int64_t*)r.r_seq.p : nullptr;
+  (void)next_seq;
   if (b.n == 0) {
     l.last_m = 0;
     return SHP_OK;
@@ -409,8 +416,18 @@ int run_local(shp_group& g, shp_group::Local& l, int64_t push_clock, int64_t nex
   return SHP_OK;
 }
 
-int push_impl(shp_group& g, const shp_batch* slices, int64_t* counts) {
+// steps 1-3 for one batch into the next receive slot (asynchronous once the counts are known)
+int stage_impl(shp_group& g, const shp_batch* slices) {
   const int G = g.world;
+  if (g.staged - g.ran >= 3) return g.fail(SHP_ERR_ARG, "three batches are staged already (run one first)");
+  const int sl = (int)(g.staged % 3);
+  if (!g.rccl && g.staged > 0) {  // the previous batch's copies read the send columns this split rewrites
+    const int prev = (int)((g.staged - 1) % 3);
+    for (auto& a : g.L) {
+      GH(hipSetDevice(a.dev));
+      for (auto& b : g.L) GH(hipStreamWaitEvent(a.s, b.slot[prev].done, 0));
+    }
+  }
   // 1a + 2: counts, slice lengths, largest ts of every rank
   for (int i = 0; i < g.nlocal; i++) split_count(g, g.L[i], slices[i]);
   std::vector<int64_t> all((size_t)G * (G + 2));  // per rank: counts[G], n, maxts
@@ -440,27 +457,29 @@ int push_impl(shp_group& g, const shp_batch* slices, int64_t* counts) {
     base[r + 1] = base[r] + all[(size_t)r * (G + 2) + G];
     seed[r + 1] = std::max(seed[r], all[(size_t)r * (G + 2) + G + 1]);
   }
-  const int64_t push_clock = seed[G];
   for (int i = 0; i < g.nlocal; i++) {
-    shp_group::Local& l = g.L[i];
-    l.recv_cnt.assign(G, 0);
-    l.n_recv = 0;
+    shp_group::Local::Slot& r = g.L[i].slot[sl];
+    r.recv_cnt.assign(G, 0);
+    r.n_recv = 0;
     for (int s = 0; s < G; s++) {
-      l.recv_cnt[s] = cnt(s, l.rank);
-      l.n_recv += l.recv_cnt[s];
+      r.recv_cnt[s] = cnt(s, g.L[i].rank);
+      r.n_recv += r.recv_cnt[s];
     }
-    if (l.n_recv + 1 > g.cfg.max_batch)
-      return g.fail(SHP_ERR_CAPACITY, "rank " + std::to_string(l.rank) + " would receive " +
-                                          std::to_string(l.n_recv) + " events (> max_batch)");
+    if (r.n_recv + 1 > g.cfg.max_batch)
+      return g.fail(SHP_ERR_CAPACITY, "rank " + std::to_string(g.L[i].rank) + " would receive " +
+                                          std::to_string(r.n_recv) + " events (> max_batch)");
+    r.push_clock = seed[G];
+    r.next_seq = base[G];
   }
   // 1b: scatter
   for (int i = 0; i < g.nlocal; i++) split_scatter(g, g.L[i], slices[i], seed[g.L[i].rank], base[g.L[i].rank]);
-  for (int i = 0; i < g.nlocal; i++) ensure_recv(g, g.L[i], g.L[i].n_recv);
+  for (int i = 0; i < g.nlocal; i++) ensure_recv(g, g.L[i].slot[sl], g.L[i].slot[sl].n_recv);
   // 3: exchange
   if (g.rccl) {
     shp_group::Local& l = g.L[0];
+    shp_group::Local::Slot& r = l.slot[sl];
     GH(hipSetDevice(l.dev));
-    auto cols = column_pairs(g, l, l);
+    auto cols = column_pairs(g, l, r);
     GN(ncclGroupStart());
     for (auto& c : cols) {
       void* sb = std::get<0>(c);
@@ -468,7 +487,7 @@ int push_impl(shp_group& g, const shp_batch* slices, int64_t* counts) {
       const int sz = std::get<2>(c);
       int64_t so = 0, ro = 0;
       for (int p = 0; p < G; p++) {
-        const int64_t sn = l.send_cnt[p], rn = l.recv_cnt[p];
+        const int64_t sn = l.send_cnt[p], rn = r.recv_cnt[p];
         if (sn) GN(ncclSend((char*)sb + so * sz, (size_t)sn * sz, ncclChar, p, g.comm, l.s));
         if (rn) GN(ncclRecv((char*)rb + ro * sz, (size_t)rn * sz, ncclChar, p, g.comm, l.s));
         so += sn;
@@ -479,6 +498,7 @@ int push_impl(shp_group& g, const shp_batch* slices, int64_t* counts) {
   } else {
     for (int di = 0; di < g.nlocal; di++) {
       shp_group::Local& dst = g.L[di];
+      shp_group::Local::Slot& r = dst.slot[sl];
       GH(hipSetDevice(dst.dev));
       int64_t ro = 0;
       for (int si = 0; si < g.nlocal; si++) {
@@ -488,7 +508,7 @@ int push_impl(shp_group& g, const shp_batch* slices, int64_t* counts) {
         for (int d = 0; d < dst.rank; d++) so += src.send_cnt[d];
         const int64_t k = src.send_cnt[dst.rank];
         if (k)
-          for (auto& c : column_pairs(g, src, dst)) {
+          for (auto& c : column_pairs(g, src, r)) {
             const int sz = std::get<2>(c);
             GH(hipMemcpyPeerAsync((char*)std::get<1>(c) + ro * sz, dst.dev, (char*)std::get<0>(c) + so * sz, src.dev,
                                   (size_t)k * sz, dst.s));
@@ -497,31 +517,53 @@ int push_impl(shp_group& g, const shp_batch* slices, int64_t* counts) {
       }
     }
   }
-  // 4: every local engine runs what it received (one host thread per engine: GPUs overlap)
-  const int64_t next_seq = base[G];
+  // the received batch's stream column (when the query reads one stream) and its end-of-push
+  // clock event, then the slot is ready
+  for (int i = 0; i < g.nlocal; i++) {
+    shp_group::Local& l = g.L[i];
+    shp_group::Local::Slot& r = l.slot[sl];
+    GH(hipSetDevice(l.dev));
+    if (!g.has_stream_col) GH(hipMemsetAsync(r.r_stream.p, 0, (size_t)r.n_recv * 4, l.s));
+    if (g.need_clock && r.push_clock != INT64_MIN)
+      k_gs_fill_tail<<<1, 1, 0, l.s>>>((int64_t*)r.r_ts.p, (int32_t*)r.r_key.p, (int32_t*)r.r_stream.p,
+                                       (int64_t*)r.r_clk.p, g.need_seq ? (int64_t*)r.r_seq.p : nullptr, r.n_recv,
+                                       r.push_clock, r.next_seq);
+    GH(hipGetLastError());
+    GH(hipEventRecord(r.done, l.s));
+  }
+  g.seq = base[G];
+  if (seed[G] != INT64_MIN) g.clock = std::max(g.clock, seed[G]);
+  g.staged++;
+  return SHP_OK;
+}
+
+// step 4 for the oldest staged batch: every local engine runs what it received (one host thread
+// per engine, so the GPUs of an in-process group overlap)
+int run_impl(shp_group& g, int64_t* counts) {
+  if (g.ran == g.staged) return g.fail(SHP_ERR_ARG, "no staged batch to run");
+  const int sl = (int)(g.ran % 3);
   std::vector<int> rcs(g.nlocal, SHP_OK);
   std::vector<std::string> errs(g.nlocal);
+  auto one = [&](int i) {
+    try {
+      rcs[i] = run_local(g, g.L[i], g.L[i].slot[sl]);
+    } catch (std::exception& ex) {
+      errs[i] = ex.what();
+      rcs[i] = SHP_ERR_DEVICE;
+    }
+  };
   if (g.nlocal == 1) {
-    rcs[0] = run_local(g, g.L[0], push_clock, next_seq);
+    one(0);
   } else {
     std::vector<std::thread> th;
-    for (int i = 0; i < g.nlocal; i++)
-      th.emplace_back([&, i]() {
-        try {
-          rcs[i] = run_local(g, g.L[i], push_clock, next_seq);
-        } catch (std::exception& ex) {
-          errs[i] = ex.what();
-          rcs[i] = SHP_ERR_DEVICE;
-        }
-      });
+    for (int i = 0; i < g.nlocal; i++) th.emplace_back(one, i);
     for (auto& t : th) t.join();
   }
+  g.ran++;
   for (int i = 0; i < g.nlocal; i++) {
     if (!errs[i].empty()) return g.fail(rcs[i], errs[i]);
     if (rcs[i] != SHP_OK) return rcs[i];
   }
-  g.seq = next_seq;
-  if (push_clock != INT64_MIN) g.clock = std::max(g.clock, push_clock);
   if (counts)
     for (int i = 0; i < g.nlocal; i++) counts[i] = g.L[i].last_m;
   return SHP_OK;
@@ -554,10 +596,11 @@ int create_impl(shp_group* g, const char* json, const shp_config* cfg, int world
     GH(hipSetDevice(l.dev));
     GH(hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking));
     GH(hipEventCreateWithFlags(&l.split_done, hipEventDisableTiming));
+    for (auto& r : l.slot) GH(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
     const int rc = shp_engine_create(json, &ec, &l.eng);
     if (rc != SHP_OK) return g->fail(rc, "engine creation failed on rank " + std::to_string(l.rank));
   }
-  if (comm_id && world > 1) {
+  if (comm_id) {  // (world 1 too: a one-rank communicator runs the same RCCL calls, sends to itself)
     g->rccl = true;
     ncclUniqueId id;
     std::memcpy(&id, comm_id, sizeof id);
@@ -573,6 +616,8 @@ void destroy_impl(shp_group* g) {
     (void)hipSetDevice(l.dev);
     if (l.eng) shp_engine_destroy(l.eng);
     if (l.split_done) (void)hipEventDestroy(l.split_done);
+    for (auto& r : l.slot)
+      if (r.done) (void)hipEventDestroy(r.done);
     if (l.s) (void)hipStreamDestroy(l.s);
   }
 }
@@ -641,7 +686,21 @@ int shp_group_create_rank(const char* json, const shp_config* cfg, int32_t world
 
 int shp_group_push(shp_group* g, const shp_batch* slices, int64_t* matches) {
   if (!g || !slices) return SHP_ERR_ARG;
-  return guarded(g, [&]() { return push_impl(*g, slices, matches); });
+  return guarded(g, [&]() {
+    if (g->staged != g->ran) return g->fail(SHP_ERR_ARG, "staged batches pending (shp_group_run them first)");
+    const int rc = stage_impl(*g, slices);
+    return rc != SHP_OK ? rc : run_impl(*g, matches);
+  });
+}
+
+int shp_group_stage(shp_group* g, const shp_batch* slices) {
+  if (!g || !slices) return SHP_ERR_ARG;
+  return guarded(g, [&]() { return stage_impl(*g, slices); });
+}
+
+int shp_group_run(shp_group* g, int64_t* matches) {
+  if (!g) return SHP_ERR_ARG;
+  return guarded(g, [&]() { return run_impl(*g, matches); });
 }
 
 int shp_group_local_engines(const shp_group* g) { return g ? g->nlocal : 0; }

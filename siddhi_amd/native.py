@@ -27,7 +27,8 @@ SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_
            "shp_dev_to_host", "shp_host_alloc", "shp_host_free", "shp_host_register",
            "shp_host_unregister", "shp_snapshot", "shp_restore", "shp_shard_workspace_bytes",
            "shp_shard_partition", "shp_shard_unpack", "shp_shard_partition_soa", "shp_comm_id",
-           "shp_group_create", "shp_group_create_rank", "shp_group_push", "shp_group_fetch_matches",
+           "shp_group_create", "shp_group_create_rank", "shp_group_push", "shp_group_stage", "shp_group_run",
+           "shp_group_fetch_matches",
            "shp_group_local_engines", "shp_group_engine", "shp_group_last_error", "shp_group_destroy"]
 
 
@@ -109,6 +110,8 @@ def lib():
         L.shp_group_create_rank.argtypes = [ctypes.c_char_p, ctypes.POINTER(ShpConfig), ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
         L.shp_group_push.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.shp_group_stage.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.shp_group_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.shp_group_fetch_matches.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpMatches)]
         L.shp_group_local_engines.argtypes = [ctypes.c_void_p]
         L.shp_group_engine.restype = ctypes.c_void_p
@@ -282,8 +285,7 @@ class HipGroup:
         if rc != 0:
             raise ShpError(rc, lib().shp_group_last_error(self.h).decode())
 
-    def push_device(self, slices):
-        """slices: per local rank, (ts, key, stream-or-None, [cols]) torch tensors on that rank's device."""
+    def _batches(self, slices):
         arr = (ShpBatch * self.nlocal)()
         keep = []
         for i, (ts, key, stream, cols) in enumerate(slices):
@@ -291,8 +293,25 @@ class HipGroup:
             keep.append(colp)
             arr[i] = ShpBatch(ts.numel(), ts.data_ptr(), key.data_ptr(), None if stream is None else stream.data_ptr(),
                               ctypes.cast(colp, ctypes.c_void_p), None)
+        return arr, keep
+
+    def push_device(self, slices):
+        """slices: per local rank, (ts, key, stream-or-None, [cols]) torch tensors on that rank's device."""
+        arr, keep = self._batches(slices)
         counts = (ctypes.c_int64 * self.nlocal)()
         self._check(lib().shp_group_push(self.h, arr, counts))
+        return list(counts)
+
+    def stage_device(self, slices):
+        """Split + exchange one batch into a receive slot (the inputs may be reused once this returns
+        only after the next run(): the exchange reads them asynchronously)."""
+        arr, keep = self._batches(slices)
+        self._check(lib().shp_group_stage(self.h, arr))
+        return keep
+
+    def run(self):
+        counts = (ctypes.c_int64 * self.nlocal)()
+        self._check(lib().shp_group_run(self.h, counts))
         return list(counts)
 
     def fetch(self):

@@ -116,3 +116,29 @@ def test_group_rank_overflow_is_refused():
     g["key"] = (g["key"] // 2) * 2  # every key even: all events to rank 0
     with pytest.raises(ShpError, match="SHP_ERR_CAPACITY"):
         _run_group(cq, g, 2, 600, 1, LAYOUT_FULL, max_batch=30_000)
+
+
+@pytest.mark.parametrize("q,keys", [(2, 600), (4, 200)], ids=["c2", "c4"])
+def test_group_member_rccl_one_rank(q, keys):
+    """The per-process member (shp_group_create_rank) with a one-rank RCCL communicator: the
+    count all-gather and the grouped ncclSend / ncclRecv (to itself) run as they do across
+    processes on an 8-GPU node."""
+    import torch
+    from siddhi_amd.native import LAYOUT_FULL, HipGroup, comm_id
+    cq = program_for(q)
+    g = small_stream(q, 80_000, keys)
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    grp = HipGroup(cq.program_json(), 0, max_keys=keys, max_batch=1 << 17, max_matches=1 << 17, world=1, rank=0,
+                   comm=comm_id(), device=0, match_layout=LAYOUT_FULL)
+    cols = columns_for(cq, g)
+    parts = []
+    for lo, hi in ((0, 30_000), (30_000, 80_000)):
+        grp.push_device(_slices(g, cols, lo, hi, 1, len(cq.program["streams"]) > 1))
+        parts.append(grp.fetch())
+        torch.cuda.synchronize()
+    grp.close()
+    got = per_key(_concat(parts))
+    if q == 4:
+        want, got = _drop_pos(want), _drop_pos(got)
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(v) for v in want.values()) > 1000
