@@ -133,6 +133,15 @@ int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out);
  * SnapshotService (core/util/snapshot/SnapshotService.java:90-188) for the query. */
 int shp_snapshot(shp_engine* e, void** buf, size_t* len);
 int shp_restore(shp_engine* e, const void* buf, size_t len);
+/* A snapshot of this engine decoded into the reference's State.snapshot() key names, as JSON:
+ * {"engine": {path, seq, clock}, "keys": {"<key id>": {"<state>": {"FirstEvent",
+ * "PendingStateEventList", "NewAndEveryStateEventList", "Initialized", "Started"
+ * (StreamPreStateProcessor.java:450-469), count states also "SuccessCondition", "StartStateReset"
+ * (CountPreStateProcessor.java:206-219), absent states "IsActive", "LastScheduledTime",
+ * "LastArrivalTime" (AbsentStreamPreStateProcessor.java:328-341)}, "scheduler<i>": {"ToNotifyQueue"}
+ * (Scheduler.java:349-360)}}}; a partial is {ts, type, slots: per state the [{seq, ts}] chain}.
+ * Writes at most cap bytes (NUL-terminated) and returns the full length, or a negative status. */
+int64_t shp_snapshot_describe(shp_engine* e, const void* buf, size_t len, char* out, size_t cap);
 int shp_engine_num_states(const shp_engine* e);
 /* Which kernels the engine runs: 2 = sweep (owner partition + LDS sweep), 1 = specialised 2-state
  * scan kernel, 0 = general NFA lanes. */

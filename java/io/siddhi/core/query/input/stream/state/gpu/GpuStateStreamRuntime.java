@@ -1,0 +1,313 @@
+/*
+ * GpuStateStreamRuntime — the drop-in StreamRuntime for a pattern / sequence query whose state
+ * machine runs in libsiddhi_hip.so (SURVEY.md §8b, §8f-2).  Replaces StateStreamRuntime
+ * (core/query/input/stream/state/StateStreamRuntime.java:38-98) and, below it, the
+ * Stream/Count/Logical/Absent Pre/PostStateProcessor chain.  The Java host keeps SiddhiManager,
+ * SiddhiAppRuntime, InputHandler.send, QuerySelector and the callbacks unchanged.
+ *
+ * Wiring (reference side):
+ *   core/util/parser/InputStreamParser.java:88-93 — for a StateInputStream whose program the
+ *     host can lower (the JSON siddhi_amd/query/compiler.py emits), return
+ *     `new GpuStateStreamRuntime(...)` instead of StateInputStreamParser.parseInputStream(...).
+ *   core/util/SiddhiAppRuntimeBuilder.java:172-190 — unchanged: it subscribes the receivers
+ *     getSingleStreamRuntimes() returns (GpuStateReceiver, one per distinct stream).
+ *   core/partition/PartitionStreamReceiver.java:176-283 — for a partitioned GPU query, append
+ *     (key dictionary id, event) to the same batch instead of one send() per key
+ *     (GpuStateReceiver.receive(long, Object[], int keyId)); the engine partitions on the device.
+ *
+ * Concurrency: the reference serialises a query with synchronized(patternSyncObject)
+ * (SingleProcessStreamReceiver.java:52); every entry point here takes `lock`.
+ * Source only: no JDK in this repository's image, so it is not compiled here (DESIGN.md §6).
+ */
+package io.siddhi.core.query.input.stream.state.gpu;
+
+import io.siddhi.core.config.SiddhiQueryContext;
+import io.siddhi.core.event.ComplexEvent;
+import io.siddhi.core.event.ComplexEventChunk;
+import io.siddhi.core.event.MetaComplexEvent;
+import io.siddhi.core.event.state.MetaStateEvent;
+import io.siddhi.core.event.state.StateEvent;
+import io.siddhi.core.event.stream.StreamEvent;
+import io.siddhi.core.exception.SiddhiAppCreationException;
+import io.siddhi.core.exception.SiddhiAppRuntimeException;
+import io.siddhi.core.query.input.stream.StreamRuntime;
+import io.siddhi.core.query.input.stream.single.SingleStreamRuntime;
+import io.siddhi.core.query.processor.ProcessingMode;
+import io.siddhi.core.query.processor.Processor;
+import io.siddhi.core.query.selector.QuerySelector;
+
+import java.lang.foreign.Arena;
+import java.lang.foreign.MemorySegment;
+import java.util.ArrayList;
+import java.util.List;
+import java.util.Map;
+import java.util.concurrent.locks.ReentrantLock;
+
+import static java.lang.foreign.ValueLayout.ADDRESS;
+import static java.lang.foreign.ValueLayout.JAVA_BYTE;
+import static java.lang.foreign.ValueLayout.JAVA_INT;
+import static java.lang.foreign.ValueLayout.JAVA_LONG;
+import static java.lang.foreign.ValueLayout.JAVA_SHORT;
+
+public final class GpuStateStreamRuntime implements StreamRuntime {
+
+    private final Arena arena = Arena.ofShared();
+    private final ReentrantLock lock = new ReentrantLock();
+    private final MemorySegment engine;            // shp_engine*
+    private final MemorySegment matches;           // shp_matches, filled by the library
+    private final ColumnarBatch batch;
+    private final MetaStateEvent metaStateEvent;
+    private final int numStates;
+    private final int outputDataSize;
+    private final List<SingleStreamRuntime> singleStreamRuntimes = new ArrayList<>();
+    private Processor selector;                    // QuerySelector (setCommonProcessor)
+
+    /**
+     * @param programJson  the flattened processor graph (siddhi_amd/query/compiler.py's format:
+     *                     processors, next/every/partner links, within, start states, filters as
+     *                     predicate bytecode) the host lowers from the StateInputStream
+     * @param streamIds    the program's streams, in program["streams"] order
+     * @param columns      program["columns"]
+     * @param maxKeys      partition-key dictionary capacity (1 when the query is not partitioned)
+     * @param maxBatch     events per push (a batch is flushed when full, on send return, or by timer)
+     * @param device       HIP device ordinal
+     * @param startClock   the event-time clock at start() (0 in playback mode)
+     */
+    public GpuStateStreamRuntime(String programJson, String[] streamIds, ColumnarBatch.Column[] columns,
+                                 int maxKeys, long maxBatch, int device, long startClock,
+                                 MetaStateEvent metaStateEvent, SiddhiQueryContext queryContext,
+                                 Map<String, Integer> stringDictionary) {
+        this.metaStateEvent = metaStateEvent;
+        this.outputDataSize = metaStateEvent.getOutputDataAttributes() == null ? 0
+                : metaStateEvent.getOutputDataAttributes().size();
+        MemorySegment cfg = arena.allocate(ShpNative.CONFIG);
+        cfg.set(JAVA_INT, 0, device);
+        cfg.set(JAVA_INT, 4, maxKeys);
+        cfg.set(JAVA_LONG, 8, maxBatch);
+        cfg.set(JAVA_LONG, 16, 0L);                 // max_matches: engine default
+        cfg.set(JAVA_LONG, 24, startClock);
+        cfg.set(JAVA_INT, 32, 0);                   // force_general: auto path
+        cfg.set(JAVA_INT, 36, 0);                   // profile_kernels
+        cfg.set(JAVA_INT, 40, ShpNative.LAYOUT_FULL);
+        MemorySegment out = arena.allocate(ADDRESS);
+        int rc;
+        try {
+            rc = (int) ShpNative.ENGINE_CREATE.invokeExact(arena.allocateFrom(programJson), cfg, out);
+        } catch (Throwable t) {
+            throw new SiddhiAppCreationException("shp_engine_create failed: " + t, t);
+        }
+        if (rc != ShpNative.OK) {
+            // SHP_ERR_UNSUPPORTED = a construct outside the state path: the host falls back to
+            // StateInputStreamParser (the reference runtime) for this query
+            throw new SiddhiAppCreationException("shp_engine_create: " + ShpNative.codeName(rc));
+        }
+        engine = out.get(ADDRESS, 0);
+        matches = arena.allocate(ShpNative.MATCHES);
+        try {
+            numStates = (int) ShpNative.NUM_STATES.invokeExact(engine);
+        } catch (Throwable t) {
+            throw new SiddhiAppCreationException("shp_engine_num_states failed", t);
+        }
+        batch = new ColumnarBatch(arena, maxBatch, columns, stringDictionary, 64);
+        for (int s = 0; s < streamIds.length; s++) {
+            GpuStateReceiver r = new GpuStateReceiver(streamIds[s], s, this, queryContext);
+            singleStreamRuntimes.add(new SingleStreamRuntime(r, null, ProcessingMode.BATCH,
+                    metaStateEvent.getMetaStreamEvent(s)));
+        }
+    }
+
+    // ---------------------------------------------------------------- StreamRuntime
+    @Override
+    public List<SingleStreamRuntime> getSingleStreamRuntimes() {
+        return singleStreamRuntimes;
+    }
+
+    @Override
+    public void setCommonProcessor(Processor commonProcessor) {
+        this.selector = commonProcessor;
+    }
+
+    @Override
+    public MetaComplexEvent getMetaComplexEvent() {
+        return metaStateEvent;
+    }
+
+    @Override
+    public ProcessingMode getProcessingMode() {
+        return ProcessingMode.BATCH;
+    }
+
+    @Override
+    public QuerySelector getQuerySelector() {
+        return null;
+    }
+
+    // ---------------------------------------------------------------- ingress (GpuStateReceiver)
+    void append(long timestamp, int keyId, int streamIndex, Object[] data) {
+        lock.lock();
+        try {
+            batch.append(timestamp, keyId, streamIndex, data);
+            if (batch.full()) {
+                flush();
+            }
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /** One shp_push_batch of the appended events, then one StateEvent per match into the
+     * selector, in record order (per key = the reference's emission order). */
+    void flush() {
+        lock.lock();
+        try {
+            if (batch.size() == 0) {
+                return;
+            }
+            int rc;
+            try {
+                rc = (int) ShpNative.PUSH_BATCH.invokeExact(engine, batch.descriptor(), matches);
+            } catch (Throwable t) {
+                throw new SiddhiAppRuntimeException("shp_push_batch failed: " + t, t);
+            }
+            batch.clear();
+            if (rc != ShpNative.OK) {
+                throw new SiddhiAppRuntimeException("shp_push_batch: " + ShpNative.codeName(rc) + ": "
+                        + ShpNative.lastError(engine));
+            }
+            deliver();
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /** TimestampGeneratorImpl.setCurrentTimestamp with no event (absent-state timers). */
+    void advanceClock(long now) {
+        lock.lock();
+        try {
+            flush();
+            int rc;
+            try {
+                rc = (int) ShpNative.ADVANCE_CLOCK.invokeExact(engine, now, matches);
+            } catch (Throwable t) {
+                throw new SiddhiAppRuntimeException("shp_advance_clock failed: " + t, t);
+            }
+            if (rc != ShpNative.OK) {
+                throw new SiddhiAppRuntimeException("shp_advance_clock: " + ShpNative.lastError(engine));
+            }
+            deliver();
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    // StateEvents from the match records: slot s of match i holds slot_len[i*S+s] event sequence
+    // numbers from refs[ref_off[i] + ...] (a count state's chain, in order); -1 = an empty slot
+    private void deliver() {
+        long m = ShpNative.matchesLong(matches, "m");
+        if (m == 0) {
+            return;
+        }
+        MemorySegment ts = ShpNative.matchesPtr(matches, "ts", m * 8);
+        MemorySegment type = ShpNative.matchesPtr(matches, "type", m);
+        MemorySegment refOff = ShpNative.matchesPtr(matches, "ref_off", m * 8);
+        MemorySegment slotLen = ShpNative.matchesPtr(matches, "slot_len", m * numStates * 2L);
+        long nrefs = 0;
+        for (long i = 0; i < m * numStates; i++) {
+            nrefs += slotLen.getAtIndex(JAVA_SHORT, i);
+        }
+        MemorySegment refs = ShpNative.matchesPtr(matches, "refs", Math.max(1, nrefs) * 8);
+        for (long i = 0; i < m; i++) {
+            StateEvent se = new StateEvent(numStates, outputDataSize);
+            se.setTimestamp(ts.getAtIndex(JAVA_LONG, i));
+            se.setType(type.get(JAVA_BYTE, i) == 0 ? ComplexEvent.Type.CURRENT : ComplexEvent.Type.EXPIRED);
+            long r = refOff.getAtIndex(JAVA_LONG, i);
+            for (int s = 0; s < numStates; s++) {
+                int len = slotLen.getAtIndex(JAVA_SHORT, i * numStates + s);
+                for (int k = 0; k < len; k++) {
+                    long seq = refs.getAtIndex(JAVA_LONG, r++);
+                    if (seq >= 0) {
+                        StreamEvent e = batch.event(seq,
+                                metaStateEvent.getMetaStreamEvent(s).getOutputData().size());
+                        se.addEvent(s, e);   // count states: a `next` chain, as StateEvent.addEvent builds it
+                    }
+                }
+            }
+            selector.process(new ComplexEventChunk<>(se, se));
+        }
+    }
+
+    // ---------------------------------------------------------------- snapshot (GpuStateHolder)
+    byte[] snapshot() {
+        lock.lock();
+        try {
+            flush();
+            MemorySegment buf = arena.allocate(ADDRESS);
+            MemorySegment len = arena.allocate(JAVA_LONG);
+            int rc = (int) ShpNative.SNAPSHOT.invokeExact(engine, buf, len);
+            if (rc != ShpNative.OK) {
+                throw new SiddhiAppRuntimeException("shp_snapshot: " + ShpNative.lastError(engine));
+            }
+            long n = len.get(JAVA_LONG, 0);
+            return buf.get(ADDRESS, 0).reinterpret(n).toArray(JAVA_BYTE);
+        } catch (RuntimeException e) {
+            throw e;
+        } catch (Throwable t) {
+            throw new SiddhiAppRuntimeException("shp_snapshot failed: " + t, t);
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /** The snapshot in the reference's State.snapshot() key names (shp_snapshot_describe, JSON):
+     * per key and state, FirstEvent / PendingStateEventList / NewAndEveryStateEventList /
+     * Initialized / Started (StreamPreStateProcessor.java:450-469), plus IsActive /
+     * LastScheduledTime / LastArrivalTime for absent states and ToNotifyQueue for timers. */
+    String describe(byte[] blob) {
+        try (Arena a = Arena.ofConfined()) {
+            MemorySegment in = a.allocateFrom(JAVA_BYTE, blob);
+            long need = (long) ShpNative.SNAPSHOT_DESCRIBE.invokeExact(engine, in, (long) blob.length,
+                    MemorySegment.NULL, 0L);
+            if (need < 0) {
+                throw new SiddhiAppRuntimeException("shp_snapshot_describe: " + ShpNative.codeName((int) need));
+            }
+            MemorySegment out = a.allocate(need + 1);
+            long got = (long) ShpNative.SNAPSHOT_DESCRIBE.invokeExact(engine, in, (long) blob.length, out, need + 1);
+            return out.getString(0);
+        } catch (RuntimeException e) {
+            throw e;
+        } catch (Throwable t) {
+            throw new SiddhiAppRuntimeException("shp_snapshot_describe failed: " + t, t);
+        }
+    }
+
+    void restore(byte[] blob) {
+        lock.lock();
+        try (Arena a = Arena.ofConfined()) {
+            MemorySegment in = a.allocateFrom(JAVA_BYTE, blob);
+            int rc = (int) ShpNative.RESTORE.invokeExact(engine, in, (long) blob.length);
+            if (rc != ShpNative.OK) {
+                throw new SiddhiAppRuntimeException("shp_restore: " + ShpNative.lastError(engine));
+            }
+        } catch (RuntimeException e) {
+            throw e;
+        } catch (Throwable t) {
+            throw new SiddhiAppRuntimeException("shp_restore failed: " + t, t);
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /** SiddhiAppRuntime.shutdown for the query. */
+    public void shutdown() {
+        lock.lock();
+        try {
+            flush();
+            ShpNative.ENGINE_DESTROY.invokeExact(engine);
+        } catch (Throwable t) {
+            throw new SiddhiAppRuntimeException("shp_engine_destroy failed: " + t, t);
+        } finally {
+            lock.unlock();
+            arena.close();
+        }
+    }
+}

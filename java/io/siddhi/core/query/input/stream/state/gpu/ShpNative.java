@@ -1,0 +1,161 @@
+/*
+ * Panama FFM (java.lang.foreign, JDK >= 22) binding of libsiddhi_hip.so — include/siddhi_hip.h.
+ * Source only: this repository's image has no JDK, so it is not compiled here (DESIGN.md §6).
+ *
+ * Every downcall mirrors one C-ABI entry point; struct layouts mirror shp_config, shp_batch and
+ * shp_matches field for field (tests/test_abi.py checks the C layouts against the ctypes mirror
+ * siddhi_amd/native.py; the offsets below are the same).
+ */
+package io.siddhi.core.query.input.stream.state.gpu;
+
+import java.lang.foreign.Arena;
+import java.lang.foreign.FunctionDescriptor;
+import java.lang.foreign.Linker;
+import java.lang.foreign.MemoryLayout;
+import java.lang.foreign.MemorySegment;
+import java.lang.foreign.StructLayout;
+import java.lang.foreign.SymbolLookup;
+import java.lang.invoke.MethodHandle;
+
+import static java.lang.foreign.ValueLayout.ADDRESS;
+import static java.lang.foreign.ValueLayout.JAVA_DOUBLE;
+import static java.lang.foreign.ValueLayout.JAVA_INT;
+import static java.lang.foreign.ValueLayout.JAVA_LONG;
+
+final class ShpNative {
+
+    static final int OK = 0;
+    static final int ERR_ARG = -1;
+    static final int ERR_UNSUPPORTED = -2;
+    static final int ERR_CAPACITY = -3;
+    static final int ERR_OUTPUT = -4;
+    static final int ERR_DEVICE = -5;
+    static final int ERR_KEYS = -6;
+
+    static final int LAYOUT_FULL = 0;
+    static final int LAYOUT_PAIRS = 1;
+    static final int LAYOUT_AGG = 2;
+    static final int LAYOUT_PAIRS32 = 3;
+
+    static final int COMM_ID_BYTES = 128;
+
+    static final Linker LINKER = Linker.nativeLinker();
+    static final SymbolLookup LIB = SymbolLookup.libraryLookup(
+            System.getProperty("siddhi.hip.lib", "libsiddhi_hip.so"), Arena.global());
+
+    /** struct shp_config (48 bytes). */
+    static final StructLayout CONFIG = MemoryLayout.structLayout(
+            JAVA_INT.withName("device"), JAVA_INT.withName("max_keys"),
+            JAVA_LONG.withName("max_batch"), JAVA_LONG.withName("max_matches"),
+            JAVA_LONG.withName("start_clock"), JAVA_INT.withName("force_general"),
+            JAVA_INT.withName("profile_kernels"), JAVA_INT.withName("match_layout"),
+            MemoryLayout.paddingLayout(4));
+
+    /** struct shp_batch (64 bytes): n, ts, key, stream, cols, nulls, clock, seq. */
+    static final StructLayout BATCH = MemoryLayout.structLayout(
+            JAVA_LONG.withName("n"), ADDRESS.withName("ts"), ADDRESS.withName("key"),
+            ADDRESS.withName("stream"), ADDRESS.withName("cols"), ADDRESS.withName("nulls"),
+            ADDRESS.withName("clock"), ADDRESS.withName("seq"));
+
+    /** struct shp_matches (88 bytes). */
+    static final StructLayout MATCHES = MemoryLayout.structLayout(
+            JAVA_LONG.withName("m"), JAVA_INT.withName("num_states"), MemoryLayout.paddingLayout(4),
+            ADDRESS.withName("key"), ADDRESS.withName("ts"), ADDRESS.withName("type"),
+            ADDRESS.withName("pos"), ADDRESS.withName("ref_off"), ADDRESS.withName("slot_len"),
+            ADDRESS.withName("refs"), JAVA_INT.withName("layout"), MemoryLayout.paddingLayout(4),
+            ADDRESS.withName("agg"));
+
+    // ---- one engine (StateInputStreamParser.parseInputStream + the processor chain)
+    static final MethodHandle ENGINE_CREATE = fn("shp_engine_create", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
+    static final MethodHandle PUSH_BATCH = fn("shp_push_batch", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
+    static final MethodHandle PUSH_BATCH_DEVICE = fn("shp_push_batch_device", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
+    static final MethodHandle FETCH_MATCHES = fn("shp_fetch_matches", JAVA_INT, ADDRESS, ADDRESS);
+    static final MethodHandle ADVANCE_CLOCK = fn("shp_advance_clock", JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS);
+    static final MethodHandle SNAPSHOT = fn("shp_snapshot", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
+    static final MethodHandle RESTORE = fn("shp_restore", JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG);
+    static final MethodHandle SNAPSHOT_DESCRIBE = fn("shp_snapshot_describe", JAVA_LONG, ADDRESS, ADDRESS, JAVA_LONG,
+            ADDRESS, JAVA_LONG);
+    static final MethodHandle NUM_STATES = fn("shp_engine_num_states", JAVA_INT, ADDRESS);
+    static final MethodHandle LAST_ERROR = fn("shp_last_error", ADDRESS, ADDRESS);
+    static final MethodHandle ENGINE_DESTROY = fnVoid("shp_engine_destroy", ADDRESS);
+
+    // ---- page-locked receive memory for match payloads
+    static final MethodHandle HOST_REGISTER = fn("shp_host_register", JAVA_INT, ADDRESS, JAVA_LONG);
+    static final MethodHandle HOST_UNREGISTER = fn("shp_host_unregister", JAVA_INT, ADDRESS);
+
+    // ---- key-sharded groups (multi-GPU behind the C-ABI)
+    static final MethodHandle COMM_ID = fn("shp_comm_id", JAVA_INT, ADDRESS, JAVA_LONG);
+    static final MethodHandle GROUP_CREATE = fn("shp_group_create", JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, ADDRESS,
+            ADDRESS);
+    static final MethodHandle GROUP_CREATE_RANK = fn("shp_group_create_rank", JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
+            JAVA_INT, ADDRESS, ADDRESS);
+    static final MethodHandle GROUP_PUSH = fn("shp_group_push", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
+    static final MethodHandle GROUP_STAGE = fn("shp_group_stage", JAVA_INT, ADDRESS, ADDRESS);
+    static final MethodHandle GROUP_RUN = fn("shp_group_run", JAVA_INT, ADDRESS, ADDRESS);
+    static final MethodHandle GROUP_FETCH = fn("shp_group_fetch_matches", JAVA_INT, ADDRESS, ADDRESS);
+    static final MethodHandle GROUP_LAST_ERROR = fn("shp_group_last_error", ADDRESS, ADDRESS);
+    static final MethodHandle GROUP_DESTROY = fnVoid("shp_group_destroy", ADDRESS);
+
+    private ShpNative() {
+    }
+
+    private static MethodHandle fn(String name, MemoryLayout ret, MemoryLayout... args) {
+        return LINKER.downcallHandle(LIB.find(name).orElseThrow(
+                () -> new UnsatisfiedLinkError("libsiddhi_hip.so does not export " + name)),
+                FunctionDescriptor.of(ret, args));
+    }
+
+    private static MethodHandle fnVoid(String name, MemoryLayout... args) {
+        return LINKER.downcallHandle(LIB.find(name).orElseThrow(
+                () -> new UnsatisfiedLinkError("libsiddhi_hip.so does not export " + name)),
+                FunctionDescriptor.ofVoid(args));
+    }
+
+    /** The engine's last error text (shp_last_error). */
+    static String lastError(MemorySegment engine) {
+        try {
+            MemorySegment s = (MemorySegment) LAST_ERROR.invokeExact(engine);
+            return s.reinterpret(1 << 16).getString(0);
+        } catch (Throwable t) {
+            return "shp_last_error failed: " + t;
+        }
+    }
+
+    static String groupLastError(MemorySegment group) {
+        try {
+            MemorySegment s = (MemorySegment) GROUP_LAST_ERROR.invokeExact(group);
+            return s.reinterpret(1 << 16).getString(0);
+        } catch (Throwable t) {
+            return "shp_group_last_error failed: " + t;
+        }
+    }
+
+    static String codeName(int rc) {
+        switch (rc) {
+            case ERR_ARG: return "SHP_ERR_ARG";
+            case ERR_UNSUPPORTED: return "SHP_ERR_UNSUPPORTED";
+            case ERR_CAPACITY: return "SHP_ERR_CAPACITY";
+            case ERR_OUTPUT: return "SHP_ERR_OUTPUT";
+            case ERR_DEVICE: return "SHP_ERR_DEVICE";
+            case ERR_KEYS: return "SHP_ERR_KEYS";
+            default: return Integer.toString(rc);
+        }
+    }
+
+    /** Reads field `name` of an shp_matches the library filled. */
+    static long matchesLong(MemorySegment m, String name) {
+        return m.get(JAVA_LONG, MATCHES.byteOffset(MemoryLayout.PathElement.groupElement(name)));
+    }
+
+    static int matchesInt(MemorySegment m, String name) {
+        return m.get(JAVA_INT, MATCHES.byteOffset(MemoryLayout.PathElement.groupElement(name)));
+    }
+
+    static MemorySegment matchesPtr(MemorySegment m, String name, long bytes) {
+        return m.get(ADDRESS, MATCHES.byteOffset(MemoryLayout.PathElement.groupElement(name))).reinterpret(bytes);
+    }
+
+    static double aggAt(MemorySegment agg, long i) {
+        return agg.getAtIndex(JAVA_DOUBLE, i);
+    }
+}

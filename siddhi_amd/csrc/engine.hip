@@ -660,6 +660,194 @@ struct shp_engine {
     return SHP_OK;
   }
 
+  // ---- the snapshot in the reference's State.snapshot() key names (shp_snapshot_describe):
+  // per partition key and state, what StreamPreState.snapshot (StreamPreStateProcessor.java:
+  // 450-469) and its Count / Absent / Scheduler subclasses would hold.  Events are named by
+  // {seq, ts}: the host rebuilds StreamEvents from the sequence numbers, as for match records.
+  static void jnum(std::string& o, int64_t v) { o += std::to_string(v); }
+  static void jbool(std::string& o, bool b) { o += b ? "true" : "false"; }
+
+  std::string describe(const void* buf, size_t len) {
+    SnapHeader h;
+    if (!buf || len < sizeof h) throw std::runtime_error("snapshot too short");
+    memcpy(&h, buf, sizeof h);
+    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 2 || h.path != fast || h.max_keys != cfg.max_keys ||
+        h.program_hash != fnv1a(program))
+      throw std::runtime_error("not a snapshot of this engine's query, path and key capacity");
+    auto secs = state_sections();
+    std::vector<const char*> sp(secs.size());
+    const char* q = (const char*)buf + sizeof h;
+    for (size_t i = 0; i < secs.size(); i++) {
+      uint64_t b;
+      memcpy(&b, q, 8);
+      if (b != secs[i].bytes || (size_t)(q + 8 + b - (const char*)buf) > len)
+        throw std::runtime_error("snapshot layout mismatch");
+      sp[i] = q + 8;
+      q += 8 + b;
+    }
+    const DevProg& P = comp.P;
+    std::string o = "{\"engine\":{\"path\":";
+    jnum(o, fast);
+    o += ",\"seq\":";
+    jnum(o, h.seq);
+    o += ",\"clock\":";
+    jnum(o, h.clock);
+    o += "},\"keys\":{";
+    bool firstKey = true;
+    auto ev = [&](std::string& s, int64_t seqv, int64_t tsv) {
+      s += "{\"seq\":";
+      jnum(s, seqv);
+      s += ",\"ts\":";
+      jnum(s, tsv);
+      s += "}";
+    };
+    if (fast == 2 || fast == 1) {
+      // 2-state `every e1 -> e2 within`: e1's start partial, e2's open candidates (partials
+      // holding e1); the key's latest event, when it opened a candidate, left that one (and
+      // e1's re-armed partial) on the new-and-every lists
+      std::vector<std::vector<std::pair<int64_t, int64_t>>> open(cfg.max_keys);  // (seq, ts) per key
+      std::vector<uint8_t> lastc(cfg.max_keys, 0), seen(cfg.max_keys, 0);
+      if (fast == 2) {
+        int32_t nown = 0;
+        std::vector<uint32_t> kmap;
+        SweepState::build_map(cfg.max_keys, nown, kmap);
+        std::vector<int32_t> inv((size_t)nown * SW_LK, -1);
+        for (int32_t k = 0; k < cfg.max_keys; k++) inv[(size_t)(kmap[k] & 0xffffu) * SW_LK + (kmap[k] >> 16)] = k;
+        const int32_t* c_n = (const int32_t*)sp[0];
+        const int64_t* c_ts = (const int64_t*)sp[1];
+        const int64_t* c_seq = (const int64_t*)sp[2];
+        const uint8_t* c_lk = (const uint8_t*)sp[4];
+        const uint8_t* lc = (const uint8_t*)sp[6];
+        for (int32_t ow = 0; ow < nown; ow++) {
+          for (int i = 0; i < c_n[ow]; i++) {
+            const int64_t c = (int64_t)ow * SWS_CCAP + i;
+            const int32_t k = inv[(size_t)ow * SW_LK + c_lk[c]];
+            if (k >= 0) open[k].push_back({c_seq[c], c_ts[c]});
+          }
+          for (int l = 0; l < SW_LK; l++) {
+            const int32_t k = inv[(size_t)ow * SW_LK + l];
+            if (k >= 0) lastc[k] = lc[(size_t)ow * SW_LK + l];
+          }
+        }
+      } else {
+        const int64_t* c_seq = (const int64_t*)sp[0];
+        const int64_t* c_ts = (const int64_t*)sp[1];
+        const int32_t* c_n = (const int32_t*)sp[4];
+        const int64_t* last_ts = (const int64_t*)sp[6];
+        const uint8_t* lc = (const uint8_t*)sp[8];
+        for (int32_t k = 0; k < cfg.max_keys; k++) {
+          for (int i = 0; i < c_n[k]; i++) open[k].push_back({c_seq[(int64_t)k * FCC + i], c_ts[(int64_t)k * FCC + i]});
+          lastc[k] = lc[k];
+          seen[k] = last_ts[k] != INT64_MIN;
+        }
+      }
+      for (int32_t k = 0; k < cfg.max_keys; k++) {
+        if (open[k].empty() && !lastc[k] && !seen[k]) continue;
+        o += firstKey ? "\"" : ",\"";
+        firstKey = false;
+        jnum(o, k);
+        o += "\":{\"e1\":{\"FirstEvent\":null,\"PendingStateEventList\":[";
+        const char* empty = "{\"ts\":-1,\"slots\":[[],[]]}";
+        if (!lastc[k]) o += empty;
+        o += "],\"NewAndEveryStateEventList\":[";
+        if (lastc[k]) o += empty;
+        o += "],\"Initialized\":true,\"Started\":false},\"e2\":{\"FirstEvent\":null,\"PendingStateEventList\":[";
+        const size_t np = open[k].size() - ((lastc[k] && !open[k].empty()) ? 1 : 0);
+        for (size_t i = 0; i < open[k].size(); i++) {
+          if (i == np) o += "],\"NewAndEveryStateEventList\":[";
+          else if (i) o += ",";
+          o += "{\"ts\":";
+          jnum(o, open[k][i].second);
+          o += ",\"slots\":[[";
+          ev(o, open[k][i].first, open[k][i].second);
+          o += "],[]]}";
+        }
+        if (np == open[k].size()) o += "],\"NewAndEveryStateEventList\":[";
+        o += "],\"Initialized\":false,\"Started\":false}}";
+      }
+    } else {
+      // general lanes: decode each key's arena (lane-interleaved SoA, LaneLayout)
+      const char* a = sp[0];
+      auto at = [&](int64_t off, int64_t i, int64_t k, int sz) -> const char* {
+        return a + off + (i * Y.L + k) * sz;
+      };
+      auto i16 = [&](int64_t off, int64_t i, int64_t k) { int16_t v; memcpy(&v, at(off, i, k, 2), 2); return v; };
+      auto i64 = [&](int64_t off, int64_t i, int64_t k) { int64_t v; memcpy(&v, at(off, i, k, 8), 8); return v; };
+      auto u8 = [&](int64_t off, int64_t i, int64_t k) { return *(const uint8_t*)at(off, i, k, 1); };
+      for (int64_t k = 0; k < Y.L; k++) {
+        if (!u8(Y.o_kinit, 0, k)) continue;
+        o += firstKey ? "\"" : ",\"";
+        firstKey = false;
+        jnum(o, k);
+        o += "\":{";
+        auto partial = [&](std::string& s, int se) {
+          s += "{\"ts\":";
+          jnum(s, i64(Y.o_se_ts, se, k));
+          s += ",\"type\":\"";
+          s += u8(Y.o_se_type, se, k) ? "EXPIRED" : "CURRENT";
+          s += "\",\"slots\":[";
+          for (int st = 0; st < P.nstates; st++) {
+            s += st ? ",[" : "[";
+            int guard = 0;
+            for (int nd = i16(Y.o_se_slot, (int64_t)se * MAXS + st, k); nd >= 0 && guard < NN;
+                 nd = i16(Y.o_nd_next, nd, k), guard++) {
+              if (guard) s += ",";
+              ev(s, i64(Y.o_nd_seq, nd, k), i64(Y.o_nd_ts, nd, k));
+            }
+            s += "]";
+          }
+          s += "]}";
+        };
+        for (int p = 0; p < P.npre; p++) {
+          const DPre& d = P.pre[p];
+          o += p ? ",\"" : "\"";
+          o += "pre" + std::to_string(p) + "(e" + std::to_string(d.stateId + 1) + ")\":{\"FirstEvent\":null";
+          for (int which = 0; which < 2; which++) {
+            o += which == 0 ? ",\"PendingStateEventList\":[" : ",\"NewAndEveryStateEventList\":[";
+            const int n = i16(Y.o_lst_len, which * MAXP + p, k);
+            for (int i = 0; i < n; i++) {
+              if (i) o += ",";
+              partial(o, i16(Y.o_lst, (int64_t)(which * MAXP + p) * LCAP + i, k));
+            }
+            o += "]";
+          }
+          const uint8_t f = u8(Y.o_pflags, p, k);
+          o += ",\"Initialized\":";
+          jbool(o, f & F_INIT);
+          o += ",\"Started\":";
+          jbool(o, f & F_STARTED);
+          if (d.kind == K_COUNT) {
+            o += ",\"SuccessCondition\":";
+            jbool(o, f & F_SUCCESS);
+            o += ",\"StartStateReset\":";
+            jbool(o, f & F_SSRESET);
+          }
+          if (d.kind == K_ABSENT_STREAM || d.kind == K_ABSENT_LOGICAL) {
+            o += ",\"IsActive\":";
+            jbool(o, !(f & F_INACTIVE));
+            o += ",\"LastScheduledTime\":";
+            jnum(o, i64(Y.o_lsched, p, k));
+            o += ",\"LastArrivalTime\":";
+            jnum(o, i64(Y.o_larr, p, k));
+          }
+          o += "}";
+        }
+        for (int s = 0; s < P.nsched; s++) {  // Scheduler.SchedulerState: ToNotifyQueue (FIFO)
+          o += ",\"scheduler" + std::to_string(s) + "\":{\"ToNotifyQueue\":[";
+          const int hd = i16(Y.o_qhead, s, k), n = i16(Y.o_qlen, s, k);
+          for (int i = 0; i < n; i++) {
+            if (i) o += ",";
+            jnum(o, i64(Y.o_q, (int64_t)s * QCAP + (hd + i) % QCAP, k));
+          }
+          o += "]}";
+        }
+        o += "}";
+      }
+    }
+    o += "}}";
+    return o;
+  }
+
   // sweep path, PAIRS layout: materialise the full records of the last push on demand
   void ensure_expanded() {
     if (fast != 2 || expanded || cfg.match_layout == SHP_LAYOUT_AGG) return;
@@ -917,6 +1105,22 @@ int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out) {
     e->fetch(out);
     return SHP_OK;
   });
+}
+
+int64_t shp_snapshot_describe(shp_engine* e, const void* blob, size_t len, char* out, size_t cap) {
+  if (!e || !blob) return SHP_ERR_ARG;
+  std::string s;
+  const int rc = guarded(e, [&]() {
+    s = e->describe(blob, len);
+    return SHP_OK;
+  });
+  if (rc != SHP_OK) return rc;
+  if (out && cap) {
+    const size_t n = std::min(cap - 1, s.size());
+    memcpy(out, s.data(), n);
+    out[n] = 0;
+  }
+  return (int64_t)s.size();
 }
 
 int shp_engine_num_states(const shp_engine* e) { return e ? e->comp.P.nstates : 0; }

@@ -25,7 +25,7 @@ SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_
            "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
            "shp_dev_to_host", "shp_host_alloc", "shp_host_free", "shp_host_register",
-           "shp_host_unregister", "shp_snapshot", "shp_restore", "shp_shard_workspace_bytes",
+           "shp_host_unregister", "shp_snapshot", "shp_restore", "shp_snapshot_describe", "shp_shard_workspace_bytes",
            "shp_shard_partition", "shp_shard_unpack", "shp_shard_partition_soa", "shp_comm_id",
            "shp_group_create", "shp_group_create_rank", "shp_group_push", "shp_group_stage", "shp_group_run",
            "shp_group_fetch_matches",
@@ -97,6 +97,9 @@ def lib():
         L.shp_host_unregister.argtypes = [ctypes.c_void_p]
         L.shp_snapshot.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
         L.shp_restore.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        L.shp_snapshot_describe.restype = ctypes.c_int64
+        L.shp_snapshot_describe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.c_size_t]
         L.shp_shard_workspace_bytes.restype = ctypes.c_int64
         L.shp_shard_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int]
         L.shp_shard_partition.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int] + \
@@ -216,6 +219,17 @@ class HipEngine:
         """Load a snapshot taken from an engine of the same query (shp_restore)."""
         b = ctypes.create_string_buffer(blob, len(blob))
         self._check(lib().shp_restore(self.h, b, len(blob)))
+
+    def describe(self, blob: bytes) -> dict:
+        """A snapshot in the reference's State.snapshot() key names (shp_snapshot_describe)."""
+        import json
+        b = ctypes.create_string_buffer(blob, len(blob))
+        need = lib().shp_snapshot_describe(self.h, b, len(blob), None, 0)
+        if need < 0:
+            raise ShpError(int(need), lib().shp_last_error(self.h).decode())
+        out = ctypes.create_string_buffer(need + 1)
+        lib().shp_snapshot_describe(self.h, b, len(blob), out, need + 1)
+        return json.loads(out.value.decode())
 
     def kernel_ms(self, which="total"):
         return lib().shp_last_kernel_ms(self.h, which.encode())

@@ -611,3 +611,53 @@ def test_device_minmax_java_nan_and_signed_zero(fn):
         assert (np.isnan(w) == np.isnan(h)).all(), k
         ok = ~np.isnan(w)
         assert (w[ok].view(np.uint64) == h[ok].view(np.uint64)).all(), k  # bitwise: -0.0 != 0.0
+
+
+def _lists_by_key(desc, e1, e2):
+    """{key: (e1 pending, e1 new, e2 pending, e2 new)} as seq lists, from a decoded snapshot."""
+    out = {}
+    for k, st in desc["keys"].items():
+        row = []
+        for name in (e1, e2):
+            s = st[name]
+            for lst in ("PendingStateEventList", "NewAndEveryStateEventList"):
+                row.append([tuple(ev["seq"] for slot in p["slots"] for ev in slot) for p in s[lst]])
+        out[int(k)] = tuple(row)
+    return out
+
+
+@pytest.mark.parametrize("sweep_force", [3, 2], ids=["sweep", "scan"])
+def test_snapshot_describe_agrees_across_paths(sweep_force):
+    """shp_snapshot_describe (the reference's State.snapshot() key names): the 2-state paths'
+    carried candidates decode to the same per-key PendingStateEventList / NewAndEveryStateEventList
+    of e1 and e2 as the general lanes, which keep the processor chain's lists as such."""
+    cq = program_for(2)
+    g = small_stream(2, 30_000, 300)
+    lanes = hip(1, max_keys=300, max_batch=1 << 15)(cq.program_json(), 0)
+    fastp = hip(sweep_force, max_keys=300, max_batch=1 << 15)(cq.program_json(), 0)
+    run(lanes, cq, g, 9_973)
+    run(fastp, cq, g, 9_973)
+    dl = lanes.describe(lanes.snapshot())
+    df = fastp.describe(fastp.snapshot())
+    assert dl["engine"]["seq"] == df["engine"]["seq"] == 30_000
+    a = _lists_by_key(dl, "pre0(e1)", "pre1(e2)")
+    b = _lists_by_key(df, "e1", "e2")
+    # the 2-state paths omit keys with nothing open (as fresh as a new key for this shape)
+    a = {k: v for k, v in a.items() if any(v[2:]) or v[1]}
+    assert a == b
+    assert sum(len(v[2]) + len(v[3]) for v in b.values()) > 100
+
+
+def test_snapshot_describe_absent_state_keys():
+    """C4 (logical + absent) on the lanes: absent states carry IsActive / LastScheduledTime /
+    LastArrivalTime and the key's scheduler its ToNotifyQueue."""
+    cq = program_for(4)
+    g = small_stream(4, 20_000, 50)
+    eng = hip(1, max_keys=50, max_batch=1 << 15)(cq.program_json(), 0)
+    run(eng, cq, g)
+    d = eng.describe(eng.snapshot())
+    assert len(d["keys"]) == 50
+    st = next(iter(d["keys"].values()))
+    absent = [v for k, v in st.items() if k.startswith("pre") and "IsActive" in v]
+    assert absent and all("LastScheduledTime" in v and "LastArrivalTime" in v for v in absent)
+    assert any("ToNotifyQueue" in v for k, v in st.items() if k.startswith("scheduler"))
