@@ -1309,7 +1309,9 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
               S.cv[nx][pre] = S.cv[cur][r];
               S.cseq[nx][pre] = S.cseq[cur][r];
             } else {
-              S.ckt[nx][pre] = sw_kt(lk, tb + S.tv[p].x, (f & SW_LKF_NULL) ? SW_NULL : 0ull);
+              // a slow key's tv.x may be clamped to the chunk span: take the exact ts instead
+              const int64_t ts = S.slow[lk] ? B.ts[r] - base : tb + S.tv[p].x;
+              S.ckt[nx][pre] = sw_kt(lk, ts, (f & SW_LKF_NULL) ? SW_NULL : 0ull);
               S.cv[nx][pre] = (uint32_t)S.tv[p].y;
               S.cseq[nx][pre] = bseq(B, r);
             }
