@@ -72,6 +72,7 @@ class ProgramCompiler {
       }
     }
     if ((int)code_.size() > MAXCODE) throw CompileError(-2, "predicate program too long");
+    verifyCode();
     P.ncode = (int)code_.size();
     for (size_t i = 0; i < code_.size(); i++) P.code[i] = code_[i];
     std::vector<int> all;
@@ -197,6 +198,50 @@ class ProgramCompiler {
       code_.push_back(in);
     } else {
       throw CompileError(-2, "unsupported predicate op " + op);
+    }
+  }
+
+  // The device VM (run_filter) does no per-instruction bounds checks: every program is proven
+  // safe here instead.  Abstract interpretation of the stack depth over every path of the
+  // bytecode: each filter starts at depth 0, every pop has its operands, no push passes
+  // MAXSTACK, jumps go forward and in range (so every run ends at its OP_END), and paths that
+  // merge agree on the depth.
+  void verifyCode() {
+    const int n = (int)code_.size();
+    std::vector<int> d(n + 1, -1);
+    auto reach = [&](int pc, int depth) {
+      if (pc < 0 || pc >= n) throw CompileError(-2, "predicate bytecode: jump out of range");
+      if (depth < 0 || depth > MAXSTACK) throw CompileError(-2, "predicate bytecode: stack bound");
+      if (d[pc] != -1 && d[pc] != depth) throw CompileError(-2, "predicate bytecode: inconsistent stack");
+      d[pc] = depth;
+    };
+    for (int pc0 : filterPc_)
+      if (pc0 >= 0) reach(pc0, 0);
+    for (int pc = 0; pc < n; pc++) {  // forward-only jumps: one pass in pc order sees every path
+      if (d[pc] < 0) continue;
+      const Instr& in = code_[pc];
+      const int s = d[pc];
+      auto need = [&](int k) {
+        if (s < k) throw CompileError(-2, "predicate bytecode: stack underflow");
+      };
+      switch (in.op) {
+        case OP_END: need(1); break;
+        case OP_CONST: case OP_VAR: case OP_ISNULLSTATE: reach(pc + 1, s + 1); break;
+        case OP_AND: case OP_OR:
+          need(1);
+          if (in.d <= pc) throw CompileError(-2, "predicate bytecode: backward jump");
+          reach(in.d, s);          // short circuit: the result replaces the operand
+          reach(pc + 1, s - 1);
+          break;
+        case OP_ANDEND: case OP_OREND: case OP_NOT: case OP_ISNULL: case OP_INSTOF:
+          need(1); reach(pc + 1, s); break;
+        case OP_CMP: case OP_ARITH: need(2); reach(pc + 1, s - 1); break;
+        case OP_IFTE: need(3); reach(pc + 1, s - 2); break;
+        case OP_COALESCE:
+          if (in.a < 1) throw CompileError(-2, "predicate bytecode: coalesce arity");
+          need(in.a); reach(pc + 1, s - in.a + 1); break;
+        default: throw CompileError(-2, "predicate bytecode: unknown op");
+      }
     }
   }
 

@@ -1117,10 +1117,12 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
         const uint32_t lk = f & 0xFFu;
         const int end = (int)S.binoff[lk + 1];
         // the closed form needs non-decreasing ts over the key's [carried..., events...]
+#ifndef SHP_AB_NOSLOW
         if (p > (int)S.binoff[lk] && S.tv[p - 1].x > a.x) {
           S.slow[lk] = 1;
           S.anyslow = 1;
         }
+#endif
         const int q0 = max(p + 1, (int)S.fe[lk]);  // carried candidates are not events
         const SwCand<CT> cbv = sw_cand<NT2, CT>(f2, (uint32_t)a.y, af, ai, an);
         res = cand ? -4 : -3;  // -4: unresolved
