@@ -7,6 +7,7 @@ this module.  The oracle is the CPU restatement of the reference semantics
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 import subprocess
 
@@ -57,11 +58,14 @@ class OracleEngine:
         if not self.h:
             raise ValueError(err.value.decode())
         self.S = L.oracle_num_states(self.h)
+        self.ncol = len(json.loads(program_json)["columns"])
         self._keep = []
 
     def push(self, ts, key, stream, cols, nulls, clock=None, seq=None):
         L = lib()
         n = len(ts)
+        if len(cols) != self.ncol or len(nulls) != self.ncol:  # the C side reads one pointer per column
+            raise ValueError(f"the program has {self.ncol} columns; got {len(cols)} columns, {len(nulls)} null arrays")
         ts = np.ascontiguousarray(ts, np.int64)
         key = np.ascontiguousarray(key, np.int32)
         stream = np.ascontiguousarray(stream, np.int32)

@@ -98,6 +98,7 @@ __global__ void k_clamp_clock(int64_t* rmax, int64_t n, int64_t clock0) {
 #define SHP_LANES_ATTR
 #endif
 
+template <int T>
 __global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes(const DevProg* __restrict__ Pp, LaneLayout Y, char* arena,
                                                   BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
                                                   const uint32_t* __restrict__ kbeg,
@@ -105,8 +106,8 @@ __global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes(const DevProg* 
   int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nlanes) return;
   const DevProg& P = *Pp;
-  LaneT<1> ln(P, Y, arena, k, k, B, O);
-  if (!B.partitioned && !ln.at<uint8_t>(Y.o_kinit, 0)) {
+  LaneT<1, T> ln(P, Y, arena, k, k, B, O);
+  if (!B.partitioned && !ln.template at<uint8_t>(Y.o_kinit, 0)) {
     ln.clock = B.init_clock;
     ln.emit_pos = B.seq0;
     ln.init_partition();
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes(const DevProg* 
   }
   ln.flush_ret();
   if (ln.err) {
-    ln.at<int32_t>(Y.o_err, 0) |= ln.err;
+    ln.template at<int32_t>(Y.o_err, 0) |= ln.err;
     atomicOr(err, ln.err);
   }
 }
@@ -149,10 +150,44 @@ __device__ inline void lane_copy(const LaneLayout& Yd, char* dst, int64_t ld, co
   }
 }
 
+// Capacity growth: the committed arena of layout Ys (tier t) into layout Yd (tier >= t), every
+// lane.  Fields keep their order and element sizes across tiers; element indices that embed a
+// capacity are re-indexed: list items ((which * MAXP + p) * LCAP + i) and the timer rings
+// (s * QCAP + (head + i) % QCAP, linearised so the new head is 0).  The new arena is zeroed first
+// (free pool bits, empty lists).
+__global__ __launch_bounds__(256) void k_lane_migrate(LaneLayout Yd, char* dst, LaneLayout Ys, const char* src) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= Ys.L) return;
+  auto sp = [&](int64_t off, int64_t i, int sz) { return src + off + (i * Ys.L + l) * sz; };
+  auto dp = [&](int64_t off, int64_t i, int sz) { return dst + off + (i * Yd.L + l) * sz; };
+  auto cp = [&](char* d, const char* s_, int sz) {
+    for (int b = 0; b < sz; b++) d[b] = s_[b];
+  };
+  for (int f = 0; f < Ys.nf; f++) {
+    const int64_t so = Ys.f_off[f], d_o = Yd.f_off[f];
+    const int sz = Ys.f_sz[f];
+    if (so == Ys.o_lst) {
+      for (int li = 0; li < 2 * MAXP; li++)
+        for (int i = 0; i < Ys.lcap; i++) cp(dp(d_o, (int64_t)li * Yd.lcap + i, sz), sp(so, (int64_t)li * Ys.lcap + i, sz), sz);
+    } else if (so == Ys.o_q) {
+      for (int q = 0; q < MAXQ; q++) {
+        const int16_t h = *(const int16_t*)sp(Ys.o_qhead, q, 2), n = *(const int16_t*)sp(Ys.o_qlen, q, 2);
+        for (int i = 0; i < n; i++)
+          cp(dp(d_o, (int64_t)q * Yd.qcap + i, sz), sp(so, (int64_t)q * Ys.qcap + (h + i) % Ys.qcap, sz), sz);
+      }
+    } else if (so == Ys.o_qhead) {
+      for (int q = 0; q < MAXQ; q++) *(int16_t*)dp(d_o, q, 2) = 0;
+    } else {
+      for (int i = 0; i < Ys.f_elems[f]; i++) cp(dp(d_o, i, sz), sp(so, i, sz), sz);
+    }
+  }
+}
+
 // Few keys: the lanes' state lives in LDS for the batch (copied in and out of the HBM arena),
 // so the per-event chain of dependent state accesses runs at LDS latency instead of HBM
 // latency.  Same Lane code, one lane per thread, blockDim lanes per workgroup.
-__global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes_lds(const DevProg* __restrict__ Pp, LaneLayout Y, char* arena, LaneLayout Yl,
+__global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes_lds(const DevProg* __restrict__ Pp, LaneLayout Y,
+                                const char* arena, char* arena_out, LaneLayout Yl,
                                 BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
                                 const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt, int32_t nlanes,
                                 int* err) {
@@ -160,7 +195,7 @@ __global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes_lds(const DevPr
   const int32_t t = threadIdx.x;
   const int32_t k = blockIdx.x * blockDim.x + t;
   if (k >= nlanes) return;
-  lane_copy(Yl, lds, t, Y, arena, k);
+  lane_copy(Yl, lds, t, Y, (char*)arena, k);
   const DevProg& P = *Pp;
   LaneT<3> ln(P, Yl, lds, t, k, B, O);
   if (!B.partitioned && !ln.at<uint8_t>(Yl.o_kinit, 0)) {
@@ -186,7 +221,7 @@ __global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes_lds(const DevPr
     ln.at<int32_t>(Yl.o_err, 0) |= ln.err;
     atomicOr(err, ln.err);
   }
-  lane_copy(Y, arena, k, Yl, lds, t);
+  lane_copy(Y, arena_out, k, Yl, lds, t);
 }
 
 // ---------------------------------------------------------------- engine
@@ -199,7 +234,11 @@ struct shp_engine {
   DevProg* dprog = nullptr;
   shp_config cfg{};
   LaneLayout Y{};
+  // general lanes: the committed arena and the one a push writes (the committed state copied in
+  // first); the push swaps them only when it succeeded
   char* arena = nullptr;
+  char* arena2 = nullptr;
+  int tier = 0;  // LaneCaps tier of Y
   int fast = 0;   // 1: specialised scan kernels (fastpath.h), 2: sweep (sweep.h)
   FastState fs{};
   SweepState sw{};
@@ -260,6 +299,7 @@ struct shp_engine {
     };
     F(dprog);
     F(arena);
+    F(arena2);
     F(d_ts);
     F(d_clk);
     F(d_seq);
@@ -413,6 +453,7 @@ struct shp_engine {
         }
       }
       HIP_OK(hipMalloc((void**)&arena, Y.bytes));
+      HIP_OK(hipMalloc((void**)&arena2, Y.bytes));
       HIP_OK(hipMemsetAsync(arena, 0, Y.bytes, stream));
     }
     HIP_OK(hipStreamSynchronize(stream));
@@ -501,11 +542,15 @@ struct shp_engine {
       } else {
         int L = cfg.max_keys;
         kt.mark("nfa_lanes", stream);
-        if (lds_lanes > 0) {
+        if (lds_lanes > 0 && tier == 0) {  // reads the committed arena, writes arena2
           k_nfa_lanes_lds<<<(L + lds_lanes - 1) / lds_lanes, lds_lanes, (size_t)Yl.bytes, stream>>>(
-              dprog, Y, arena, Yl, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+              dprog, Y, arena, arena2, Yl, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
         } else {
-          k_nfa_lanes<<<(L + 63) / 64, 64, 0, stream>>>(dprog, Y, arena, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+          HIP_OK(hipMemcpyAsync(arena2, arena, Y.bytes, hipMemcpyDeviceToDevice, stream));
+          const unsigned gl = (unsigned)((L + 63) / 64);
+          if (tier == 0) k_nfa_lanes<0><<<gl, 64, 0, stream>>>(dprog, Y, arena2, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+          else if (tier == 1) k_nfa_lanes<1><<<gl, 64, 0, stream>>>(dprog, Y, arena2, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+          else k_nfa_lanes<2><<<gl, 64, 0, stream>>>(dprog, Y, arena2, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
         }
         kt.mark(nullptr, stream);
       }
@@ -537,8 +582,14 @@ struct shp_engine {
       if (tsmax != INT64_MIN && tsmax > clock) clock = tsmax;
       if (!clock_only) seq += n;
       if (fast == 2) sw.commit();
+      if (fast == 0) std::swap(arena, arena2);
     } else {
       last_m = 0;
+      // a lane's pools or lists overflowed: re-run the push from the committed state at the next
+      // capacity tier (the reference's lists are unbounded)
+      const int lane_cap = E_SE | E_ND | E_LIST | E_Q;
+      if (fast == 0 && (herr & lane_cap) && !(herr & ~lane_cap) && tier + 1 < LANE_TIERS && grow(tier + 1))
+        return run(n, clock_only, in, staged_clk, staged_seq);
       if (herr & SWE_KEYS) return fail(SHP_ERR_KEYS, "partition key id >= max_keys");
       if (herr & E_OUT) return fail(SHP_ERR_OUTPUT, "match buffer too small for this batch (max_matches)");
       if (herr & SWE_MONO) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state scan kernels");
@@ -551,6 +602,36 @@ struct shp_engine {
     }
     return SHP_OK;
   }
+
+  // the general lanes at capacity tier t: new arenas of layout LaneLayout(max_keys, t); with
+  // migrate, the committed state is carried over (else the caller overwrites it).  False when
+  // the two arenas would not fit in free device memory (the engine is then unchanged).
+  bool set_tier(int t, bool migrate) {
+    LaneLayout Yn{};
+    Yn.build(cfg.max_keys, t);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+    if ((size_t)Yn.bytes * 2 + (256u << 20) > fr + (migrate ? 0 : (size_t)Y.bytes * 2)) return false;
+    HIP_OK(hipStreamSynchronize(stream));
+    char *a = nullptr, *b = nullptr;
+    if (hipMalloc((void**)&a, Yn.bytes) != hipSuccess) return false;
+    if (hipMalloc((void**)&b, Yn.bytes) != hipSuccess) {
+      (void)hipFree(a);
+      return false;
+    }
+    HIP_OK(hipMemsetAsync(a, 0, Yn.bytes, stream));
+    if (migrate) k_lane_migrate<<<(unsigned)((Y.L + 255) / 256), 256, 0, stream>>>(Yn, a, Y, arena);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(stream));
+    (void)hipFree(arena);
+    (void)hipFree(arena2);
+    arena = a;
+    arena2 = b;
+    Y = Yn;
+    tier = t;
+    return true;
+  }
+  bool grow(int t) { return set_tier(t, true); }
 
   // ---- snapshot / restore (State.snapshot/restore, core/util/snapshot/state/State.java:25-36):
   // the device buffers that carry per-key state across pushes, for the engine's path
@@ -616,6 +697,7 @@ struct shp_engine {
     h.payload = (int64_t)payload;
     h.program_hash = fnv1a(program);
     h.maybe_null = fast == 2 ? sw.D.maybe_null : 0;
+    h.pad = fast == 0 ? tier : 0;  // lanes: capacity tier of the arena
     memcpy(snap.data(), &h, sizeof h);
     char* q = snap.data() + sizeof h;
     for (auto& x : secs) {
@@ -636,6 +718,13 @@ struct shp_engine {
     if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 2) return fail(SHP_ERR_ARG, "not a snapshot (or of another version)");
     if (h.path != fast || h.max_keys != cfg.max_keys || h.program_hash != fnv1a(program))
       return fail(SHP_ERR_ARG, "snapshot is of a different query, path or key capacity");
+    if (fast == 0 && (h.pad < 0 || h.pad >= LANE_TIERS)) return fail(SHP_ERR_ARG, "snapshot capacity tier unknown");
+    if (fast == 0 && h.pad != tier) {  // the arena layout of the snapshot's tier (contents copied below)
+      LaneLayout Yn{};
+      Yn.build(cfg.max_keys, h.pad);
+      if (sizeof h + 8 + (size_t)Yn.bytes != len) return fail(SHP_ERR_ARG, "snapshot layout mismatch");
+      if (!set_tier(h.pad, false)) return fail(SHP_ERR_CAPACITY, "no device memory for the snapshot's capacity tier");
+    }
     auto secs = state_sections();
     if ((size_t)h.sections != secs.size() || sizeof h + (size_t)h.payload != len)
       return fail(SHP_ERR_ARG, "snapshot layout mismatch");
@@ -674,7 +763,13 @@ struct shp_engine {
     if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 2 || h.path != fast || h.max_keys != cfg.max_keys ||
         h.program_hash != fnv1a(program))
       throw std::runtime_error("not a snapshot of this engine's query, path and key capacity");
+    LaneLayout Yb = Y;  // lanes: the layout of the snapshot's capacity tier
+    if (fast == 0) {
+      if (h.pad < 0 || h.pad >= LANE_TIERS) throw std::runtime_error("snapshot capacity tier unknown");
+      Yb.build(cfg.max_keys, h.pad);
+    }
     auto secs = state_sections();
+    if (fast == 0) secs[0].bytes = (size_t)Yb.bytes;
     std::vector<const char*> sp(secs.size());
     const char* q = (const char*)buf + sizeof h;
     for (size_t i = 0; i < secs.size(); i++) {
@@ -692,6 +787,10 @@ struct shp_engine {
     jnum(o, h.seq);
     o += ",\"clock\":";
     jnum(o, h.clock);
+    if (fast == 0) {  // general lanes: the capacity tier of the pools and lists (LaneCaps)
+      o += ",\"tier\":";
+      jnum(o, h.pad);
+    }
     o += "},\"keys\":{";
     bool firstKey = true;
     auto ev = [&](std::string& s, int64_t seqv, int64_t tsv) {
@@ -769,30 +868,30 @@ struct shp_engine {
       // general lanes: decode each key's arena (lane-interleaved SoA, LaneLayout)
       const char* a = sp[0];
       auto at = [&](int64_t off, int64_t i, int64_t k, int sz) -> const char* {
-        return a + off + (i * Y.L + k) * sz;
+        return a + off + (i * Yb.L + k) * sz;
       };
       auto i16 = [&](int64_t off, int64_t i, int64_t k) { int16_t v; memcpy(&v, at(off, i, k, 2), 2); return v; };
       auto i64 = [&](int64_t off, int64_t i, int64_t k) { int64_t v; memcpy(&v, at(off, i, k, 8), 8); return v; };
       auto u8 = [&](int64_t off, int64_t i, int64_t k) { return *(const uint8_t*)at(off, i, k, 1); };
-      for (int64_t k = 0; k < Y.L; k++) {
-        if (!u8(Y.o_kinit, 0, k)) continue;
+      for (int64_t k = 0; k < Yb.L; k++) {
+        if (!u8(Yb.o_kinit, 0, k)) continue;
         o += firstKey ? "\"" : ",\"";
         firstKey = false;
         jnum(o, k);
         o += "\":{";
         auto partial = [&](std::string& s, int se) {
           s += "{\"ts\":";
-          jnum(s, i64(Y.o_se_ts, se, k));
+          jnum(s, i64(Yb.o_se_ts, se, k));
           s += ",\"type\":\"";
-          s += u8(Y.o_se_type, se, k) ? "EXPIRED" : "CURRENT";
+          s += u8(Yb.o_se_type, se, k) ? "EXPIRED" : "CURRENT";
           s += "\",\"slots\":[";
           for (int st = 0; st < P.nstates; st++) {
             s += st ? ",[" : "[";
             int guard = 0;
-            for (int nd = i16(Y.o_se_slot, (int64_t)se * MAXS + st, k); nd >= 0 && guard < NN;
-                 nd = i16(Y.o_nd_next, nd, k), guard++) {
+            for (int nd = i16(Yb.o_se_slot, (int64_t)se * MAXS + st, k); nd >= 0 && guard < Yb.nn;
+                 nd = i16(Yb.o_nd_next, nd, k), guard++) {
               if (guard) s += ",";
-              ev(s, i64(Y.o_nd_seq, nd, k), i64(Y.o_nd_ts, nd, k));
+              ev(s, i64(Yb.o_nd_seq, nd, k), i64(Yb.o_nd_ts, nd, k));
             }
             s += "]";
           }
@@ -804,14 +903,14 @@ struct shp_engine {
           o += "pre" + std::to_string(p) + "(e" + std::to_string(d.stateId + 1) + ")\":{\"FirstEvent\":null";
           for (int which = 0; which < 2; which++) {
             o += which == 0 ? ",\"PendingStateEventList\":[" : ",\"NewAndEveryStateEventList\":[";
-            const int n = i16(Y.o_lst_len, which * MAXP + p, k);
+            const int n = i16(Yb.o_lst_len, which * MAXP + p, k);
             for (int i = 0; i < n; i++) {
               if (i) o += ",";
-              partial(o, i16(Y.o_lst, (int64_t)(which * MAXP + p) * LCAP + i, k));
+              partial(o, i16(Yb.o_lst, (int64_t)(which * MAXP + p) * Yb.lcap + i, k));
             }
             o += "]";
           }
-          const uint8_t f = u8(Y.o_pflags, p, k);
+          const uint8_t f = u8(Yb.o_pflags, p, k);
           o += ",\"Initialized\":";
           jbool(o, f & F_INIT);
           o += ",\"Started\":";
@@ -826,18 +925,18 @@ struct shp_engine {
             o += ",\"IsActive\":";
             jbool(o, !(f & F_INACTIVE));
             o += ",\"LastScheduledTime\":";
-            jnum(o, i64(Y.o_lsched, p, k));
+            jnum(o, i64(Yb.o_lsched, p, k));
             o += ",\"LastArrivalTime\":";
-            jnum(o, i64(Y.o_larr, p, k));
+            jnum(o, i64(Yb.o_larr, p, k));
           }
           o += "}";
         }
         for (int s = 0; s < P.nsched; s++) {  // Scheduler.SchedulerState: ToNotifyQueue (FIFO)
           o += ",\"scheduler" + std::to_string(s) + "\":{\"ToNotifyQueue\":[";
-          const int hd = i16(Y.o_qhead, s, k), n = i16(Y.o_qlen, s, k);
+          const int hd = i16(Yb.o_qhead, s, k), n = i16(Yb.o_qlen, s, k);
           for (int i = 0; i < n; i++) {
             if (i) o += ",";
-            jnum(o, i64(Y.o_q, (int64_t)s * QCAP + (hd + i) % QCAP, k));
+            jnum(o, i64(Yb.o_q, (int64_t)s * Yb.qcap + (hd + i) % Yb.qcap, k));
           }
           o += "]}";
         }

@@ -9,7 +9,10 @@
 // (every routine names the Java method it follows), with fixed-capacity pools
 // and index-based lists instead of heap objects; aliasing (shared count chains,
 // logical partners sharing one StateEvent) is kept by sharing indices.
-// Overflow of any pool sets the lane's error word; the engine fails the push.
+// Overflow of any pool sets the lane's error word.  The pools come in capacity tiers
+// (LaneCaps<T>): the engine runs every push on a copy of the committed arena, and a push that
+// overflows tier T is re-run from the committed state at tier T + 1 (the arena migrated to the
+// larger layout), as the reference's lists are unbounded (StreamPreStateProcessor.java:437-438).
 #pragma once
 #include <math.h>
 #include <stdint.h>
@@ -18,18 +21,27 @@
 
 namespace shp {
 
-constexpr int NSE = 64;    // StateEvent pool per key
-constexpr int NN = 128;    // StreamEvent node pool per key
-constexpr int LCAP = 32;   // capacity of each pending / new-and-every list
-constexpr int QCAP = 64;   // timer FIFO capacity per scheduler per key
-constexpr int GC_SE_RESERVE = 24;
-constexpr int GC_ND_RESERVE = 48;
+// per-key capacities of tier T (x1, x4, x16)
+template <int T>
+struct LaneCaps {
+  static constexpr int SCALE = T == 0 ? 1 : (T == 1 ? 4 : 16);
+  static constexpr int NSE = 64 * SCALE;   // StateEvent pool per key
+  static constexpr int NN = 128 * SCALE;   // StreamEvent node pool per key
+  static constexpr int LCAP = 32 * SCALE;  // capacity of each pending / new-and-every list
+  static constexpr int QCAP = 64 * SCALE;  // timer FIFO capacity per scheduler per key
+  // the lane collects garbage before an event when fewer are free: one event may allocate a
+  // StateEvent / node per partial on the lists it walks, so the reserves scale with the lists
+  static constexpr int GC_SE_RESERVE = 24 * SCALE;
+  static constexpr int GC_ND_RESERVE = 48 * SCALE;
+};
+constexpr int LANE_TIERS = 3;
 
 enum LaneErr : int32_t { E_SE = 1, E_ND = 2, E_LIST = 4, E_Q = 8, E_OUT = 16, E_REF = 32 };
 enum PFlag : uint8_t { F_CHANGED = 1, F_INIT = 2, F_STARTED = 4, F_SUCCESS = 8, F_SSRESET = 16, F_INACTIVE = 32 };
 
 struct LaneLayout {
   int64_t L;  // lanes (keys) in the arena
+  int32_t tier, nse, nn, lcap, qcap, pad_;  // the capacity tier (LaneCaps) the layout is built for
   int64_t o_se_ts, o_se_slot, o_se_type, o_nd_seq, o_nd_ts, o_nd_val, o_nd_next, o_nd_null;
   int64_t o_se_used, o_nd_used, o_lst_len, o_lst, o_pflags, o_lsched, o_larr, o_ret, o_q, o_qhead, o_qlen;
   int64_t o_kinit, o_err, bytes;
@@ -39,8 +51,14 @@ struct LaneLayout {
   int64_t f_off[24];
   int32_t f_elems[24], f_sz[24];
 
-  void build(int64_t lanes) {
+  void build(int64_t lanes, int t = 0) {
     L = lanes;
+    tier = t;
+    nse = t == 0 ? LaneCaps<0>::NSE : (t == 1 ? LaneCaps<1>::NSE : LaneCaps<2>::NSE);
+    nn = t == 0 ? LaneCaps<0>::NN : (t == 1 ? LaneCaps<1>::NN : LaneCaps<2>::NN);
+    lcap = t == 0 ? LaneCaps<0>::LCAP : (t == 1 ? LaneCaps<1>::LCAP : LaneCaps<2>::LCAP);
+    qcap = t == 0 ? LaneCaps<0>::QCAP : (t == 1 ? LaneCaps<1>::QCAP : LaneCaps<2>::QCAP);
+    const int NSE = nse, NN = nn, LCAP = lcap, QCAP = qcap;
     int64_t o = 0;
     nf = 0;
     auto f = [&](int64_t& off, int64_t elems, int64_t sz) {
@@ -369,8 +387,11 @@ struct LaneAS<3> {
 };
 #endif
 
-template <int AS>
+template <int AS, int TIER = 0>
 struct LaneT {
+  using C = LaneCaps<TIER>;
+  static constexpr int NSE = C::NSE, NN = C::NN, LCAP = C::LCAP, QCAP = C::QCAP;
+  static constexpr int GC_SE_RESERVE = C::GC_SE_RESERVE, GC_ND_RESERVE = C::GC_ND_RESERVE;
   const DevProg& P;
   const LaneLayout& Y;
   char* base;

@@ -6,6 +6,7 @@ the library is missing, and engine creation fails when no HIP device is present.
 from __future__ import annotations
 
 import ctypes
+import json
 import sys
 import os
 
@@ -145,6 +146,27 @@ def matches_to_numpy(mt: ShpMatches):
     }
 
 
+_TYPE_BYTES = {"int": 4, "long": 8, "float": 4, "double": 8, "bool": 1, "string": 4}
+
+
+def _column_bytes(program_json: str):
+    """Element size of each program column (shp_batch.cols holds one pointer per column, in order)."""
+    return [_TYPE_BYTES[c["type"]] for c in json.loads(program_json)["columns"]]
+
+
+def _check_columns(cols, nulls, col_bytes, n):
+    """The C-ABI reads one column pointer (and one null pointer) per program column: a short list
+    would make it read past the caller's pointer array, so refuse it here."""
+    if len(cols) != len(col_bytes) or len(nulls) != len(col_bytes):
+        raise ValueError(f"the program has {len(col_bytes)} columns; got {len(cols)} columns, {len(nulls)} null arrays")
+    for i, (c, b) in enumerate(zip(cols, col_bytes)):
+        if c.itemsize != b or len(c) < n:
+            raise ValueError(f"column {i}: need {n} elements of {b} bytes, got {len(c)} of {c.itemsize}")
+    for i, m in enumerate(nulls):
+        if m is not None and len(m) < n:
+            raise ValueError(f"null array {i}: need {n} elements, got {len(m)}")
+
+
 class HipEngine:
     """One engine per query (libsiddhi_hip.so). Same interface as the test oracle."""
 
@@ -161,6 +183,7 @@ class HipEngine:
             raise ShpError(rc, "shp_engine_create failed (see stderr)")
         self.h = h
         self.S = L.shp_engine_num_states(h)
+        self.col_bytes = _column_bytes(program_json)
         self.max_batch = max_batch
         self.layout = int(match_layout)
         self._pending = None
@@ -187,6 +210,7 @@ class HipEngine:
             s = np.ascontiguousarray(stream[lo:hi], np.int32)
             cs = [np.ascontiguousarray(c[lo:hi]) for c in cols]
             ns = [None if m is None else np.ascontiguousarray(m[lo:hi], np.uint8) for m in nulls]
+            _check_columns(cs, ns, self.col_bytes, hi - lo)
             colp = (ctypes.c_void_p * max(1, len(cs)))(*[c.ctypes.data for c in cs])
             nulp = (ctypes.c_void_p * max(1, len(ns)))(*[0 if m is None else m.ctypes.data for m in ns])
             ck = None if clock is None else np.ascontiguousarray(clock[lo:hi], np.int64)

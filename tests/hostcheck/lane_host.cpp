@@ -27,7 +27,39 @@ struct HC {
   int err = 0;
 };
 
+// the lanes of one push at capacity tier T (LaneCaps), as k_nfa_lanes<T> runs them
+template <int T>
+static int run_lanes(HC* h, const BatchView& B, const MatchOut& O, const std::vector<uint32_t>& kbeg,
+                     const std::vector<uint32_t>& kcnt, const std::vector<uint32_t>& perm, int64_t n) {
+  const DevProg& P = h->comp.P;
+  int err = 0;
+  for (int k = 0; k < h->nk; k++) {
+    LaneT<0, T> ln(P, h->Y, h->arena.data(), k, k, B, O);
+    if (!P.partitioned && !ln.template at<uint8_t>(h->Y.o_kinit, 0)) {
+      ln.clock = h->start; ln.emit_pos = h->seq; ln.init_partition();
+    }
+    int64_t lo = 0;
+    for (uint32_t p = kbeg[k]; p < kbeg[k] + kcnt[k] && !ln.err; p++) {
+      int64_t g = perm[p];
+      ln.maybe_gc(); ln.timers(lo, g); ln.on_event(g); lo = g + 1;
+    }
+    if (!ln.err) { ln.maybe_gc(); ln.timers(lo, n - 1); }
+    ln.flush_ret();
+    err |= ln.err;
+  }
+  return err;
+}
+
 extern "C" {
+
+// capacity tier of the arena (before the first push)
+int hc_set_tier(void* hp, int tier) {
+  HC* h = (HC*)hp;
+  if (tier < 0 || tier >= LANE_TIERS) return -1;
+  h->Y.build(h->nk, tier);
+  h->arena.assign(h->Y.bytes, 0);
+  return 0;
+}
 
 void* hc_create(const char* json, int64_t start_clock, int max_keys) {
   auto* h = new HC();
@@ -72,20 +104,9 @@ int hc_push(void* hp, int64_t n, const int64_t* ts, const int32_t* key, const in
   unsigned long long cnt[2] = {0, 0};
   MatchOut O{cap, cap * 4, cnt, mk.data(), mts.data(), mty.data(), mpos.data(), moff.data(), msl.data(), mrefs.data()};
   int err = 0;
-  for (int k = 0; k < h->nk; k++) {
-    Lane ln(P, h->Y, h->arena.data(), k, k, B, O);
-    if (!P.partitioned && !ln.at<uint8_t>(h->Y.o_kinit, 0)) {
-      ln.clock = h->start; ln.emit_pos = h->seq; ln.init_partition();
-    }
-    int64_t lo = 0;
-    for (uint32_t p = kbeg[k]; p < kbeg[k] + kcnt[k] && !ln.err; p++) {
-      int64_t g = perm[p];
-      ln.maybe_gc(); ln.timers(lo, g); ln.on_event(g); lo = g + 1;
-    }
-    if (!ln.err) { ln.maybe_gc(); ln.timers(lo, n - 1); }
-    ln.flush_ret();
-    err |= ln.err;
-  }
+  if (h->Y.tier == 0) err = run_lanes<0>(h, B, O, kbeg, kcnt, perm, n);
+  else if (h->Y.tier == 1) err = run_lanes<1>(h, B, O, kbeg, kcnt, perm, n);
+  else err = run_lanes<2>(h, B, O, kbeg, kcnt, perm, n);
   if (n) h->clock = rmax[n - 1];
   if (!clock_only) h->seq += n;
   int64_t m = (int64_t)cnt[0];

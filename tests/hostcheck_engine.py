@@ -29,6 +29,7 @@ def lib():
         L.hc_fast.argtypes = [ctypes.c_void_p]
         L.hc_fetch.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 6
         L.hc_destroy.argtypes = [ctypes.c_void_p]
+        L.hc_set_tier.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _L = L
     return _L
 
@@ -38,10 +39,12 @@ def _p(a):
 
 
 class HostCheckEngine:
-    def __init__(self, program_json, start_clock=0, max_keys=256):
+    def __init__(self, program_json, start_clock=0, max_keys=256, tier=0):
         self.h = lib().hc_create(program_json.encode(), int(start_clock), max_keys)
         if not self.h:
             raise ValueError("hc_create failed")
+        if tier and lib().hc_set_tier(self.h, int(tier)) != 0:
+            raise ValueError("bad capacity tier")
         self.S = lib().hc_num_states(self.h)
 
     def _push(self, ts, key, stream, cols, nulls, clock_only=0):
