@@ -104,8 +104,17 @@ __global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes(const DevProg* 
                                                   const uint32_t* __restrict__ kbeg,
                                                   const uint32_t* __restrict__ kcnt, int32_t nlanes, int* err) {
   int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+#ifdef SHP_LANES_PLDS  // A/B: the program in LDS (the lanes' field reads at LDS latency)
+  __shared__ DevProg sP;
+  for (int i = threadIdx.x; i < (int)(sizeof(DevProg) / 4); i += blockDim.x)
+    ((uint32_t*)&sP)[i] = ((const uint32_t*)Pp)[i];
+  __syncthreads();
+  if (k >= nlanes) return;
+  const DevProg& P = sP;
+#else
   if (k >= nlanes) return;
   const DevProg& P = *Pp;
+#endif
   LaneT<1, T> ln(P, Y, arena, k, k, B, O);
   if (!B.partitioned && !ln.template at<uint8_t>(Y.o_kinit, 0)) {
     ln.clock = B.init_clock;
