@@ -36,9 +36,10 @@ BYTES_PER_MATCH = {"pairs32": 8,  # (e2 batch index, e2 seq - e1 seq) as two u32
                    "pairs": 16,  # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
                    "agg": 12,    # (key u32, aggregate f64) per match (SHP_LAYOUT_AGG, C5)
                    "full": 16}
-KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_solve", "sw_expand",
+KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_lean", "sw_solve", "sw_expand",
            "radix_sort", "clock_scan", "key_hist", "key_scan", "sort_keys", "iota", "clamp_clock",
-           "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry", "nfa_lanes")
+           "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry", "nfa_lanes",
+           "cseq")
 WORKLOADS = {
     "1": "C1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec (one key)",
     "2": "C2: partition with (symbol of StockStream) every e1=StockStream[price>20] -> "
@@ -48,7 +49,8 @@ WORKLOADS = {
          "within 10 sec",
     "5": "C5: partition every e1 -> e2[price>e1.price] within 1 sec select symbol, avg(e2.price)",
 }
-PATHS = {2: "sweep (owner partition + LDS sweep)", 1: "scan kernels over a key-sorted batch", 0: "general NFA lanes"}
+PATHS = {2: "sweep (owner partition + LDS sweep)", 1: "scan kernels over a key-sorted batch", 0: "general NFA lanes",
+         3: "count-sequence automaton over a key-sorted batch (cseq)"}
 
 
 def parse():

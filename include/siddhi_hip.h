@@ -51,7 +51,8 @@ typedef struct shp_config {
   int64_t max_matches;     /* match-record capacity per push */
   int64_t start_clock;     /* event-time clock at start() (0 in playback mode) */
   int32_t force_general;   /* 0 auto; 1 general NFA lanes only; 2 no sweep path (scan kernels or
-                              lanes); 3 sweep path whenever the shape allows (any key count) */
+                              lanes); 3 sweep path whenever the shape allows (any key count).
+                              The count-sequence path (3) is taken for its shape unless 1. */
   int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
   int32_t match_layout;    /* SHP_LAYOUT_FULL (0), SHP_LAYOUT_PAIRS (1), SHP_LAYOUT_AGG (2) or
                               SHP_LAYOUT_PAIRS32 (3); PAIRS, PAIRS32 and AGG need the sweep path */
@@ -144,7 +145,10 @@ int shp_restore(shp_engine* e, const void* buf, size_t len);
 int64_t shp_snapshot_describe(shp_engine* e, const void* buf, size_t len, char* out, size_t cap);
 int shp_engine_num_states(const shp_engine* e);
 /* Which kernels the engine runs: 2 = sweep (owner partition + LDS sweep), 1 = specialised 2-state
- * scan kernel, 0 = general NFA lanes. */
+ * scan kernel, 0 = general NFA lanes, 3 = count-sequence automaton (`every e1=S[f1]<1:M>, e2=S[f2]`
+ * with f2 over e2 and e1[last], M <= 8, no within; siddhi_amd/csrc/cseq.h).  A path-3 snapshot
+ * describes each key as {"e1": {"Count": L, "PendingStateEventList": [the chain partial]},
+ * "LastEvent": {seq, ts}}. */
 int shp_engine_path(const shp_engine* e);
 /* ---- Key-sharded multi-GPU (SURVEY.md §8b "Multi-GPU is internal to the engine", §8e) ----
  * A partitioned query's keys are split over `world` engines: key k on rank k % world (the dense
@@ -219,6 +223,11 @@ int shp_host_unregister(void* p);
  * which = "total" | "partition" | "nfa" | a kernel name (needs cfg.profile_kernels), e.g.
  * "radix_sort", "nfa_lanes", "fast_search", "fast_emit". */
 double shp_last_kernel_ms(const shp_engine* e, const char* which);
+/* Engine counters since create: which = "pushes" | "lean_pushes" (sweep pushes run by the
+ * k_sw_lean solve) | "lean_fallbacks" (of those, pushes that
+ * k_sw_lean handed back to the exact k_sw_solve: a ts decrease within a key, a push spanning
+ * more than 2^30 ms, a large carry).  -1 for an unknown name. */
+int64_t shp_engine_stat(const shp_engine* e, const char* which);
 const char* shp_last_error(const shp_engine* e);
 void shp_engine_destroy(shp_engine* e);
 

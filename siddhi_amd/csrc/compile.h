@@ -27,6 +27,7 @@ class ProgramCompiler {
  public:
   DevProg P{};
   FastShape fast{};
+  CseqShape cseq{};
   // select-side aggregate over the matches (SHP_LAYOUT_AGG): 0 none, 1 avg, 2 sum, 3 count, 4 min, 5 max;
   // over the value of state agg_state in predicate column agg_col (count: no argument)
   int agg_fn = 0, agg_state = -1, agg_col = -1;
@@ -100,6 +101,7 @@ class ProgramCompiler {
       }
     }
     detectFast(root);
+    detectCseq(root);
   }
 
  private:
@@ -550,6 +552,41 @@ class ProgramCompiler {
     fast.ok = 1;
     fast.stream = P.pre[0].stream;
     fast.within = P.within;
+  }
+
+  // every var operand of state `st` in the filter has index `idx` (e1[last] in e2's filter)
+  static bool varIndex(const JV& e, int st, int idx) {
+    if (e.t != JV::OBJECT) return true;
+    if (e.get("op").sv == "var") return e.get("state").i() != st || e.get("index").i() == idx;
+    for (const char* k : {"a", "b"})
+      if (!varIndex(e.get(k), st, idx)) return false;
+    return true;
+  }
+
+  // every e1=S[f1]<1:M>, e2=S[f2] (sequence, no within): a per-key automaton over the count of
+  // e1's chain (cseq.h).  f1 reads e1's own value, f2 e2's and e1[last]'s.
+  void detectCseq(const JV& root) {
+    cseq.ok = 0;
+    const JV& t = root.get("tree");
+    if (P.type != SEQUENCE || P.nstates != 2 || P.within >= 0 || P.nsched != 0 || P.playback || P.nstream != 1)
+      return;
+    if (t.get("t").sv != "next") return;
+    const JV& a = t.get("a");
+    const JV& b = t.get("b");
+    if (a.get("t").sv != "every" || b.get("t").sv != "stream" || b.get("state").i() != 1) return;
+    const JV& c = a.get("x");
+    if (c.get("t").sv != "count" || c.get("state").i() != 0 || c.get("min").i() != 1) return;
+    const int64_t mx = c.get("max").i();
+    if (mx < 1 || mx > CSEQ_MAXM) return;
+    if (P.pre[0].stream != P.pre[1].stream || P.ncol > 1) return;
+    const JV& st = root.get("states");
+    const JV& f1 = st[0].get("filter");
+    const JV& f2 = st[1].get("filter");
+    // f1 reads only the arriving event (e1's own value), f2 e1[last] and e2
+    if (!varIndex(f1, 1, 0x7fff) || !varIndex(f1, 0, -1) || !varIndex(f2, 0, -1)) return;
+    if (!fastPred(f1, cseq.f1) || !fastPred(f2, cseq.f2)) return;
+    cseq.M = (int32_t)mx;
+    cseq.ok = 1;
   }
 };
 

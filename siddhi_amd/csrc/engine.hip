@@ -27,6 +27,7 @@
 #include "fastpath.h"
 #include "nfa_lane.h"
 #include "sweep.h"
+#include "cseq.h"
 
 using namespace shp;
 
@@ -248,9 +249,10 @@ struct shp_engine {
   char* arena = nullptr;
   char* arena2 = nullptr;
   int tier = 0;  // LaneCaps tier of Y
-  int fast = 0;   // 1: specialised scan kernels (fastpath.h), 2: sweep (sweep.h)
+  int fast = 0;   // 1: specialised scan kernels (fastpath.h), 2: sweep (sweep.h), 3: count sequence (cseq.h)
   FastState fs{};
   SweepState sw{};
+  CseqState cs{};
   bool expanded = true;  // sweep matches materialised as full records
   BatchView lastB{};
   const int32_t* lastKey = nullptr;
@@ -266,6 +268,7 @@ struct shp_engine {
   int32_t* d_stream = nullptr;
   void* d_cols[MAXCOL] = {};
   uint8_t* d_nulls[MAXCOL] = {};
+  bool staged_null[MAXCOL] = {};  // the last staged (host) push carried a null bitmap for column c
   int64_t* d_rmax = nullptr;
   uint32_t *d_skey = nullptr, *d_skey2 = nullptr, *d_idx = nullptr, *d_perm = nullptr;
   uint32_t *d_kcnt = nullptr, *d_kbeg = nullptr;
@@ -299,6 +302,7 @@ struct shp_engine {
   int lds_lanes = 0;
   double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
   int64_t last_m = 0;
+  int64_t pushes = 0, lean_pushes = 0, lean_fallbacks = 0;  // shp_engine_stat
 
   ~shp_engine() { release(); }
 
@@ -338,6 +342,7 @@ struct shp_engine {
     F(d_magg);
     fs.release();
     sw.release();
+    cs.release();
     kt.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -385,6 +390,7 @@ struct shp_engine {
     if (fast && want_sweep && SweepState::shape_ok(comp.P, comp.fast) &&
         SweepState::build_map(cfg.max_keys, nown, kmap))
       fast = 2;
+    if (!fast && cfg.force_general != 1 && CseqState::shape_ok(comp.P, comp.cseq)) fast = 3;
     if ((cfg.match_layout == SHP_LAYOUT_PAIRS || cfg.match_layout == SHP_LAYOUT_PAIRS32) && fast != 2)
       throw CompileError(-2, "match_layout PAIRS / PAIRS32 needs the sweep path");
     if (cfg.match_layout == SHP_LAYOUT_AGG) {
@@ -448,6 +454,8 @@ struct shp_engine {
 #endif
     } else if (fast == 1) {
       fs.create(comp.P, comp.fast, cfg.max_keys, cap, mcap, stream);
+    } else if (fast == 3) {
+      cs.create(comp.P, comp.cseq, cfg.max_keys, stream);
     } else {
       Y.build(cfg.max_keys);
       // few keys: lanes in LDS, as many per workgroup as fit 64 KB (at most 16)
@@ -486,6 +494,7 @@ struct shp_engine {
       x_stream = d_stream;
     }
     HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));  // counts + error bits
+    pushes++;
     kt.begin_push();
     HIP_OK(hipEventRecord(ev0, stream));
     BatchView B{};
@@ -501,7 +510,7 @@ struct shp_engine {
     B.rmax = d_rmax;
     for (int c = 0; c < P.ncol; c++) {
       B.cols[c] = in ? in->cols[c] : d_cols[c];
-      B.nulls[c] = in ? (in->nulls ? in->nulls[c] : nullptr) : d_nulls[c];
+      B.nulls[c] = in ? (in->nulls ? in->nulls[c] : nullptr) : (staged_null[c] ? d_nulls[c] : nullptr);
     }
     MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs, d_magg};
     int64_t* h_tsmax = reinterpret_cast<int64_t*>(h_status + 3);
@@ -509,6 +518,7 @@ struct shp_engine {
     if (fast == 2) {
       // sweep: no clock scan, no global sort (the engine clock is the running max of ts)
       HIP_OK(hipEventRecord(ev1, stream));
+      if (!clock_only && n > 0 && sw.lean_push_for(B)) lean_pushes++;
       if (!clock_only) sw.run(B, x_key, O, d_err, stream, kt);
       lastB = B;
       lastKey = x_key;
@@ -521,12 +531,14 @@ struct shp_engine {
     } else {
       int gb = (int)std::min<int64_t>((n + 255) / 256, 2048);
       if (gb < 1) gb = 1;
-      // 1. clock
+      // 1. clock (the count-sequence path has no timers: its kernel keeps the push's max ts)
       size_t tb = tmp_bytes;
-      kt.mark("clock_scan", stream);
-      HIP_OK(rocprim::inclusive_scan(d_tmp, tb, B.tclk, d_rmax, (size_t)n, rocprim::maximum<int64_t>(), stream));
-      kt.mark("clamp_clock", stream);
-      k_clamp_clock<<<gb, 256, 0, stream>>>(d_rmax, n, clock);
+      if (fast != 3) {
+        kt.mark("clock_scan", stream);
+        HIP_OK(rocprim::inclusive_scan(d_tmp, tb, B.tclk, d_rmax, (size_t)n, rocprim::maximum<int64_t>(), stream));
+        kt.mark("clamp_clock", stream);
+        k_clamp_clock<<<gb, 256, 0, stream>>>(d_rmax, n, clock);
+      }
       // 2. partition by key (stable)
       HIP_OK(hipMemsetAsync(d_kcnt, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
       kt.mark("key_hist", stream);
@@ -548,6 +560,10 @@ struct shp_engine {
       // 3. NFA
       if (fast == 1) {
         fs.run(P, B, O, d_perm, d_kbeg, d_kcnt, cfg.max_keys, d_tmp, tmp_bytes, d_err, stream, d_skey2, dprog, kt);
+      } else if (fast == 3) {
+        kt.mark("cseq", stream);
+        cs.run(B, O, d_perm, d_kbeg, d_kcnt, d_err, stream);
+        kt.mark(nullptr, stream);
       } else {
         int L = cfg.max_keys;
         kt.mark("nfa_lanes", stream);
@@ -563,7 +579,10 @@ struct shp_engine {
         }
         kt.mark(nullptr, stream);
       }
-      if (n > 0) HIP_OK(hipMemcpyAsync(h_tsmax, d_rmax + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+      if (fast == 3)
+        HIP_OK(hipMemcpyAsync(h_tsmax, cs.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+      else if (n > 0)
+        HIP_OK(hipMemcpyAsync(h_tsmax, d_rmax + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
     }
     HIP_OK(hipEventRecord(ev2, stream));
     HIP_OK(hipGetLastError());
@@ -571,9 +590,22 @@ struct shp_engine {
     HIP_OK(hipStreamSynchronize(stream));
     int herr = 0;
     std::memcpy(&herr, h_status + 2, sizeof(int));
+    if (fast == 2 && (herr & SWE_LEAN) && !(herr & (SWE_KEYS | SWE_RANGE))) {
+      // k_sw_lean handed the push back (a ts decrease within a key, a wide ts span, a large
+      // carry): the exact solve re-runs it over the same partition from the same committed state
+      lean_fallbacks++;
+      HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
+      sw.solve(B, O, d_err, stream, kt);
+      if (cfg.match_layout == SHP_LAYOUT_FULL) sw.expand(B, x_key, O, stream, kt);
+      HIP_OK(hipEventRecord(ev2, stream));
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      std::memcpy(&herr, h_status + 2, sizeof(int));
+    }
     const unsigned long long cnt[2] = {h_status[0], h_status[1]};
     int64_t tsmax = *h_tsmax;
-    if (fast == 2) {  // the sweep's per-push max is kept as ts ^ 2^63 (0: no event)
+    if (fast == 2 || fast == 3) {  // the per-push max is kept as ts ^ 2^63 (0: no event)
       const unsigned long long raw = h_status[3];
       tsmax = raw ? (int64_t)(raw ^ (1ull << 63)) : INT64_MIN;
     }
@@ -591,6 +623,7 @@ struct shp_engine {
       if (tsmax != INT64_MIN && tsmax > clock) clock = tsmax;
       if (!clock_only) seq += n;
       if (fast == 2) sw.commit();
+      if (fast == 3) cs.commit();
       if (fast == 0) std::swap(arena, arena2);
     } else {
       last_m = 0;
@@ -662,6 +695,11 @@ struct shp_engine {
         v.push_back({D.agg_s[c], (size_t)no * SW_LK * 8});
         v.push_back({D.agg_c[c], (size_t)no * SW_LK * 8});
       }
+    } else if (fast == 3) {
+      const CseqDev& C = cs.D;
+      const int c = C.cur;
+      const size_t hm = (size_t)C.M * nk * 8;
+      v = {{C.len[c], (size_t)nk}, {C.prev[c], (size_t)nk * 4}, {C.pnull[c], (size_t)nk}, {C.hseq[c], hm}, {C.hts[c], hm}};
     } else if (fast == 1) {
       const FastDev& F = fs.F;
       v = {{F.c_seq, (size_t)nk * FCC * 8}, {F.c_ts, (size_t)nk * FCC * 8}, {F.c_val, (size_t)nk * FCC * 16},
@@ -809,7 +847,34 @@ struct shp_engine {
       jnum(s, tsv);
       s += "}";
     };
-    if (fast == 2 || fast == 1) {
+    if (fast == 3) {
+      // count sequence: e1's chain is the partial CountPreStateProcessor holds (its e1 slot, the
+      // key's last L events); with L == 0 only the re-armed start partial (no events) is pending
+      const CseqDev& C = cs.D;
+      const uint8_t* len = (const uint8_t*)sp[0];
+      const int64_t* hseq = (const int64_t*)sp[3];
+      const int64_t* hts = (const int64_t*)sp[4];
+      for (int32_t k = 0; k < cfg.max_keys; k++) {
+        const int64_t last = hseq[(int64_t)(C.M - 1) * cfg.max_keys + k];
+        if (last < 0) continue;  // no event of this key yet
+        o += firstKey ? "\"" : ",\"";
+        firstKey = false;
+        jnum(o, k);
+        const int L = len[k];
+        o += "\":{\"e1\":{\"Count\":";
+        jnum(o, L);
+        o += ",\"PendingStateEventList\":[{\"ts\":";
+        jnum(o, L ? hts[(int64_t)(C.M - 1) * cfg.max_keys + k] : -1);
+        o += ",\"slots\":[[";
+        for (int i = C.M - L; i < C.M; i++) {
+          if (i > C.M - L) o += ",";
+          ev(o, hseq[(int64_t)i * cfg.max_keys + k], hts[(int64_t)i * cfg.max_keys + k]);
+        }
+        o += "],[]]}]},\"LastEvent\":";
+        ev(o, last, hts[(int64_t)(C.M - 1) * cfg.max_keys + k]);
+        o += "}";
+      }
+    } else if (fast == 2 || fast == 1) {
       // 2-state `every e1 -> e2 within`: e1's start partial, e2's open candidates (partials
       // holding e1); the key's latest event, when it opened a candidate, left that one (and
       // e1's re-armed partial) on the new-and-every lists
@@ -982,8 +1047,9 @@ struct shp_engine {
     else HIP_OK(hipMemsetAsync(d_stream, 0, n * 4, stream));
     for (int c = 0; c < P.ncol; c++) {
       HIP_OK(hipMemcpyAsync(d_cols[c], in->cols[c], n * colBytes(P.colTag[c]), kind, stream));
-      if (in->nulls && in->nulls[c]) HIP_OK(hipMemcpyAsync(d_nulls[c], in->nulls[c], n, kind, stream));
-      else HIP_OK(hipMemsetAsync(d_nulls[c], 0, n, stream));
+      // a column without nulls is run with no null bitmap (as a device push without one)
+      staged_null[c] = in->nulls && in->nulls[c];
+      if (staged_null[c]) HIP_OK(hipMemcpyAsync(d_nulls[c], in->nulls[c], n, kind, stream));
     }
   }
 
@@ -1233,6 +1299,15 @@ int64_t shp_snapshot_describe(shp_engine* e, const void* blob, size_t len, char*
 
 int shp_engine_num_states(const shp_engine* e) { return e ? e->comp.P.nstates : 0; }
 int shp_engine_path(const shp_engine* e) { return e ? e->fast : -1; }
+
+int64_t shp_engine_stat(const shp_engine* e, const char* which) {
+  if (!e || !which) return -1;
+  const std::string w = which;
+  if (w == "pushes") return e->pushes;
+  if (w == "lean_pushes") return e->lean_pushes;
+  if (w == "lean_fallbacks") return e->lean_fallbacks;
+  return -1;
+}
 
 double shp_last_kernel_ms(const shp_engine* e, const char* which) {
   if (!e) return -1;

@@ -125,4 +125,14 @@ struct FastShape {
   FPred f1, f2;
 };
 
+// Recognised shape for the count-sequence kernel (cseq.h): the sequence
+// `every e1=S[f1]<1:M>, e2=S[f2]`, same stream, no `within`, f1 over e1's own value and f2 over
+// e2's value and e1[last]'s (FPred operands: state 0 = e1[last], state 1 = e2).
+constexpr int CSEQ_MAXM = 8;
+struct CseqShape {
+  int32_t ok;
+  int32_t M;  // max count (1..CSEQ_MAXM)
+  FPred f1, f2;
+};
+
 }  // namespace shp

@@ -161,7 +161,8 @@ struct SweepDev {
   uint8_t* c_null[2];
   uint8_t* lastc[2];     // nown * SW_LK: the key's latest event opened a candidate (it is then the
                          // key's last carried candidate, still on the new-and-every list)
-  unsigned long long* tsmax;  // max of ts over the push, as ts ^ 2^63 (0: no event); reset per push
+  unsigned long long* tsmax;  // [0] max of ts over the push, as ts ^ 2^63 (0: no event); [1] some ts
+                              // lies beyond base +- 2^30 (k_sw_lean does not apply); reset per push
   // SHP_LAYOUT_AGG: selector aggregate over e2's value (1 avg, 2 sum, 3 count, 4 min, 5 max; 0 off), its
   // running per-key state (sum, count as doubles: exact integers to 2^53) and the owner-local
   // key -> partition key map for the output rows
@@ -442,6 +443,7 @@ __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchVie
   const uint8_t* ncol = B.nulls[0];
   const bool vnull = D.vtag == T_NULL, vflt = D.vtag == T_FLOAT;
   int e = 0;
+  bool wide = false;  // some ts beyond base +- 2^30: the lean solve's 32-bit ts do not hold
   int64_t tmax = INT64_MIN;
   for (int64_t r0 = lo; r0 < hi; r0 += SWP_ROUND) {
     for (int b = lane; b < nown; b += 64) wcw[b] = 0;
@@ -479,6 +481,7 @@ __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchVie
         tmax = max(tmax, t);
         const int64_t rel = t - base;
         if (!sw_rel_ok(rel)) e |= SWE_RANGE;
+        wide |= rel >= (1ll << 30) || rel < -(1ll << 30);
         const bool nl = (kk[s] & 0x40000000) != 0;
         double af, ai;
         sw_conv(rec[s].v, vflt, af, ai);
@@ -529,6 +532,7 @@ __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchVie
     __syncthreads();
   }
   if (e) atomicOr(err, e);
+  if (wide) atomicOr(D.tsmax + 1, 1ull);
   // running max of ts (the engine clock after the push)
   for (int d = 32; d > 0; d >>= 1) tmax = max(tmax, (int64_t)__shfl_xor((long long)tmax, d, 64));
   if (lane == 0 && tmax != INT64_MIN) atomicMax(D.tsmax, (unsigned long long)tmax ^ (1ull << 63));
@@ -1441,12 +1445,15 @@ __global__ void k_sw_init(SweepDev D) {
 
 }  // namespace shp
 
+#include "sweep_lean.h"
+
 // ------------------------------------------------------------------ host side
 namespace shp {
 
 struct SweepState {
   SweepDev D{};
   int ct = 0;  // compare type of the probe loop (see SwCand)
+  int lean_opc = 0;  // > 0: k_sw_lean applies to the query (its f2 comparison class)
   int64_t st_len = 65536;
   int32_t nst_max = 1;
   void* tmp = nullptr;
@@ -1672,11 +1679,16 @@ struct SweepState {
       al(D.c_null[c], (int64_t)nown * SWS_CCAP);
       al(D.lastc[c], (int64_t)nown * SW_LK);
     }
-    al(D.tsmax, 1);
+    al(D.tsmax, 2);
     D.cur = 0;
     (void)rocprim::exclusive_scan(nullptr, tmp_bytes, D.cnt, D.off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s);
     if (hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)) != hipSuccess)
       throw std::runtime_error("hipMalloc failed (sweep scan scratch)");
+    // k_sw_lean: one f2 term `e2.v OP B` in the column's own type (float / int32), one of the six
+    // standard comparisons; the pair layouts without nulls are checked per push (run)
+    lean_opc = 0;
+    if (D.f2.n == 1 && (ct == 1 || ct == 2) && !D.f2.t[0].flt && D.vtag != T_NULL && !getenv("SHP_NO_LEAN"))
+      lean_opc = sw_opclass(D.f2.t[0].mask);
     int64_t ninit = std::max<int64_t>(nown, (int64_t)nown * SW_LK);
     k_sw_init<<<(unsigned)((ninit + 255) / 256), 256, 0, s>>>(D);
   }
@@ -1719,7 +1731,7 @@ struct SweepState {
     if (B.n <= 0) return;
     if (B.nulls[0]) D.maybe_null = 1;
     D.nst = (int32_t)((B.n + st_len - 1) / st_len);
-    (void)hipMemsetAsync(D.tsmax, 0, sizeof(unsigned long long), s);
+    (void)hipMemsetAsync(D.tsmax, 0, 2 * sizeof(unsigned long long), s);
     size_t nc = (size_t)D.nown * D.nst + 1;
     kt.mark("sw_count", s);
     k_sw_count<<<D.nst, SW_THREADS, 0, s>>>(D, B, key, err);
@@ -1729,6 +1741,33 @@ struct SweepState {
     kt.mark("sw_scatter", s);
     const size_t lds = (size_t)(SWP_WAVES + 1) * D.nown * 4 + (D.lk_lds ? (size_t)(D.maxkeys + 3) / 4 * 4 : 0);
     k_sw_scatter<<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
+    if (lean_push()) {
+      kt.mark("sw_lean", s);
+      launch_lean(B, O, err, s);
+      kt.mark(nullptr, s);
+    } else {
+      solve(B, O, err, s, kt);
+    }
+  }
+
+  // does this push run k_sw_lean (so SWE_LEAN may come back and ask for solve())?
+  bool lean_push() const { return lean_opc && !D.agg && !D.maybe_null; }
+  bool lean_push_for(const BatchView& B) const { return lean_opc && !D.agg && !D.maybe_null && !B.nulls[0]; }
+
+  void launch_lean(const BatchView& B, const MatchOut& O, int* err, hipStream_t s) {
+#define SL_CASE(c, p) \
+  case c * 8 + p: k_sw_lean<c, p><<<D.nown, SL_THREADS, 0, s>>>(D, B, O, err); break;
+    switch (ct * 8 + lean_opc) {
+      SL_CASE(1, 1) SL_CASE(1, 2) SL_CASE(1, 3) SL_CASE(1, 4) SL_CASE(1, 5) SL_CASE(1, 6)
+      SL_CASE(2, 1) SL_CASE(2, 2) SL_CASE(2, 3) SL_CASE(2, 4) SL_CASE(2, 5) SL_CASE(2, 6)
+      default: break;
+    }
+#undef SL_CASE
+  }
+
+  // the exact solve (k_sw_solve) over the partition the scatter left; also the re-run of a push
+  // k_sw_lean handed back with SWE_LEAN (the per-owner state it read is unchanged)
+  void solve(const BatchView& B, const MatchOut& O, int* err, hipStream_t s, KTimer& kt) {
     kt.mark("sw_solve", s);
     switch ((D.f1.n * 3 + D.f2.n) * 3 + ct) {
 #define SW_CASE(a, b, c) \

@@ -1,0 +1,482 @@
+// siddhi-hip: k_sw_lean, the sweep solve for the common 2-state shape (included by sweep.h).
+//
+// Same semantics and output as k_sw_solve (StreamPreStateProcessor
+// .processAndReturn / expireEvents :326-403): per key, candidate i (e1's filter, evaluated by the
+// scatter) closes at the first later event j of the key with ts_j - ts_i <= W and f2(i, j), and
+// expires at the first later event beyond W; matches per key in (j, i) order.
+//
+// It covers the shape the headline configs use -- one f2 term `e2.v OP e1.v` or `e2.v OP const`
+// over a float or int column compared in its own type, no nulls, pair layouts -- and keeps every
+// quantity of the per-chunk work 32-bit.  Anything outside that (a push whose timestamps leave
+// base +- 2^30 ms, a key whose timestamps decrease, a carry beyond SL_CCAP, a closing event with
+// more than 255 far candidates) raises SWE_LEAN: the engine then re-runs the solve of the same
+// push with k_sw_solve, which is exact for all of them.  The two kernels share the per-owner
+// state in HBM (carry in key order, absolute ts), so either can continue from the other.
+//
+// Structure per chunk of SL_CHUNK records of the owner (512 threads, 3 block barriers):
+//   rank    stable ranks by local key (wave ballots, per-wave counters)          | barrier A
+//   scan    wave 0: key run offsets (carried first), write cursors, and the split
+//           of the sorted positions into 8 wave ranges aligned to key runs         | barrier B
+//   place   records and carried candidates at their sorted positions             | barrier C
+//   then every wave works alone on its range (whole key runs, so nothing crosses waves):
+//   probe   each candidate tests the next SW_P1 events of its key; unresolved ones go to the
+//           wave's worklist (SW_P2 events per round).  A closer records its distance in a
+//           32-bit word of the closing event: bits 0..23 = distance 1..24, bits 24..31 = count
+//           of farther ones.
+//   scan    per lane a contiguous block of positions: closes and still-open candidates, one
+//           wave scan, one global atomic for the wave's output range, one LDS atomic for its
+//           carry slots; open candidates are compacted (key order) as the next carry
+//   emit    a candidate's rank among its closer's candidates is the popcount of the nearer
+//           distance bits, so each match is written straight to its slot.
+#pragma once
+
+namespace shp {
+
+constexpr int SL_THREADS = 512;
+constexpr int SL_WAVES = SL_THREADS / 64;
+constexpr int SL_R = 4;                       // records per thread per chunk
+constexpr int SL_CHUNK = SL_THREADS * SL_R;   // 2048
+constexpr int SL_CCAP = 384;                  // carried candidates per owner (<= SWS_CCAP)
+constexpr int SL_EMAX = SL_CHUNK + SL_CCAP;
+constexpr int SL_PAD = 16;                    // sentinel positions past E (probe reads)
+constexpr int SL_WL = 128;                    // worklist entries per wave
+constexpr int SL_NEAR = 24;                   // closer distances kept as bits
+constexpr int SWE_LEAN = 1 << 26;             // the push needs k_sw_solve (not an error)
+static_assert(SL_CCAP <= SWS_CCAP, "lean carry must fit the HBM carry arrays");
+
+struct SwLeanSmem {
+  int2 tv[SL_EMAX + SL_PAD];         // (ts - chunk base, value) by sorted position; later x = output offset
+  uint32_t ref[SL_EMAX];             // batch index, or carry slot (carried)
+  uint32_t cl[SL_EMAX];              // closers of this position: distance bits | far count << 24
+  uint16_t lkf[SL_EMAX + SL_PAD];    // local key | carried | e1's filter
+  int16_t m[SL_EMAX];                // >= 0 closing position, -1 expired, -2 open, -3 not a candidate
+  uint16_t wc[SL_WAVES][256];        // per-wave rank counters, then write cursors
+  uint32_t binoff[257];              // key run starts (then, at the end, key-order carry offsets)
+  uint16_t fe[256];                  // first event position of a key's run (after its carried)
+  uint32_t ncar[256];                // carried candidates of a key in the current carry buffer
+  uint16_t ckf[2][256];              // index of a key's first entry in carry buffer 0/1
+  uint8_t lastc[256];                // the key's latest event opened a candidate (SweepDev::lastc)
+  int64_t cts[2][SL_CCAP];           // carry: ts - batch base (exact)
+  int64_t cseq[2][SL_CCAP];
+  uint32_t cv[2][SL_CCAP];
+  uint8_t clk[2][SL_CCAP];
+  uint32_t wl[SL_WAVES][SL_WL];      // worklists: position | next probe position << 16
+  int32_t ps[SL_WAVES + 1];          // wave ranges of sorted positions
+  int32_t cn[2];                     // entries in carry buffer 0/1
+  uint32_t wtot[SL_WAVES];
+  int32_t flag;
+};
+
+template <int CT, int OPC, int P>
+__device__ __forceinline__ int sl_probe(const int2* tv, int qb, int end, int32_t a_ts, int32_t W,
+                                        typename SwTy<CT>::T b) {
+  int2 x[P];
+#pragma unroll
+  for (int d = 0; d < P; d++) x[d] = tv[qb + d];
+  int res = -4;
+#pragma unroll
+  for (int d = 0; d < P; d++) {
+    const bool hit = sw_cmp_op<OPC>(0, sw_val<CT>((uint32_t)x[d].y, 0.0, 0.0, false), b);
+    const int r = qb + d >= end ? -2 : (x[d].x - a_ts > W ? -1 : (hit ? qb + d : -4));
+    res = res == -4 ? r : res;
+  }
+  return res;
+}
+
+__device__ __forceinline__ uint32_t sl_closes(uint32_t c) { return (uint32_t)__popc(c & 0xFFFFFFu) + (c >> 24); }
+
+template <int CT, int OPC>
+__global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView B, MatchOut O, int* err) {
+  using T = typename SwTy<CT>::T;
+  __shared__ SwLeanSmem S;
+  const int o = blockIdx.x;
+  const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+  const uint64_t lt = sw_lanemask_lt();
+  const int64_t rb = D.off[(int64_t)o * D.nst], re = D.off[(int64_t)(o + 1) * D.nst];
+  const int rd = D.cur, wr = D.cur ^ 1;
+  if (rb == re) {  // no events for this owner: its state passes through unchanged
+    const int n0 = D.c_n[rd][o];
+    for (int i = tid; i < n0; i += SL_THREADS) {
+      const int64_t c = (int64_t)o * SWS_CCAP + i;
+      D.c_ts[wr][c] = D.c_ts[rd][c];
+      D.c_seq[wr][c] = D.c_seq[rd][c];
+      D.c_v[wr][c] = D.c_v[rd][c];
+      D.c_lk[wr][c] = D.c_lk[rd][c];
+      D.c_null[wr][c] = D.c_null[rd][c];
+    }
+    for (int i = tid; i < SW_LK; i += SL_THREADS) {
+      const int64_t k = (int64_t)o * SW_LK + i;
+      D.lastc[wr][k] = D.lastc[rd][k];
+    }
+    if (tid == 0) D.c_n[wr][o] = n0;
+    return;
+  }
+  const int nc0 = D.c_n[rd][o];
+  // the scatter saw a ts beyond base +- 2^30 (batch-relative ts are 32-bit here), or the carry
+  // is larger than the lean kernel holds
+  if (D.tsmax[1] != 0 || nc0 > SL_CCAP) {
+    if (tid == 0) atomicOr(err, SWE_LEAN);
+    return;
+  }
+  const int64_t base = B.ts[0];
+  const int32_t W = (int32_t)D.within;  // <= SW_TS_SPAN (SweepState::shape_ok)
+  const SwTerm t2 = D.f2.t[0];
+  const bool bconst = t2.bk == 0;
+  const T bc = (T)t2.bc;
+  const int lkbits = D.lk_bits;
+  const int nb = lkbits >= 8 ? SW_LK : (1 << lkbits);  // local keys 0..nb-1
+  int e = 0;
+  for (int i = tid; i < 256; i += SL_THREADS) {
+    S.ncar[i] = 0;
+    S.ckf[0][i] = 0;
+    S.lastc[i] = i < SW_LK ? D.lastc[rd][(int64_t)o * SW_LK + i] : 0;
+  }
+  for (int i = tid; i < SL_WAVES * 256; i += SL_THREADS) (&S.wc[0][0])[i] = 0;
+  if (tid == 0) {
+    S.flag = 0;
+    S.cn[0] = nc0;
+    S.cn[1] = 0;
+  }
+  __syncthreads();
+  // carry from the previous push (key order): counts and first index per key
+  for (int x = tid; x < nc0; x += SL_THREADS) {
+    const int64_t c = (int64_t)o * SWS_CCAP + x;
+    const uint32_t lk = D.c_lk[rd][c];
+    S.cts[0][x] = D.c_ts[rd][c] - base;
+    S.cv[0][x] = D.c_v[rd][c];
+    S.cseq[0][x] = D.c_seq[rd][c];
+    S.clk[0][x] = (uint8_t)lk;
+    atomicAdd(&S.ncar[lk], 1u);
+    if (x == 0 || D.c_lk[rd][c - 1] != lk) S.ckf[0][lk] = (uint16_t)x;
+  }
+  int cur = 0;
+  SwRec pf[SL_R];
+#pragma unroll
+  for (int s = 0; s < SL_R; s++) {
+    const int jj = (int)w * (64 * SL_R) + s * 64 + (int)lane;
+    if (rb + jj < re) pf[s] = D.recs[rb + jj];
+  }
+  uint64_t tbk = D.recs[rb].kt;
+  __syncthreads();
+  for (int64_t cb = rb; cb < re; cb += SL_CHUNK) {
+    const int nchunk = (int)min((int64_t)SL_CHUNK, re - cb);
+    const int nx = cur ^ 1;
+    const int32_t tb32 = (int32_t)(uint32_t)tbk;  // chunk base, batch-relative (|.| < 2^30)
+    // 1. rank by local key (stable: wave-major, then slot, then lane = arrival order)
+    uint32_t rk[SL_R], bin[SL_R];
+#pragma unroll
+    for (int s = 0; s < SL_R; s++) {
+      const int j = (int)w * (64 * SL_R) + s * 64 + (int)lane;
+      const bool valid = j < nchunk;
+      const uint32_t lk = valid ? (uint32_t)(pf[s].kt >> 56) : 0u;
+      const uint64_t peers = sw_match_peers(lk, lkbits, valid);
+      bin[s] = valid ? lk : 0xFFFFu;
+      rk[s] = 0;
+      if (valid) {
+        const uint32_t before = S.wc[w][lk];
+        rk[s] = before + (uint32_t)__popcll(peers & lt);
+        if ((peers & lt) == 0) S.wc[w][lk] = (uint16_t)(before + (uint32_t)__popcll(peers));
+      }
+    }
+    __syncthreads();  // A
+    // flags raised by the previous chunk are read here, where no thread writes S.flag (all
+    // threads take the same branch)
+    if (S.flag) break;
+    const int E = S.cn[cur] + nchunk;
+    // 2. key run offsets and the wave split (wave 0)
+    if (w == 0) {
+      uint32_t run = 0;
+      int32_t psv[SL_WAVES];
+#pragma unroll
+      for (int k = 0; k < SL_WAVES; k++) psv[k] = -1;
+      for (int b0 = 0; b0 < nb; b0 += 64) {
+        const int b = b0 + (int)lane;
+        const bool v = b < nb;
+        uint32_t c[SL_WAVES], t = 0;
+#pragma unroll
+        for (int ww = 0; ww < SL_WAVES; ww++) {
+          c[ww] = v ? S.wc[ww][b] : 0u;
+          t += c[ww];
+        }
+        const uint32_t nk = v ? S.ncar[b] : 0u;
+        t += nk;
+        uint32_t x = t;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(x, d, 64);
+          if (lane >= (uint32_t)d) x += y;
+        }
+        const uint32_t pre = run + x - t;
+        if (v) {
+          S.binoff[b] = pre;
+          S.fe[b] = (uint16_t)(pre + nk);
+          uint32_t g = pre + nk;
+#pragma unroll
+          for (int ww = 0; ww < SL_WAVES; ww++) {
+            S.wc[ww][b] = (uint16_t)g;
+            g += c[ww];
+          }
+        }
+        // wave k starts at the first key run that starts at or after k * E / 8
+#pragma unroll
+        for (int k = 1; k < SL_WAVES; k++) {
+          const uint64_t mk = __ballot(v && (int64_t)pre * SL_WAVES >= (int64_t)k * E);
+          if (mk && psv[k] < 0) psv[k] = __builtin_amdgcn_readlane((int)pre, __ffsll((unsigned long long)mk) - 1);
+        }
+        run += __shfl(x, 63, 64);
+      }
+      if (lane == 0) {
+        S.binoff[nb] = run;  // = E
+        S.ps[0] = 0;
+        S.ps[SL_WAVES] = E;
+      }
+      if (lane > 0 && lane < (uint32_t)SL_WAVES) {
+        int32_t pv = -1;
+#pragma unroll
+        for (int k = 1; k < SL_WAVES; k++) pv = (uint32_t)k == lane ? psv[k] : pv;
+        S.ps[lane] = pv < 0 ? E : pv;
+      }
+    }
+    __syncthreads();  // B
+    // 3. place records and carried candidates at their sorted positions
+#pragma unroll
+    for (int s = 0; s < SL_R; s++) {
+      if (bin[s] == 0xFFFFu) continue;
+      const uint32_t p = S.wc[w][bin[s]] + rk[s];
+      const int32_t rel = (int32_t)(uint32_t)pf[s].kt - tb32;
+      if (rel > (int32_t)SW_TS_SPAN || rel < -(int32_t)SW_TS_SPAN) S.flag = 1;
+      S.tv[p] = make_int2(rel, (int32_t)pf[s].v);
+      S.lkf[p] = (uint16_t)(bin[s] | ((pf[s].kt & SW_F1) ? SW_LKF_F1 : 0u));
+      S.ref[p] = pf[s].ref;
+    }
+    {
+      const int ncur = S.cn[cur];
+      for (int x = tid; x < ncur; x += SL_THREADS) {
+        const uint32_t lk = S.clk[cur][x];
+        const uint32_t p = S.binoff[lk] + (uint32_t)x - S.ckf[cur][lk];
+        const int64_t r = S.cts[cur][x] - (int64_t)tb32;
+        if (r > SW_TS_SPAN) S.flag = 1;  // later than the chunk's span: the exact kernel
+        const int32_t crel = r < (int64_t)SW_TS_FLOOR ? SW_TS_FLOOR : (int32_t)r;
+        S.tv[p] = make_int2(crel, (int32_t)S.cv[cur][x]);
+        S.lkf[p] = (uint16_t)(lk | SW_LKF_CAR);
+        S.ref[p] = (uint32_t)x;
+      }
+    }
+    if (tid < SL_PAD) {
+      S.tv[E + tid] = make_int2(0, 0);
+      S.lkf[E + tid] = (uint16_t)SW_LKF_NONE;
+    }
+    if (tid == 0) S.cn[nx] = 0;
+    {  // prefetch the next chunk while this one is solved
+      const int64_t nbk = cb + SL_CHUNK;
+#pragma unroll
+      for (int s = 0; s < SL_R; s++) {
+        const int jj = (int)w * (64 * SL_R) + s * 64 + (int)lane;
+        if (nbk + jj < re) pf[s] = D.recs[nbk + jj];
+      }
+      if (nbk < re) tbk = D.recs[nbk].kt;
+    }
+    __syncthreads();  // C
+    // ---- from here each wave works alone on its key runs [PS, PE)
+    const int PS = S.ps[w], PE = S.ps[w + 1];
+    for (int b = (int)lane; b < nb; b += 64) S.wc[w][b] = 0;  // this wave's counters, next chunk
+    for (int p = PS + (int)lane; p < PE; p += 64) S.cl[p] = 0;
+    auto record = [&](int p, int res) {
+      S.m[p] = (int16_t)res;
+      if (res >= 0) {
+        const int d = res - p;
+        if (d <= SL_NEAR) {
+          atomicOr(&S.cl[res], 1u << (d - 1));
+        } else {
+          const uint32_t old = atomicAdd(&S.cl[res], 1u << 24);
+          if ((old >> 24) == 255u) S.flag = 1;
+        }
+      }
+    };
+    uint32_t* wl = S.wl[w];
+    // 4. probe: round 1 per position, unresolved candidates to the worklist, drained 8 events a round
+    auto drain = [&](uint32_t nwl) -> uint32_t {
+      uint32_t nn = 0;
+      for (uint32_t b0 = 0; b0 < nwl; b0 += 64) {
+        const uint32_t idx = b0 + lane;
+        int p = 0, res = -3;
+        uint32_t qn = 0;
+        if (idx < nwl) {
+          const uint32_t ent = wl[idx];
+          p = (int)(ent & 0xFFFFu);
+          qn = ent >> 16;
+          const int2 a = S.tv[p];
+          const uint32_t lk = S.lkf[p] & 0xFFu;
+          const int end = (int)S.binoff[lk + 1];
+          const T bv = bconst ? bc : sw_val<CT>((uint32_t)a.y, 0.0, 0.0, false);
+          res = sl_probe<CT, OPC, SW_P2>(S.tv, (int)qn, end, a.x, W, bv);
+          qn += SW_P2;
+          if (res == -4 && (int)qn >= end) res = -2;
+        }
+        const bool unres = res == -4;
+        const uint64_t um = __ballot(unres);
+        if (unres) wl[nn + (uint32_t)__popcll(um & lt)] = (uint32_t)p | (qn << 16);
+        else if (idx < nwl) record(p, res);
+        nn += (uint32_t)__popcll(um);
+      }
+      return nn;
+    };
+    uint32_t nwl = 0;
+    for (int g = PS; g < PE; g += 64) {
+      const int p = g + (int)lane;
+      int res = -3;
+      uint32_t qn = 0;
+      if (p < PE) {
+        const uint32_t f = S.lkf[p];
+        const int2 a = S.tv[p];
+        const uint32_t lk = f & 0xFFu;
+        const int beg = (int)S.binoff[lk], end = (int)S.binoff[lk + 1], fe = (int)S.fe[lk];
+        if (p == beg) S.ncar[lk] = 0;  // recounted by the carry step below
+        if (p == end - 1 && p >= fe) S.lastc[lk] = (f & SW_LKF_F1) ? 1 : 0;
+        if (p > beg && S.tv[p - 1].x > a.x) S.flag = 1;  // ts decrease within the key: exact kernel
+        if (f & (SW_LKF_CAR | SW_LKF_F1)) {
+          const T bv = bconst ? bc : sw_val<CT>((uint32_t)a.y, 0.0, 0.0, false);
+          const int q0 = max(p + 1, fe);
+          res = sl_probe<CT, OPC, SW_P1>(S.tv, q0, end, a.x, W, bv);
+          qn = (uint32_t)(q0 + SW_P1);
+          if (res == -4 && (int)qn >= end) res = -2;
+        }
+      }
+      const bool unres = res == -4;
+      const uint64_t um = __ballot(unres);
+      if (unres) wl[nwl + (uint32_t)__popcll(um & lt)] = (uint32_t)p | (qn << 16);
+      else if (p < PE) record(p, res);
+      nwl += (uint32_t)__popcll(um);
+      if (nwl >= 64) nwl = drain(nwl);
+    }
+    while (nwl > 0) nwl = drain(nwl);
+    // 5. closes and open candidates per position (contiguous block per lane), output range and
+    //    carry slots; open candidates compacted in key order; tv.x becomes the output offset
+    const int nw = PE - PS;
+    const int K = (nw + 63) >> 6;
+    const int lb = PS + (int)lane * K, le = min(lb + K, PE);
+    uint32_t cs = 0, os = 0;
+    for (int q = lb; q < le; q++) {
+      cs += sl_closes(S.cl[q]);
+      os += S.m[q] == -2 ? 1u : 0u;
+    }
+    const uint32_t pk = (cs << 16) | os;
+    uint32_t incl = pk;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    const uint32_t tot = __shfl(incl, 63, 64);
+    const uint32_t ctot = tot >> 16, otot = tot & 0xFFFFu;
+    unsigned long long gb = 0;
+    int cbase = 0;
+    if (lane == 0) {
+      gb = ctot ? atomicAdd(O.count, (unsigned long long)ctot) : 0ull;
+      cbase = otot ? atomicAdd(&S.cn[nx], (int)otot) : 0;
+    }
+    gb = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(gb >> 32), 0, 64) << 32) |
+         (uint32_t)__shfl((int)(uint32_t)gb, 0, 64);
+    cbase = __shfl(cbase, 0, 64);
+    if (gb + ctot > (unsigned long long)O.cap) e |= E_OUT;
+    if (cbase + (int)otot > SL_CCAP) S.flag = 1;
+    {
+      uint32_t co = (incl - pk) >> 16, oo = (incl - pk) & 0xFFFFu;
+      for (int q = lb; q < le; q++) {
+        const uint32_t c = sl_closes(S.cl[q]);
+        if (S.m[q] == -2) {
+          const int x = cbase + (int)oo;
+          if (x < SL_CCAP) {
+            const uint32_t f = S.lkf[q];
+            const uint32_t r = S.ref[q];
+            if (f & SW_LKF_CAR) {
+              S.cts[nx][x] = S.cts[cur][r];
+              S.cv[nx][x] = S.cv[cur][r];
+              S.cseq[nx][x] = S.cseq[cur][r];
+            } else {
+              const int2 a = S.tv[q];
+              S.cts[nx][x] = (int64_t)tb32 + a.x;
+              S.cv[nx][x] = (uint32_t)a.y;
+              S.cseq[nx][x] = bseq(B, r);
+            }
+            S.clk[nx][x] = (uint8_t)(f & 0xFFu);
+          }
+          oo++;
+        }
+        S.tv[q].x = (int32_t)co;
+        co += c;
+      }
+    }
+    {  // per-key first index and count of the new carry entries
+      const int xe = min(cbase + (int)otot, SL_CCAP);
+      for (int x = cbase + (int)lane; x < xe; x += 64) {
+        const uint32_t lk = S.clk[nx][x];
+        if (x == cbase || S.clk[nx][x - 1] != lk) S.ckf[nx][lk] = (uint16_t)x;
+      }
+      for (int x = cbase + (int)lane; x < xe; x += 64) {
+        const uint32_t lk = S.clk[nx][x];
+        if (x + 1 == xe || S.clk[nx][x + 1] != lk) S.ncar[lk] = (uint32_t)(x + 1 - S.ckf[nx][lk]);
+      }
+    }
+    // 6. emit: slot = offset(q) + (closes(q) - 1 - later), later = closers of q nearer than p
+    for (int g = PS; g < PE; g += 64) {
+      const int p = g + (int)lane;
+      if (p >= PE) continue;
+      const int q = S.m[p];
+      if (q < 0) continue;
+      const uint32_t c = S.cl[q];
+      const int d = q - p;
+      uint32_t later;
+      if (d <= SL_NEAR) {
+        later = (uint32_t)__popc(c & ((1u << (d - 1)) - 1u));
+      } else {
+        later = (uint32_t)__popc(c & 0xFFFFFFu);
+        for (int p2 = p + 1; p2 < q - SL_NEAR; p2++) later += S.m[p2] == q ? 1u : 0u;
+      }
+      const uint32_t r = S.ref[p], rq = S.ref[q];
+      const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[cur][r] : bseq(B, r);
+      const int64_t sq = bseq(B, rq);
+      const uint64_t slot = gb + (uint32_t)S.tv[q].x + (sl_closes(c) - 1u - later);
+      if (slot < (uint64_t)O.cap) {
+        if (D.p32) {
+          const int64_t dq = sq - si;
+          if (dq >= (1ll << 32)) e |= SWE_P32;
+          reinterpret_cast<uint2*>(O.refs)[slot] = make_uint2(rq, (uint32_t)dq);
+        } else if (B.seq) {
+          *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, (int64_t)rq);
+        } else {
+          *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
+        }
+      }
+    }
+    cur = nx;
+  }
+  __syncthreads();
+  if (S.flag) {
+    if (tid == 0) atomicOr(err, SWE_LEAN);
+    return;
+  }
+  // write back the carry in key order (k_sw_solve's layout) and the per-key flags (copy wr)
+  {
+    uint32_t total;
+    const uint32_t v = tid < (uint32_t)nb ? S.ncar[tid] : 0u;
+    const uint32_t pre = sw_block_scan_n<SL_WAVES>(v, S.wtot, total);
+    if (tid < (uint32_t)nb) S.binoff[tid] = pre;
+  }
+  __syncthreads();
+  const int ncf = S.cn[cur];
+  for (int x = tid; x < ncf; x += SL_THREADS) {
+    const uint32_t lk = S.clk[cur][x];
+    const int64_t c = (int64_t)o * SWS_CCAP + S.binoff[lk] + (uint32_t)x - S.ckf[cur][lk];
+    D.c_ts[wr][c] = base + S.cts[cur][x];
+    D.c_seq[wr][c] = S.cseq[cur][x];
+    D.c_v[wr][c] = S.cv[cur][x];
+    D.c_lk[wr][c] = (uint8_t)lk;
+    D.c_null[wr][c] = 0;
+  }
+  for (int i = tid; i < SW_LK; i += SL_THREADS) D.lastc[wr][(int64_t)o * SW_LK + i] = S.lastc[i];
+  if (tid == 0) D.c_n[wr][o] = ncf;
+  if (e) atomicOr(err, e);
+}
+
+}  // namespace shp

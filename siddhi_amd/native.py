@@ -23,7 +23,7 @@ SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACIT
               -4: "SHP_ERR_OUTPUT", -5: "SHP_ERR_DEVICE", -6: "SHP_ERR_KEYS"}
 
 SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches",
-           "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms",
+           "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms", "shp_engine_stat",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
            "shp_dev_to_host", "shp_host_alloc", "shp_host_free", "shp_host_register",
            "shp_host_unregister", "shp_snapshot", "shp_restore", "shp_snapshot_describe", "shp_shard_workspace_bytes",
@@ -82,6 +82,8 @@ def lib():
         L.shp_engine_path.argtypes = [ctypes.c_void_p]
         L.shp_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.shp_last_kernel_ms.restype = ctypes.c_double
+        L.shp_engine_stat.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        L.shp_engine_stat.restype = ctypes.c_int64
         L.shp_last_error.argtypes = [ctypes.c_void_p]
         L.shp_last_error.restype = ctypes.c_char_p
         L.shp_engine_destroy.argtypes = [ctypes.c_void_p]
@@ -257,6 +259,10 @@ class HipEngine:
 
     def kernel_ms(self, which="total"):
         return lib().shp_last_kernel_ms(self.h, which.encode())
+
+    def stat(self, which):
+        """shp_engine_stat: "pushes" or "lean_fallbacks"."""
+        return int(lib().shp_engine_stat(self.h, which.encode()))
 
     def close(self):
         if getattr(self, "h", None):

@@ -1,0 +1,162 @@
+"""The count-sequence path (siddhi_amd/csrc/cseq.h): `every e1=S[f1]<1:M>, e2=S[f2]` (C3').
+
+CPU: the per-key automaton cseq.h implements, restated here in Python, against the oracle's
+object-level restatement of CountPreStateProcessor / CountPostStateProcessor /
+StreamPreStateProcessor (oracle/oracle.cpp) -- every M in 1..8, every comparison of
+`e2.v OP e1[last].v`, NaN values, split batches.  This pins the rule the kernel relies on.
+GPU (`-m gpu`): libsiddhi_hip.so's k_cseq against the oracle: C3' at its key counts (including
+1M keys), nulls, int columns, split batches, snapshot/restore, and the general lanes on the same
+stream.
+"""
+import operator
+
+import numpy as np
+import pytest
+
+from diff_util import compare, per_key, program_for, run, small_stream
+from oracle.oracle import OracleEngine
+
+OPS = {"<": operator.lt, "<=": operator.le, ">": operator.gt, ">=": operator.ge, "==": operator.eq,
+       "!=": operator.ne}
+
+
+def _app(M, op, typ="float", f1="v > 20"):
+    return (f"define stream S (k string, v {typ}); partition with (k of S) begin @info(name='q') "
+            f"from every e1=S[{f1}]<1:{M}>, e2=S[v {op} e1[last].v] select e1[0].v as a, e2.v as c "
+            f"insert into Out; end;")
+
+
+def _cq(app):
+    from siddhi_amd.query.compiler import compile_app
+    return compile_app(app)[1][0]
+
+
+def _push(eng, ts, key, v, batch, nul=None):
+    st = np.zeros(len(ts), np.int32)
+    for lo in range(0, len(ts), batch):
+        hi = min(len(ts), lo + batch)
+        eng.push(ts[lo:hi], key[lo:hi], st[lo:hi], [v[lo:hi]], [None if nul is None else nul[lo:hi]])
+    return per_key(eng.fetch())
+
+
+def automaton(M, op, ts, key, v, f1=lambda x: x > 20, nul=None):
+    """cseq.h's rule: per key, L = length of e1's chain (the key's last L events)."""
+    cmp = OPS[op]
+    out, chain = {}, {}
+    for i in range(len(ts)):
+        k = int(key[i])
+        c = chain.get(k, [])
+        x = v[i]
+        xn = nul is not None and nul[i]
+        prev_null = bool(c) and nul is not None and nul[c[-1]]
+        f1x = (not xn) and f1(x)
+        if c and not xn and not prev_null and cmp(x, v[c[-1]]):
+            out.setdefault(k, []).append((int(ts[i]), 0, i, (tuple(c), (i,))))
+            chain[k] = [i] if (len(c) == M and f1x) else []
+        elif c and len(c) < M and f1x:
+            chain[k] = c + [i]
+        elif f1x:
+            chain[k] = [i]
+        else:
+            chain[k] = []
+    return out
+
+
+def _stream(rng, n, keys, lo=15, hi=30, nan=0.01):
+    ts = np.cumsum(rng.integers(0, 3, n)).astype(np.int64) + 1000
+    key = rng.integers(0, keys, n).astype(np.int32)
+    v = rng.integers(lo, hi, n).astype(np.float32)
+    v[rng.random(n) < nan] = np.nan
+    return ts, key, v
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("op", list(OPS))
+def test_automaton_matches_oracle(M, op):
+    rng = np.random.default_rng(M * 31 + len(op))
+    ts, key, v = _stream(rng, 12_000, 13)
+    cq = _cq(_app(M, op))
+    want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 4_999)
+    got = automaton(M, op, ts, key, v)
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 200
+
+
+def test_automaton_matches_oracle_c3b_stream():
+    cq = program_for("3b")
+    g = small_stream(3, 150_000, 50)
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g, 33_333))
+    got = automaton(5, "<", g["ts"], g["key"], g["price"].astype(np.float32))
+    assert compare(want, got) is None, compare(want, got)
+
+
+def test_automaton_matches_oracle_with_nulls():
+    rng = np.random.default_rng(9)
+    ts, key, v = _stream(rng, 12_000, 11, nan=0.0)
+    nul = (rng.random(len(ts)) < 0.05).astype(np.uint8)
+    cq = _cq(_app(5, "<"))
+    want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 3_001, nul)
+    got = automaton(5, "<", ts, key, v, nul=nul)
+    assert compare(want, got) is None, compare(want, got)
+
+
+# ---------------------------------------------------------------- GPU (k_cseq)
+
+def _hip(cq, keys, batch, force=0):
+    from siddhi_amd.native import HipEngine
+    return HipEngine(cq.program_json(), 0, max_keys=keys, max_batch=batch, force_general=force)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("keys,n,batch", [(1, 30_000, 7_001), (64, 200_000, 65_537), (20_000, 600_000, 200_003),
+                                          (1_000_000, 3_000_000, 1_000_003)],
+                         ids=["1key", "64keys", "20k", "1M"])
+def test_c3b_cseq_vs_oracle(keys, n, batch):
+    cq = program_for("3b")
+    g = small_stream(3, n, keys)
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    eng = _hip(cq, keys, batch)
+    assert eng.path == 3
+    got = per_key(run(eng, cq, g, batch))
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 1000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,op,typ", [(1, "<", "float"), (2, ">=", "float"), (3, "==", "int"), (5, "!=", "float"),
+                                      (8, "<=", "int"), (5, ">", "int")])
+def test_cseq_shapes_vs_oracle(M, op, typ):
+    rng = np.random.default_rng(M * 7 + len(op))
+    ts, key, v = _stream(rng, 150_000, 300)
+    if typ == "int":
+        v = np.nan_to_num(v, nan=17).astype(np.int32)
+    cq = _cq(_app(M, op, typ))
+    want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 40_009)
+    eng = _hip(cq, 300, 1 << 16)
+    assert eng.path == 3
+    got = _push(eng, ts, key, v, 40_009)
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 100
+
+
+@pytest.mark.gpu
+def test_cseq_nulls_vs_oracle():
+    rng = np.random.default_rng(4)
+    ts, key, v = _stream(rng, 120_000, 500, nan=0.0)
+    nul = (rng.random(len(ts)) < 0.04).astype(np.uint8)
+    cq = _cq(_app(5, "<"))
+    want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 30_011, nul)
+    got = _push(_hip(cq, 500, 1 << 15), ts, key, v, 30_011, nul)
+    assert compare(want, got) is None, compare(want, got)
+
+
+@pytest.mark.gpu
+def test_cseq_equals_general_lanes():
+    """The same pushes through k_cseq and through the general NFA lanes (force_general=1)."""
+    cq = program_for("3b")
+    g = small_stream(3, 300_000, 3_000)
+    a = _hip(cq, 3_000, 1 << 17, force=0)
+    b = _hip(cq, 3_000, 1 << 17, force=1)
+    assert a.path == 3 and b.path == 0
+    ra, rb = per_key(run(a, cq, g, 77_777)), per_key(run(b, cq, g, 77_777))
+    assert compare(ra, rb) is None, compare(ra, rb)

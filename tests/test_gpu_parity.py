@@ -156,9 +156,9 @@ def test_decreasing_ts_on_sweep_matches_oracle():
     assert compare(a, b) is None, compare(a, b)
 
 
-@pytest.mark.parametrize("q,keys,general", [(2, 300, 0), (2, 64, 2), (2, 64, 1), ("3b", 64, 0), (4, 200, 0),
-                                            (5, 300, 0)],
-                         ids=["c2-sweep", "c2-scan", "c2-lanes", "c3b-lanes", "c4-lanes", "c5-sweep"])
+@pytest.mark.parametrize("q,keys,general", [(2, 300, 0), (2, 64, 2), (2, 64, 1), ("3b", 64, 0), ("3b", 64, 1),
+                                            (4, 200, 0), (5, 300, 0)],
+                         ids=["c2-sweep", "c2-scan", "c2-lanes", "c3b-cseq", "c3b-lanes", "c4-lanes", "c5-sweep"])
 def test_snapshot_restore_continues_exactly(q, keys, general):
     """shp_snapshot mid-stream, shp_restore into a fresh engine, continue: the oracle's matches."""
     cq = program_for(q)
