@@ -39,7 +39,7 @@ BYTES_PER_MATCH = {"pairs32": 8,  # (e2 batch index, e2 seq - e1 seq) as two u32
 KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_lean", "sw_solve", "sw_expand",
            "radix_sort", "clock_scan", "key_hist", "key_scan", "sort_keys", "iota", "clamp_clock",
            "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry", "nfa_lanes",
-           "cseq")
+           "cseq", "labs", "labs_pos")
 WORKLOADS = {
     "1": "C1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec (one key)",
     "2": "C2: partition with (symbol of StockStream) every e1=StockStream[price>20] -> "
@@ -50,7 +50,8 @@ WORKLOADS = {
     "5": "C5: partition every e1 -> e2[price>e1.price] within 1 sec select symbol, avg(e2.price)",
 }
 PATHS = {2: "sweep (owner partition + LDS sweep)", 1: "scan kernels over a key-sorted batch", 0: "general NFA lanes",
-         3: "count-sequence automaton over a key-sorted batch (cseq)"}
+         3: "count-sequence automaton over a key-sorted batch (cseq)",
+         4: "logical-absent automaton over a key-sorted batch (labs, opt-in --path labs)"}
 
 
 def parse():
@@ -66,8 +67,9 @@ def parse():
                     help="threads of the key-sharded CPU baseline (default: the box's CPU share, "
                          "OMP_NUM_THREADS, else os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--path", choices=["auto", "general", "scan"], default="auto",
-                    help="auto = sweep path (default); scan = round-1 scan kernels; general = NFA lanes")
+    ap.add_argument("--path", choices=["auto", "general", "scan", "labs"], default="auto",
+                    help="auto = the engine's default path; scan = round-1 scan kernels; general = NFA lanes; "
+                         "labs = the opt-in logical-absent kernel (C4, force_general 4)")
     ap.add_argument("--same-device", action="store_true",
                     help="N>1 rehearsal on a one-GPU box without torchrun: one process, an in-process group of "
                          "--gpus ranks all on cuda:0 (device copies stand in for RCCL)")
@@ -110,7 +112,7 @@ def main():
     K = a.keys if a.keys else spec.keys
     K_local = -(-K // G)  # each rank's engine holds a dense dictionary of the keys it owns
     cap = int(N * 1.08) + 4096 if G > 1 else N
-    force = {"auto": 0, "general": 1, "scan": 2}[a.path]
+    force = {"auto": 0, "general": 1, "scan": 2, "labs": 4}[a.path]
     sweep = force == 0 and _sweep_shape(cq, local, K_local)
     layout = ("agg" if "aggregate" in cq.program else a.pairs_layout) if sweep else "full"
     mlay = {"agg": native.LAYOUT_AGG, "pairs": native.LAYOUT_PAIRS, "pairs32": native.LAYOUT_PAIRS32,

@@ -52,7 +52,10 @@ typedef struct shp_config {
   int64_t start_clock;     /* event-time clock at start() (0 in playback mode) */
   int32_t force_general;   /* 0 auto; 1 general NFA lanes only; 2 no sweep path (scan kernels or
                               lanes); 3 sweep path whenever the shape allows (any key count).
-                              The count-sequence path (3) is taken for its shape unless 1. */
+                              The count-sequence path (3) is taken for its shape unless 1.
+                              4: the logical-absent path for the playback pattern `every (x=X and
+                              y=Y) -> not Z for T [within W]` (labs.h): needs non-decreasing
+                              timestamps per key (a push breaking that fails, engine unchanged). */
   int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
   int32_t match_layout;    /* SHP_LAYOUT_FULL (0), SHP_LAYOUT_PAIRS (1), SHP_LAYOUT_AGG (2) or
                               SHP_LAYOUT_PAIRS32 (3); PAIRS, PAIRS32 and AGG need the sweep path */
@@ -146,7 +149,8 @@ int64_t shp_snapshot_describe(shp_engine* e, const void* buf, size_t len, char* 
 int shp_engine_num_states(const shp_engine* e);
 /* Which kernels the engine runs: 2 = sweep (owner partition + LDS sweep), 1 = specialised 2-state
  * scan kernel, 0 = general NFA lanes, 3 = count-sequence automaton (`every e1=S[f1]<1:M>, e2=S[f2]`
- * with f2 over e2 and e1[last], M <= 8, no within; siddhi_amd/csrc/cseq.h).  A path-3 snapshot
+ * with f2 over e2 and e1[last], M <= 8, no within; siddhi_amd/csrc/cseq.h), 4 = logical-absent
+ * (opt-in, force_general 4; siddhi_amd/csrc/labs.h).  A path-3 snapshot
  * describes each key as {"e1": {"Count": L, "PendingStateEventList": [the chain partial]},
  * "LastEvent": {seq, ts}}. */
 int shp_engine_path(const shp_engine* e);

@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libsiddhi_hip.so")
 SRC = os.path.join(HERE, "csrc")
-DEPS = ["engine.hip", "synth.hip", "shard.hip", "group.hip", "nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h", "sweep.h", "sweep_lean.h", "cseq.h"]
+DEPS = ["engine.hip", "synth.hip", "shard.hip", "group.hip", "nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h", "sweep.h", "sweep_lean.h", "cseq.h", "labs.h"]
 
 
 def _stale(lib: str = LIB) -> bool:

@@ -28,6 +28,7 @@ class ProgramCompiler {
   DevProg P{};
   FastShape fast{};
   CseqShape cseq{};
+  LabsShape labs{};
   // select-side aggregate over the matches (SHP_LAYOUT_AGG): 0 none, 1 avg, 2 sum, 3 count, 4 min, 5 max;
   // over the value of state agg_state in predicate column agg_col (count: no argument)
   int agg_fn = 0, agg_state = -1, agg_col = -1;
@@ -102,6 +103,7 @@ class ProgramCompiler {
     }
     detectFast(root);
     detectCseq(root);
+    detectLabs(root);
   }
 
  private:
@@ -561,6 +563,95 @@ class ProgramCompiler {
     for (const char* k : {"a", "b"})
       if (!varIndex(e.get(k), st, idx)) return false;
     return true;
+  }
+
+  // ---- logical-absent shape (labs.h)
+  bool laOperand(const JV& e, LaOperand& o, int s1, int s2, int s3) {
+    const std::string& op = e.get("op").sv;
+    o = LaOperand{};
+    if (op == "const") {
+      FOperand f;
+      if (!fastOperand(e, f)) return false;
+      o.kind = 0;
+      o.tag = f.tag;
+      o.imm = f.imm;
+      return true;
+    }
+    if (op != "var") return false;
+    const int idx = (int)e.get("index").i(), st = (int)e.get("state").i();
+    if (!(idx == 0 || idx == -1) || !(st == s1 || st == s2 || st == s3)) return false;
+    o.kind = 1;
+    o.state = (int8_t)st;
+    o.col = (int32_t)e.get("col").i();
+    o.tag = P.colTag[o.col];
+    return true;
+  }
+  bool laPred(const JV& f, LaPredS& p, int s1, int s2, int s3) {
+    p = LaPredS{};
+    if (f.t == JV::NIL) return true;
+    auto term = [&](const JV& e, LaTermS& t) {
+      if (e.get("op").sv != "cmp") return false;
+      static const char* names[] = {"gt", "ge", "lt", "le", "eq", "ne"};
+      t = LaTermS{};
+      t.cmp = -1;
+      for (int i = 0; i < 6; i++)
+        if (e.get("cmp").sv == names[i]) t.cmp = (int8_t)i;
+      if (t.cmp < 0 || !laOperand(e.get("a"), t.a, s1, s2, s3) || !laOperand(e.get("b"), t.b, s1, s2, s3)) return false;
+      t.ptype = (int8_t)promote(t.a.tag, t.b.tag);
+      return t.ptype != T_NULL && t.ptype != T_BOOL;
+    };
+    const std::string& op = f.get("op").sv;
+    if (op == "cmp") {
+      p.n = 1;
+      return term(f, p.t[0]);
+    }
+    if (op == "and" || op == "or") {
+      p.n = 2;
+      p.combine = op == "or";
+      return term(f.get("a"), p.t[0]) && term(f.get("b"), p.t[1]);
+    }
+    return false;
+  }
+
+  // every (x=X[fx] and y=Y[fy]) -> not Z[fz] for T [within W], playback, three distinct streams
+  void detectLabs(const JV& root) {
+    labs = LabsShape{};
+    const JV& t = root.get("tree");
+    if (P.type != PATTERN || P.nstates != 3 || !P.playback || P.nsched != 1) return;
+    if (t.get("t").sv != "next") return;
+    const JV& a = t.get("a");
+    const JV& b = t.get("b");
+    if (a.get("t").sv != "every" || b.get("t").sv != "absent") return;
+    const JV& l = a.get("x");
+    if (l.get("t").sv != "logical" || l.get("op").sv != "and") return;
+    if (l.get("s1").get("t").sv != "stream" || l.get("s2").get("t").sv != "stream") return;
+    const int sx = (int)l.get("s1").get("state").i(), sy = (int)l.get("s2").get("state").i();
+    const int sz = (int)b.get("state").i();
+    if (sx == sy || sx == sz || sy == sz || sx < 0 || sy < 0 || sz < 0 || sx > 2 || sy > 2 || sz > 2) return;
+    const JV& st = root.get("states");
+    const int stx = (int)st[sx].get("stream").i(), sty = (int)st[sy].get("stream").i(), stz = (int)st[sz].get("stream").i();
+    if (stx == sty || stx == stz || sty == stz) return;
+    if (st[sz].get("waiting").i() <= 0) return;
+    for (int s : {stx, sty, stz})
+      if (P.streamNcol[s] > 1) return;
+    for (int c = 0; c < P.ncol; c++)
+      if (!(P.colTag[c] == T_INT || P.colTag[c] == T_FLOAT || P.colTag[c] == T_STR)) return;
+    // x's and y's filters read their own event only; z's reads the Z event, x and y
+    if (!laPred(st[sx].get("filter"), labs.fx, sx, sx, sx) || !laPred(st[sy].get("filter"), labs.fy, sy, sy, sy) ||
+        !laPred(st[sz].get("filter"), labs.fz, sx, sy, sz))
+      return;
+    labs.sx = sx;
+    labs.sy = sy;
+    labs.sz = sz;
+    labs.stx = stx;
+    labs.sty = sty;
+    labs.stz = stz;
+    labs.colx = P.streamNcol[stx] ? P.streamCols[stx][0] : -1;
+    labs.coly = P.streamNcol[sty] ? P.streamCols[sty][0] : -1;
+    labs.colz = P.streamNcol[stz] ? P.streamCols[stz][0] : -1;
+    labs.wait = st[sz].get("waiting").i();
+    labs.within = P.within;
+    labs.ok = 1;
   }
 
   // every e1=S[f1]<1:M>, e2=S[f2] (sequence, no within): a per-key automaton over the count of

@@ -15,11 +15,13 @@
 // those processors (oracle/oracle.cpp): tests/test_cseq.py runs both on random streams for every
 // M in 1..8 and every comparison, with NaN and null values, whole and split batches.
 //
-// Kernel: the batch is partitioned by key with the engine's stable radix sort (as for the
+// Kernels: the batch is partitioned by key with the engine's stable radix sort (as for the
 // general lanes); k_cseq runs one thread per key over the key's events in arrival order, with
-// the automaton, the previous value and the last M events' (seq, ts) in registers.  Matches are
-// reserved with one pair of atomics per wave and event step, so each key's records keep their
-// emission order.  Per-key state (L, previous value and null flag, last M seqs and ts) lives in
+// the automaton, the previous value and the last M events' (seq, ts) in registers.  It runs
+// twice: the first pass counts each key's records and refs, an exclusive scan over the keys
+// places them, the second pass writes them (per key contiguous, in emission order) and the
+// state.  One pair of same-address atomics per wave and event step measured 45 ms per 100M
+// events at 1M keys: they serialise.  Per-key state (L, previous value and null flag, last M seqs and ts) lives in
 // HBM, double-buffered: a push reads copy `cur`, writes `cur ^ 1`, and the engine flips `cur`
 // only when the push succeeded.
 #pragma once
@@ -43,9 +45,11 @@ struct CseqDev {
   int64_t* hseq[2];  // M * nk: seq of the key's last M events (slot M-1 = the latest), -1 none
   int64_t* hts[2];   // M * nk: their ts
   unsigned long long* tsmax;  // max ts of the push as ts ^ 2^63 (0: no event)
+  uint32_t *cm, *cr;  // nk: records and refs per key (pass 1), then their exclusive scans
+  uint32_t *om, *orf;
 };
 
-template <int NT1, int NT2>
+template <int NT1, int NT2, bool EMIT>
 __global__ __launch_bounds__(256) void k_cseq(CseqDev C, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
                                               const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                               int* err) {
@@ -81,13 +85,20 @@ __global__ __launch_bounds__(256) void k_cseq(CseqDev C, BatchView B, MatchOut O
   const uint32_t* vcol = (const uint32_t*)B.cols[0];
   const uint8_t* ncol = B.nulls[0];
   const bool vnull = C.vtag == T_NULL, vflt = C.vtag == T_FLOAT;
-  const uint64_t lt = sw_lanemask_lt();
-  uint32_t mx = cnt;
-  for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
   int64_t tmax = INT64_MIN;
   int e = 0;
-  for (uint32_t j = 0; j < mx; j++) {
-    const bool act = j < cnt;
+  uint32_t nm = 0, nr = 0;  // this key's records and refs so far
+  int64_t mi = 0, ri = 0;
+  if (EMIT && live) {
+    mi = C.om[k];
+    ri = C.orf[k];
+    if (k == C.nk - 1) {  // the push's totals
+      O.count[0] = (unsigned long long)(mi + C.cm[k]);
+      O.count[1] = (unsigned long long)(ri + C.cr[k]);
+    }
+  }
+  for (uint32_t j = 0; j < cnt; j++) {
+    const bool act = true;
     bool em = false;
     int nL = 0;
     int64_t tsg = 0, sg = 0;
@@ -109,30 +120,11 @@ __global__ __launch_bounds__(256) void k_cseq(CseqDev C, BatchView B, MatchOut O
       else if (L > 0 && L < M && f1x) nL = L + 1;
       else nL = f1x ? 1 : 0;
     }
-    const uint64_t mm = __ballot(em);
-    if (mm) {  // wave-uniform: reserve this step's records and refs with one pair of atomics
-      const uint32_t nref = em ? (uint32_t)L + 1u : 0u;
-      uint32_t inc = nref;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if (__lane_id() >= (uint32_t)d) inc += y;
-      }
-      const uint32_t rtot = __shfl(inc, 63, 64);
-      const int lead = __ffsll((unsigned long long)mm) - 1;
-      unsigned long long mb = 0, rb = 0;
-      if ((int)__lane_id() == lead) {
-        mb = atomicAdd(&O.count[0], (unsigned long long)__popcll(mm));
-        rb = atomicAdd(&O.count[1], (unsigned long long)rtot);
-      }
-      mb = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mb >> 32), lead, 64) << 32) |
-           (uint32_t)__shfl((int)(uint32_t)mb, lead, 64);
-      rb = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(rb >> 32), lead, 64) << 32) |
-           (uint32_t)__shfl((int)(uint32_t)rb, lead, 64);
-      if (em) {
-        const int64_t mi = (int64_t)mb + __popcll(mm & lt);
-        const int64_t ri = (int64_t)rb + (inc - nref);
-        if (mi >= O.cap || ri + (int64_t)nref > O.refcap) {
+    if (em) {
+      nm++;
+      nr += (uint32_t)L + 1u;
+      if (EMIT) {
+        if (mi >= O.cap || ri + L + 1 > O.refcap) {
           e |= E_OUT;
         } else {
           O.key[mi] = B.partitioned ? k : 0;
@@ -149,6 +141,8 @@ __global__ __launch_bounds__(256) void k_cseq(CseqDev C, BatchView B, MatchOut O
             if (i >= CSEQ_MAXM - L) O.refs[r++] = hs[i];
           O.refs[r] = sg;
         }
+        mi++;
+        ri += L + 1;
       }
     }
     if (act) {
@@ -163,6 +157,13 @@ __global__ __launch_bounds__(256) void k_cseq(CseqDev C, BatchView B, MatchOut O
       pv = x;
       pn = xn;
     }
+  }
+  if (!EMIT) {
+    if (live) {
+      C.cm[k] = nm;
+      C.cr[k] = nr;
+    }
+    return;
   }
   if (live) {
     C.len[wr][k] = (uint8_t)L;
@@ -221,6 +222,10 @@ struct CseqState {
       al(D.hts[c], (int64_t)s.M * max_keys);
     }
     al(D.tsmax, 1);
+    al(D.cm, max_keys);
+    al(D.cr, max_keys);
+    al(D.om, max_keys);
+    al(D.orf, max_keys);
     const int64_t n = (int64_t)s.M * max_keys;
     k_cseq_init<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(D);
   }
@@ -234,18 +239,34 @@ struct CseqState {
     return SweepState::lower(s.f1, vt, a) && SweepState::lower(s.f2, vt, b);
   }
 
-  void run(const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt,
-           int* err, hipStream_t s) {
-    (void)hipMemsetAsync(D.tsmax, 0, sizeof(unsigned long long), s);
+  template <bool EMIT>
+  void pass(const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt,
+            int* err, hipStream_t s) {
     const unsigned g = (unsigned)((D.nk + 255) / 256);
     switch (D.f1.n * 3 + D.f2.n) {
 #define CS_CASE(a, b) \
-  case a * 3 + b: k_cseq<a, b><<<g, 256, 0, s>>>(D, B, O, perm, kbeg, kcnt, err); break;
+  case a * 3 + b: k_cseq<a, b, EMIT><<<g, 256, 0, s>>>(D, B, O, perm, kbeg, kcnt, err); break;
       CS_CASE(0, 0) CS_CASE(0, 1) CS_CASE(0, 2) CS_CASE(1, 0) CS_CASE(1, 1) CS_CASE(1, 2)
       CS_CASE(2, 0) CS_CASE(2, 1) CS_CASE(2, 2)
 #undef CS_CASE
       default: break;
     }
+  }
+
+  // count pass, placement scan over the keys (tmp: rocPRIM scratch of the engine), emit pass
+  void run(const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt,
+           int* err, void* tmp, size_t tmp_bytes, hipStream_t s, KTimer& kt) {
+    (void)hipMemsetAsync(D.tsmax, 0, sizeof(unsigned long long), s);
+    kt.mark("cseq_count", s);
+    pass<false>(B, O, perm, kbeg, kcnt, err, s);
+    kt.mark("cseq_scan", s);
+    size_t tb = tmp_bytes;
+    (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
+    tb = tmp_bytes;
+    (void)rocprim::exclusive_scan(tmp, tb, D.cr, D.orf, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
+    kt.mark("cseq", s);
+    pass<true>(B, O, perm, kbeg, kcnt, err, s);
+    kt.mark(nullptr, s);
   }
 
   void commit() { D.cur ^= 1; }
@@ -256,7 +277,9 @@ struct CseqState {
       for (void* p : ps)
         if (p) (void)hipFree(p);
     }
-    if (D.tsmax) (void)hipFree(D.tsmax);
+    void* qs[] = {D.tsmax, D.cm, D.cr, D.om, D.orf};
+    for (void* p : qs)
+      if (p) (void)hipFree(p);
     D = CseqDev{};
   }
 };

@@ -28,6 +28,7 @@
 #include "nfa_lane.h"
 #include "sweep.h"
 #include "cseq.h"
+#include "labs.h"
 
 using namespace shp;
 
@@ -83,6 +84,47 @@ __global__ void k_sort_keys(const int32_t* key, const int32_t* stream, int64_t n
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = stream[i] < 0 ? nokey : (partitioned ? (uint32_t)key[i] : 0u);
+}
+
+// the same sort key with the key range checked here (paths without k_key_hist): invalid keys
+// sort past every valid one and fail the push
+__global__ void k_sort_keys_chk(const int32_t* key, const int32_t* stream, int64_t n, uint32_t* out, int partitioned,
+                                uint32_t nokey, int* err) {
+  int e = 0;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t k = 0;
+    if (stream[i] < 0) {
+      k = nokey;
+    } else if (partitioned) {
+      const int32_t x = key[i];
+      if (x < 0 || (uint32_t)x >= nokey) {
+        e = 1 << 20;
+        k = nokey;
+      } else {
+        k = (uint32_t)x;
+      }
+    }
+    out[i] = k;
+  }
+  if (e) atomicOr(err, e);
+}
+
+// each key's run in the key-sorted batch: kbeg = its first position, kend = one past its last
+// (both zero for a key without events); one coalesced pass instead of a histogram of global
+// atomics (3.7 ms per 100M events at 1M keys)
+__global__ void k_key_bounds(const uint32_t* __restrict__ sk, int64_t n, uint32_t* kbeg, uint32_t* kend, uint32_t nk) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = sk[i];
+    if (k >= nk) continue;
+    if (i == 0 || sk[i - 1] != k) kbeg[k] = (uint32_t)i;
+    if (i + 1 == n || sk[i + 1] != k) kend[k] = (uint32_t)(i + 1);
+  }
+}
+__global__ void k_key_len(const uint32_t* kbeg, uint32_t* kcnt, int32_t nk) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nk) kcnt[k] -= kbeg[k];
 }
 
 __global__ void k_clamp_clock(int64_t* rmax, int64_t n, int64_t clock0) {
@@ -253,6 +295,7 @@ struct shp_engine {
   FastState fs{};
   SweepState sw{};
   CseqState cs{};
+  LabsState la{};
   bool expanded = true;  // sweep matches materialised as full records
   BatchView lastB{};
   const int32_t* lastKey = nullptr;
@@ -343,6 +386,7 @@ struct shp_engine {
     fs.release();
     sw.release();
     cs.release();
+    la.release();
     kt.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -391,6 +435,12 @@ struct shp_engine {
         SweepState::build_map(cfg.max_keys, nown, kmap))
       fast = 2;
     if (!fast && cfg.force_general != 1 && CseqState::shape_ok(comp.P, comp.cseq)) fast = 3;
+    // the logical-absent kernel is opt-in: it needs per-key ordered timestamps (labs.h)
+    if (!fast && cfg.force_general == 4) {
+      if (!LabsState::shape_ok(comp.P, comp.labs))
+        throw CompileError(-2, "force_general 4: the query is not `every (x=X and y=Y) -> not Z for T` in playback");
+      fast = 4;
+    }
     if ((cfg.match_layout == SHP_LAYOUT_PAIRS || cfg.match_layout == SHP_LAYOUT_PAIRS32) && fast != 2)
       throw CompileError(-2, "match_layout PAIRS / PAIRS32 needs the sweep path");
     if (cfg.match_layout == SHP_LAYOUT_AGG) {
@@ -456,6 +506,8 @@ struct shp_engine {
       fs.create(comp.P, comp.fast, cfg.max_keys, cap, mcap, stream);
     } else if (fast == 3) {
       cs.create(comp.P, comp.cseq, cfg.max_keys, stream);
+    } else if (fast == 4) {
+      la.create(comp.P, comp.labs, cfg.max_keys, mcap, stream);
     } else {
       Y.build(cfg.max_keys);
       // few keys: lanes in LDS, as many per workgroup as fit 64 KB (at most 16)
@@ -524,7 +576,7 @@ struct shp_engine {
       lastKey = x_key;
       expanded = false;
       if (cfg.match_layout == SHP_LAYOUT_FULL) {
-        sw.expand(B, x_key, O, stream, kt);
+        sw.expand(B, x_key, O, stream, kt, -1, d_err);
         expanded = true;
       }
       HIP_OK(hipMemcpyAsync(h_tsmax, sw.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
@@ -541,29 +593,42 @@ struct shp_engine {
       }
       // 2. partition by key (stable)
       HIP_OK(hipMemsetAsync(d_kcnt, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
-      kt.mark("key_hist", stream);
-      k_key_hist<<<gb, 256, cfg.max_keys <= KEY_HIST_LDS ? (size_t)cfg.max_keys * 4 : 0, stream>>>(
-          x_key, x_stream, n, d_kcnt, cfg.max_keys, P.partitioned, d_err);
-      tb = tmp_bytes;
-      kt.mark("key_scan", stream);
-      HIP_OK(rocprim::exclusive_scan(d_tmp, tb, d_kcnt, d_kbeg, 0u, (size_t)cfg.max_keys, rocprim::plus<uint32_t>(),
-                                     stream));
-      kt.mark("sort_keys", stream);
-      k_sort_keys<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_skey, P.partitioned, (uint32_t)cfg.max_keys);
+      const bool bounds = fast != 1;  // key runs from the sorted keys (the scan kernels keep the histogram)
+      if (!bounds) {
+        kt.mark("key_hist", stream);
+        k_key_hist<<<gb, 256, cfg.max_keys <= KEY_HIST_LDS ? (size_t)cfg.max_keys * 4 : 0, stream>>>(
+            x_key, x_stream, n, d_kcnt, cfg.max_keys, P.partitioned, d_err);
+        tb = tmp_bytes;
+        kt.mark("key_scan", stream);
+        HIP_OK(rocprim::exclusive_scan(d_tmp, tb, d_kcnt, d_kbeg, 0u, (size_t)cfg.max_keys, rocprim::plus<uint32_t>(),
+                                       stream));
+        kt.mark("sort_keys", stream);
+        k_sort_keys<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_skey, P.partitioned, (uint32_t)cfg.max_keys);
+      } else {
+        HIP_OK(hipMemsetAsync(d_kbeg, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
+        kt.mark("sort_keys", stream);
+        k_sort_keys_chk<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_skey, P.partitioned, (uint32_t)cfg.max_keys,
+                                                 d_err);
+      }
       kt.mark("iota", stream);
       k_iota<<<gb, 256, 0, stream>>>(d_idx, n);
       tb = tmp_bytes;
       kt.mark("radix_sort", stream);
       HIP_OK(rocprim::radix_sort_pairs(d_tmp, tb, d_skey, d_skey2, d_idx, d_perm, (size_t)n, 0, key_bits + 1, stream));
+      if (bounds) {
+        kt.mark("key_bounds", stream);
+        k_key_bounds<<<gb, 256, 0, stream>>>(d_skey2, n, d_kbeg, d_kcnt, (uint32_t)cfg.max_keys);
+        k_key_len<<<(unsigned)((cfg.max_keys + 255) / 256), 256, 0, stream>>>(d_kbeg, d_kcnt, cfg.max_keys);
+      }
       kt.mark(nullptr, stream);
       HIP_OK(hipEventRecord(ev1, stream));
       // 3. NFA
       if (fast == 1) {
         fs.run(P, B, O, d_perm, d_kbeg, d_kcnt, cfg.max_keys, d_tmp, tmp_bytes, d_err, stream, d_skey2, dprog, kt);
       } else if (fast == 3) {
-        kt.mark("cseq", stream);
-        cs.run(B, O, d_perm, d_kbeg, d_kcnt, d_err, stream);
-        kt.mark(nullptr, stream);
+        cs.run(B, O, d_perm, d_kbeg, d_kcnt, d_err, d_tmp, tmp_bytes, stream, kt);
+      } else if (fast == 4) {
+        la.run(B, O, d_perm, d_kbeg, d_kcnt, d_err, d_tmp, tmp_bytes, stream, kt);
       } else {
         int L = cfg.max_keys;
         kt.mark("nfa_lanes", stream);
@@ -624,6 +689,7 @@ struct shp_engine {
       if (!clock_only) seq += n;
       if (fast == 2) sw.commit();
       if (fast == 3) cs.commit();
+      if (fast == 4) la.commit();
       if (fast == 0) std::swap(arena, arena2);
     } else {
       last_m = 0;
@@ -632,7 +698,13 @@ struct shp_engine {
       const int lane_cap = E_SE | E_ND | E_LIST | E_Q;
       if (fast == 0 && (herr & lane_cap) && !(herr & ~lane_cap) && tier + 1 < LANE_TIERS && grow(tier + 1))
         return run(n, clock_only, in, staged_clk, staged_seq);
+      // a key's ring of pairs waiting on the absent state overflowed: the next capacity tier
+      if (fast == 4 && herr == E_LIST && la.tier + 1 < LA_TIERS && la.set_tier(la.tier + 1, true, stream))
+        return run(n, clock_only, in, staged_clk, staged_seq);
       if (herr & SWE_KEYS) return fail(SHP_ERR_KEYS, "partition key id >= max_keys");
+      if (fast == 4 && (herr & LA_UNORDERED))
+        return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the logical-absent path (force_general 4); "
+                                         "the general lanes (force_general 1) replay such streams");
       if (herr & E_OUT) return fail(SHP_ERR_OUTPUT, "match buffer too small for this batch (max_matches)");
       if (herr & SWE_MONO) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state scan kernels");
       if (herr & SWE_RANGE)
@@ -695,6 +767,9 @@ struct shp_engine {
         v.push_back({D.agg_s[c], (size_t)no * SW_LK * 8});
         v.push_back({D.agg_c[c], (size_t)no * SW_LK * 8});
       }
+    } else if (fast == 4) {
+      const LabsDev& L = la.D;
+      v = {{L.pend[L.cur], (size_t)nk * sizeof(LaPend)}, {L.wq[L.cur], (size_t)nk * L.wcap * sizeof(LaWait)}};
     } else if (fast == 3) {
       const CseqDev& C = cs.D;
       const int c = C.cur;
@@ -744,7 +819,7 @@ struct shp_engine {
     h.payload = (int64_t)payload;
     h.program_hash = fnv1a(program);
     h.maybe_null = fast == 2 ? sw.D.maybe_null : 0;
-    h.pad = fast == 0 ? tier : 0;  // lanes: capacity tier of the arena
+    h.pad = fast == 0 ? tier : (fast == 4 ? la.tier : 0);  // lanes / logical-absent: capacity tier
     memcpy(snap.data(), &h, sizeof h);
     char* q = snap.data() + sizeof h;
     for (auto& x : secs) {
@@ -766,6 +841,13 @@ struct shp_engine {
     if (h.path != fast || h.max_keys != cfg.max_keys || h.program_hash != fnv1a(program))
       return fail(SHP_ERR_ARG, "snapshot is of a different query, path or key capacity");
     if (fast == 0 && (h.pad < 0 || h.pad >= LANE_TIERS)) return fail(SHP_ERR_ARG, "snapshot capacity tier unknown");
+    if (fast == 4 && h.pad != la.tier) {  // the waits rings of the snapshot's tier
+      if (h.pad < 0 || h.pad >= LA_TIERS) return fail(SHP_ERR_ARG, "snapshot capacity tier unknown");
+      const size_t need = sizeof h + 16 + (size_t)cfg.max_keys * sizeof(LaPend) +
+                          (size_t)cfg.max_keys * LA_CAPS[h.pad] * sizeof(LaWait);
+      if (need != len) return fail(SHP_ERR_ARG, "snapshot layout mismatch");
+      if (!la.set_tier(h.pad, false, stream)) return fail(SHP_ERR_CAPACITY, "no device memory for the snapshot's tier");
+    }
     if (fast == 0 && h.pad != tier) {  // the arena layout of the snapshot's tier (contents copied below)
       LaneLayout Yn{};
       Yn.build(cfg.max_keys, h.pad);
@@ -817,6 +899,10 @@ struct shp_engine {
     }
     auto secs = state_sections();
     if (fast == 0) secs[0].bytes = (size_t)Yb.bytes;
+    if (fast == 4) {
+      if (h.pad < 0 || h.pad >= LA_TIERS) throw std::runtime_error("snapshot capacity tier unknown");
+      secs[1].bytes = (size_t)cfg.max_keys * LA_CAPS[h.pad] * sizeof(LaWait);
+    }
     std::vector<const char*> sp(secs.size());
     const char* q = (const char*)buf + sizeof h;
     for (size_t i = 0; i < secs.size(); i++) {
@@ -847,7 +933,38 @@ struct shp_engine {
       jnum(s, tsv);
       s += "}";
     };
-    if (fast == 3) {
+    if (fast == 4) {
+      // logical-absent: the logical partial (x / y slots) and the pairs waiting on the absent state
+      const LaPend* pd = (const LaPend*)sp[0];
+      const LaWait* wq = (const LaWait*)sp[1];
+      const LabsDev& L = la.D;
+      const int64_t wcap = LA_CAPS[h.pad >= 0 && h.pad < LA_TIERS ? h.pad : 0];
+      for (int32_t k = 0; k < cfg.max_keys; k++) {
+        const LaPend& s = pd[k];
+        if (s.last == INT64_MIN) continue;
+        o += firstKey ? "\"" : ",\"";
+        firstKey = false;
+        jnum(o, k);
+        o += "\":{\"logical\":{\"PendingStateEventList\":[{\"slots\":{";
+        o += "\"e" + std::to_string(L.sid[0] + 1) + "\":[";
+        if (s.xseq >= 0) ev(o, s.xseq, s.xts);
+        o += "],\"e" + std::to_string(L.sid[1] + 1) + "\":[";
+        if (s.yseq >= 0) ev(o, s.yseq, s.yts);
+        o += "]}}]},\"absent\":{\"PendingStateEventList\":[";
+        for (int i = 0; i < s.nw; i++) {
+          const LaWait& w = wq[(int64_t)k * wcap + ((s.wh + i) & (wcap - 1))];
+          if (i) o += ",";
+          o += "{\"due\":";
+          jnum(o, w.due);
+          o += ",\"slots\":[";
+          ev(o, w.xseq, w.xts);
+          o += ",";
+          ev(o, w.yseq, w.yts);
+          o += "]}";
+        }
+        o += "]}}";
+      }
+    } else if (fast == 3) {
       // count sequence: e1's chain is the partial CountPreStateProcessor holds (its e1 slot, the
       // key's last L events); with L == 0 only the re-armed start partial (no events) is pending
       const CseqDev& C = cs.D;

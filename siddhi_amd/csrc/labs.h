@@ -1,0 +1,487 @@
+// siddhi-hip: the logical-absent path, the playback pattern
+//   every (x=X[fx] and y=Y[fy]) -> not Z[fz] for T [within W]        
+// over three distinct streams (engine path 4, opt-in: shp_config.force_general = 4).
+//
+// For this shape the LogicalPre/PostStateProcessor pair (LogicalPreStateProcessor.java
+// processAndReturn :128-167, addEveryState :65-84), the AbsentStreamPre/PostStateProcessor
+// (AbsentStreamPreStateProcessor.java addState :80-103, processAndReturn :257-274, the timer
+// process(ComplexEventChunk) :151-227) and the playback Scheduler (Scheduler.java :71-103, 171-209)
+// reduce, per partition key whose timestamps do not decrease, to:
+//   pend    the one logical partial: an x slot and a y slot (StateEvent with e1 / e2);
+//   waits   completed (x, y) pairs waiting on the absent state, in completion order, each due at
+//           completion ts + T.
+// On each event of the key, after the timers the clock reached have fired:
+//   a filled pend slot older than W (|slot ts - ts| > W, StreamPreStateProcessor.expireEvents
+//   :326-361) resets pend (the every re-arms it);
+//   X event with fx: fills x if empty; with y filled the pair completes: waits += (x, y, due), pend
+//   re-arms (LogicalPostStateProcessor.process :59-87 -> addState on the absent state).  Y alike;
+//   Z event: every wait with fz(z, x, y) is dropped (AbsentStreamPostStateProcessor.process :36-56).
+// A wait fires at the first event (any key) whose playback clock reaches its due time: the match
+// (ts = due, per-state slots x, y, -) is emitted if both x and y are within W of due
+// (isExpired at the timer, AbsentStreamPreStateProcessor :198-213).  The rule was derived from and
+// is checked against the oracle's restatement of those processors (tests/test_labs.py, CPU and
+// GPU).  Cross-key ties of the playback scheduler's TreeMultimap (one state per due time) are not
+// modelled, as on the general lanes (parity-unpinned).  A key whose timestamps
+// decrease fails the push with SHP_ERR_UNSUPPORTED (the general lanes, force_general = 1, replay
+// such streams exactly).  The waiting pairs of a key form a ring of wcap entries: 16 in LDS at
+// first, growing to 256 and 4096 in HBM (capacity tiers, as the general lanes have) when a push
+// overflows it; the push then re-runs from the committed state.
+//
+// Kernels: the batch is partitioned by key with the engine's stable radix sort; k_labs runs one
+// thread per key over its events in arrival order (pend in registers, waits in LDS), twice: a
+// count pass, an exclusive scan over the keys, and the pass that writes each key's records
+// contiguously and the state.  Which event fired a timer is fixed afterwards by k_labs_pos: a
+// binary search of the running clock over the events between the key's previous event and the
+// one that reached the due time.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdexcept>
+
+#include "nfa_lane.h"
+#include "prog.h"
+#include "sweep.h"
+
+namespace shp {
+
+constexpr int LA_WCAP = 16;                      // waiting pairs per key held in LDS (tier 0)
+constexpr int LA_TIERS = 3;
+constexpr int32_t LA_CAPS[LA_TIERS] = {16, 256, 4096};
+constexpr int LA_D = 16;  // events loaded ahead per key
+constexpr int LA_UNORDERED = 1 << 27;  // a key's timestamps decrease (this path needs them ordered)
+
+struct LaTermD {
+  int32_t mask;      // outcomes that make the term true: 1 A<B, 2 A==B, 4 A>B, 8 unordered
+  int8_t ak, bk;     // operand: 0 const, 1 x, 2 y, 3 z
+  int8_t aflt, bflt; // int column promoted to float
+  double ac, bc;
+};
+struct LaPredD {
+  int32_t n, combine;
+  LaTermD t[2];
+};
+
+struct __attribute__((aligned(8))) LaWait {
+  int64_t due, xseq, xts, yseq, yts;
+  uint32_t xv, yv;
+  uint32_t fl;  // 1 x null, 2 y null
+  uint32_t pad;
+};
+
+struct LaPend {
+  int64_t xseq, xts, yseq, yts;  // seq -1: slot empty
+  uint32_t xv, yv;
+  uint32_t fl;    // 1 x null, 2 y null
+  int32_t nw;     // waits held
+  int32_t wh;     // ring head of the waits
+  int32_t pad;
+  int64_t last;   // ts of the key's latest event (INT64_MIN: none)
+};
+
+struct LabsDev {
+  LaPredD fx, fy, fz;
+  int8_t tag[3];     // column tags of x, y, z (T_NULL: no column)
+  int8_t pad0;
+  int32_t st[3];     // streams of x, y, z
+  int32_t col[3];    // their columns (-1 none)
+  int32_t sid[3];    // their state ids (slot order of the records)
+  int64_t wait, within;
+  int32_t nk, cur;
+  int32_t wcap, pad1;  // waits ring per key (LA_CAPS[tier])
+  LaPend* pend[2];   // nk
+  LaWait* wq[2];     // nk * wcap
+  LaWait* wtmp;      // nk * wcap: the count pass's working rings (tiers >= 1)
+  int64_t* aux;      // per record of the push: last batch index the timer can have fired at
+  uint32_t *cm, *om; // nk: records per key (count pass), their exclusive scan
+};
+
+__device__ __forceinline__ double la_val(uint32_t v, int8_t tag, bool flt) {
+  if (tag == T_FLOAT) return (double)__uint_as_float(v);
+  const int32_t x = (int32_t)v;
+  return flt ? (double)(float)x : (double)x;
+}
+
+__device__ __forceinline__ bool la_term(const LaTermD& t, const uint32_t* v, const bool* nl, const int8_t* tag) {
+  bool nul = false;
+  double A = t.ac, B = t.bc;
+  if (t.ak) {
+    A = la_val(v[t.ak - 1], tag[t.ak - 1], t.aflt);
+    nul |= nl[t.ak - 1];
+  }
+  if (t.bk) {
+    B = la_val(v[t.bk - 1], tag[t.bk - 1], t.bflt);
+    nul |= nl[t.bk - 1];
+  }
+  const int o3 = (A < B ? 1 : 0) | (A == B ? 2 : 0) | (A > B ? 4 : 0);
+  return !nul && ((o3 | (o3 == 0 ? 8 : 0)) & t.mask) != 0;  // CompareConditionExpressionExecutor
+}
+
+__device__ __forceinline__ bool la_pred(const LaPredD& p, const uint32_t* v, const bool* nl, const int8_t* tag) {
+  if (p.n == 0) return true;
+  const bool a = la_term(p.t[0], v, nl, tag);
+  if (p.n == 1) return a;
+  const bool b = la_term(p.t[1], v, nl, tag);
+  return p.combine ? (a || b) : (a && b);
+}
+
+// HBMQ: the waits ring is worked on in HBM (tiers >= 1: the committed ring is copied to the
+// pass's own ring first); otherwise in LDS (tier 0)
+template <bool EMIT, bool HBMQ>
+__global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
+                                             const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
+                                             int* err) {
+  __shared__ LaWait W[HBMQ ? 1 : 64][HBMQ ? 1 : LA_WCAP];
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const bool live = k < D.nk;
+  const int rd = D.cur, wr = D.cur ^ 1;
+  const int cap = HBMQ ? D.wcap : LA_WCAP;
+  const int msk = cap - 1;
+  LaWait* wq = HBMQ ? (EMIT ? D.wq[wr] : D.wtmp) + (int64_t)(live ? k : 0) * cap : W[lane];
+  LaPend s{};
+  s.xseq = s.yseq = -1;
+  s.last = INT64_MIN;
+  uint32_t beg = 0, cnt = 0;
+  if (live) {
+    s = D.pend[rd][k];
+    for (int i = 0; i < s.nw; i++) {
+      const int r = (s.wh + i) & msk;
+      wq[r] = D.wq[rd][(int64_t)k * cap + r];
+    }
+    beg = kbeg[k];
+    cnt = kcnt[k];
+  }
+  const bool useW = D.within >= 0;
+  int e = 0;
+  int64_t lo = 0;  // first batch index a timer of this key can fire at (after the key's previous event)
+  uint32_t nm = 0;
+  int64_t mi = 0;
+  if (EMIT && live) {
+    mi = D.om[k];
+    if (k == D.nk - 1) {  // the push's totals
+      O.count[0] = (unsigned long long)(mi + D.cm[k]);
+      O.count[1] = 2ull * (unsigned long long)(mi + D.cm[k]);
+    }
+  }
+  // one step per event of the key, plus a final step for the timers the batch's last clock reaches
+  auto step = [&](bool act, int64_t g, int64_t clk, int64_t ts, int stm, const uint32_t* evs, const bool* ens) {
+    const int64_t hi = g;
+    // 1. timers the clock reached (FIFO: due times follow completion order)
+    int nf = 0, ne = 0;
+    while (nf < s.nw && wq[(s.wh + nf) & msk].due <= clk) {
+      const LaWait& w = wq[(s.wh + nf) & msk];
+      if (!useW || (llabs(w.xts - w.due) <= D.within && llabs(w.yts - w.due) <= D.within)) ne++;
+      nf++;
+    }
+    nm += (uint32_t)ne;
+    if (EMIT) {
+      for (int i = 0; i < nf; i++) {
+        const LaWait& w = wq[(s.wh + i) & msk];
+        if (useW && !(llabs(w.xts - w.due) <= D.within && llabs(w.yts - w.due) <= D.within)) continue;
+        if (mi >= O.cap || 2 * mi + 2 > O.refcap) {
+          e |= E_OUT;
+        } else {
+          O.key[mi] = B.partitioned ? k : 0;
+          O.ts[mi] = w.due;  // the timer's time (AbsentStreamPreStateProcessor: ev.ts = currentTime)
+          O.type[mi] = 0;
+          O.pos[mi] = lo;    // k_labs_pos: the event in [lo, aux] whose clock reached the due time
+          D.aux[mi] = hi;
+          O.ref_off[mi] = 2 * mi;
+          int64_t r = 2 * mi;
+          for (int q = 0; q < 3; q++) {
+            const bool isx = q == D.sid[0], isy = q == D.sid[1];
+            O.slot_len[mi * MAXS + q] = (int16_t)((isx || isy) ? 1 : 0);
+            if (isx) O.refs[r++] = w.xseq;
+            if (isy) O.refs[r++] = w.yseq;
+          }
+        }
+        mi++;
+      }
+    }
+    if (nf) {  // drop the fired waits
+      s.wh = (s.wh + nf) & msk;
+      s.nw -= nf;
+    }
+    if (!act) return;
+    // 2. the event
+    if (s.last != INT64_MIN && ts < s.last) e |= LA_UNORDERED;
+    s.last = ts;
+    lo = g + 1;
+    // expireEvents over every pre of the key: a half-filled logical partial older than W re-arms
+    if (useW && ((s.xseq >= 0 && llabs(s.xts - ts) > D.within) || (s.yseq >= 0 && llabs(s.yts - ts) > D.within))) {
+      s.xseq = s.yseq = -1;
+      s.fl = 0;
+    }
+    const int role = stm == D.st[0] ? 0 : (stm == D.st[1] ? 1 : (stm == D.st[2] ? 2 : -1));
+    if (role < 0) return;
+    uint32_t v[3] = {s.xv, s.yv, 0u};
+    bool nl[3] = {(s.fl & 1u) != 0, (s.fl & 2u) != 0, true};
+    const uint32_t ev = evs[role];
+    const bool en = ens[role];
+    if (role < 2) {
+      v[role] = ev;
+      nl[role] = en;
+      if (!la_pred(role == 0 ? D.fx : D.fy, v, nl, D.tag)) return;
+      const int64_t seqg = bseq(B, g);
+      if (role == 0 && s.xseq < 0) {
+        s.xseq = seqg;
+        s.xts = ts;
+        s.xv = ev;
+        s.fl = (s.fl & ~1u) | (en ? 1u : 0u);
+      } else if (role == 1 && s.yseq < 0) {
+        s.yseq = seqg;
+        s.yts = ts;
+        s.yv = ev;
+        s.fl = (s.fl & ~2u) | (en ? 2u : 0u);
+      } else {
+        return;  // the slot is taken: the partial waits for its partner
+      }
+      if (s.xseq >= 0 && s.yseq >= 0) {  // the pair completes: it waits on the absent state
+        if (s.nw >= cap) {
+          e |= E_LIST;
+        } else {
+          LaWait& w = wq[(s.wh + s.nw++) & msk];
+          w.due = ts + D.wait;
+          w.xseq = s.xseq;
+          w.xts = s.xts;
+          w.yseq = s.yseq;
+          w.yts = s.yts;
+          w.xv = s.xv;
+          w.yv = s.yv;
+          w.fl = s.fl;
+        }
+        s.xseq = s.yseq = -1;  // every: a fresh partial
+        s.fl = 0;
+      }
+    } else {  // a Z event drops every waiting pair its filter matches
+      v[2] = ev;
+      nl[2] = en;
+      int o = 0;
+      for (int i = 0; i < s.nw; i++) {
+        const LaWait w = wq[(s.wh + i) & msk];
+        v[0] = w.xv;
+        v[1] = w.yv;
+        nl[0] = (w.fl & 1u) != 0;
+        nl[1] = (w.fl & 2u) != 0;
+        if (!la_pred(D.fz, v, nl, D.tag)) wq[(s.wh + o++) & msk] = w;
+      }
+      s.nw = o;
+    }
+    };
+  // the key's events in blocks of LA_D: every load of a block is issued before the block is
+  // processed (one thread per key leaves the memory system idle: latency, not bandwidth, bounds it)
+  const uint32_t* c0 = D.col[0] >= 0 ? (const uint32_t*)B.cols[D.col[0]] : nullptr;
+  const uint32_t* c1 = D.col[1] >= 0 ? (const uint32_t*)B.cols[D.col[1]] : nullptr;
+  const uint32_t* c2 = D.col[2] >= 0 ? (const uint32_t*)B.cols[D.col[2]] : nullptr;
+  const uint8_t* n0 = D.col[0] >= 0 ? B.nulls[D.col[0]] : nullptr;
+  const uint8_t* n1 = D.col[1] >= 0 ? B.nulls[D.col[1]] : nullptr;
+  const uint8_t* n2 = D.col[2] >= 0 ? B.nulls[D.col[2]] : nullptr;
+  for (uint32_t j0 = 0; live && j0 <= cnt; j0 += LA_D) {
+    int64_t gq[LA_D], cq[LA_D], tq[LA_D];
+    int32_t sq[LA_D];
+    uint32_t vq[LA_D][3];
+    bool nq[LA_D][3];
+#pragma unroll
+    for (int d = 0; d < LA_D; d++) gq[d] = j0 + d < cnt ? (int64_t)perm[beg + j0 + d] : B.n - 1;
+#pragma unroll
+    for (int d = 0; d < LA_D; d++) {
+      const int64_t g = gq[d];
+      const bool ev = j0 + d < cnt, any = j0 + d <= cnt && B.n > 0;
+      cq[d] = any ? B.rmax[g] : INT64_MIN;
+      tq[d] = ev ? B.ts[g] : 0;
+      sq[d] = ev ? (B.stream ? B.stream[g] : 0) : -1;
+      vq[d][0] = ev && c0 ? c0[g] : 0u;
+      vq[d][1] = ev && c1 ? c1[g] : 0u;
+      vq[d][2] = ev && c2 ? c2[g] : 0u;
+      nq[d][0] = !c0 || (n0 && ev && n0[g]);
+      nq[d][1] = !c1 || (n1 && ev && n1[g]);
+      nq[d][2] = !c2 || (n2 && ev && n2[g]);
+    }
+#pragma unroll
+    for (int d = 0; d < LA_D; d++)
+      if (j0 + d <= cnt) step(j0 + d < cnt, gq[d], cq[d], tq[d], sq[d], vq[d], nq[d]);
+  }
+  if (!EMIT) {
+    if (live) D.cm[k] = nm;
+    return;
+  }
+  if (live) {
+    D.pend[wr][k] = s;
+    if (!HBMQ)
+      for (int i = 0; i < s.nw; i++) {
+        const int r = (s.wh + i) & msk;
+        D.wq[wr][(int64_t)k * cap + r] = wq[r];
+      }
+  }
+  if (e) atomicOr(err, e);
+}
+
+// the event that fired each timer record of the push: the first batch index in [pos, aux] whose
+// running clock reaches the record's due time (the playback clock is non-decreasing)
+__global__ void k_labs_pos(LabsDev D, BatchView B, MatchOut O) {
+  const int64_t m = min((int64_t)O.count[0], O.cap);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t a = O.pos[i], b = D.aux[i];
+    const int64_t due = O.ts[i];
+    while (a < b) {
+      const int64_t mid = a + ((b - a) >> 1);
+      if (B.rmax[mid] >= due) b = mid;
+      else a = mid + 1;
+    }
+    O.pos[i] = bseq(B, a);
+  }
+}
+
+// a key's waiting pairs into a ring of another capacity (tier change), head reset to 0
+__global__ void k_labs_migrate(LabsDev Dn, LabsDev Do) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= Do.nk) return;
+  const int c = Do.cur;
+  LaPend s = Do.pend[c][k];
+  for (int i = 0; i < s.nw && i < Dn.wcap; i++)
+    Dn.wq[c][k * Dn.wcap + i] = Do.wq[c][k * Do.wcap + ((s.wh + i) & (Do.wcap - 1))];
+  s.wh = 0;
+  Dn.pend[c][k] = s;
+}
+
+__global__ void k_labs_init(LabsDev D) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < D.nk) {
+    LaPend s{};
+    s.xseq = s.yseq = -1;
+    s.last = INT64_MIN;
+    D.pend[0][i] = s;
+    D.pend[1][i] = s;
+  }
+}
+
+struct LabsState {
+  LabsDev D{};
+  int tier = 0;
+
+  static bool lower_term(const LaTermS& t, const LabsShape& sh, const DevProg& P, LaTermD& o) {
+    static const int32_t masks[6] = {4, 6, 1, 3, 2, 13};  // gt ge lt le eq ne
+    o = LaTermD{};
+    o.mask = t.ptype == T_STR ? (t.cmp == 4 ? 2 : 13) : masks[t.cmp];
+    auto side = [&](const LaOperand& a, int8_t& kind, int8_t& flt, double& c) {
+      if (a.kind == 0) {
+        FOperand f{};
+        f.kind = 0;
+        f.tag = a.tag;
+        f.imm = a.imm;
+        int8_t kk;
+        return SweepState::lower_operand(f, t.ptype, T_NULL, kk, c);
+      }
+      kind = (int8_t)(a.state == sh.sx ? 1 : (a.state == sh.sy ? 2 : 3));
+      flt = (int8_t)(P.colTag[a.col] == T_INT && t.ptype == T_FLOAT);
+      return P.colTag[a.col] == T_INT || P.colTag[a.col] == T_FLOAT || P.colTag[a.col] == T_STR;
+    };
+    return side(t.a, o.ak, o.aflt, o.ac) && side(t.b, o.bk, o.bflt, o.bc);
+  }
+  static bool lower(const LaPredS& p, const LabsShape& sh, const DevProg& P, LaPredD& o) {
+    o = LaPredD{};
+    o.n = p.n;
+    o.combine = p.combine;
+    for (int i = 0; i < p.n; i++)
+      if (!lower_term(p.t[i], sh, P, o.t[i])) return false;
+    return true;
+  }
+  static bool shape_ok(const DevProg& P, const LabsShape& sh) {
+    if (!sh.ok) return false;
+    LaPredD a;
+    return lower(sh.fx, sh, P, a) && lower(sh.fy, sh, P, a) && lower(sh.fz, sh, P, a);
+  }
+
+  template <class T>
+  static void al(T*& p, int64_t n) {
+    if (hipMalloc((void**)&p, std::max<int64_t>(n, 1) * sizeof(T)) != hipSuccess)
+      throw std::runtime_error("hipMalloc failed (logical-absent path)");
+  }
+
+  void create(const DevProg& P, const LabsShape& sh, int32_t max_keys, int64_t mcap, hipStream_t s) {
+    if (!lower(sh.fx, sh, P, D.fx) || !lower(sh.fy, sh, P, D.fy) || !lower(sh.fz, sh, P, D.fz))
+      throw std::runtime_error("logical-absent: predicate not lowerable");
+    const int32_t st[3] = {sh.stx, sh.sty, sh.stz}, col[3] = {sh.colx, sh.coly, sh.colz},
+                  sid[3] = {sh.sx, sh.sy, sh.sz};
+    for (int i = 0; i < 3; i++) {
+      D.st[i] = st[i];
+      D.col[i] = col[i];
+      D.sid[i] = sid[i];
+      D.tag[i] = col[i] >= 0 ? P.colTag[col[i]] : T_NULL;
+    }
+    D.wait = sh.wait;
+    D.within = sh.within;
+    D.nk = max_keys;
+    D.cur = 0;
+    for (int c = 0; c < 2; c++) {
+      al(D.pend[c], max_keys);
+      al(D.wq[c], (int64_t)max_keys * LA_WCAP);
+    }
+    al(D.aux, mcap);
+    al(D.cm, max_keys);
+    al(D.om, max_keys);
+    D.wcap = LA_CAPS[0];
+    tier = 0;
+    k_labs_init<<<(unsigned)((max_keys + 255) / 256), 256, 0, s>>>(D);
+  }
+
+  void run(const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt,
+           int* err, void* tmp, size_t tmp_bytes, hipStream_t s, KTimer& kt) {
+    const unsigned gk = (unsigned)((D.nk + 63) / 64);
+    kt.mark("labs_count", s);
+    if (tier == 0) k_labs<false, false><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    else k_labs<false, true><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    kt.mark("labs_scan", s);
+    size_t tb = tmp_bytes;
+    (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
+    kt.mark("labs", s);
+    if (tier == 0) k_labs<true, false><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    else k_labs<true, true><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    kt.mark("labs_pos", s);
+    k_labs_pos<<<1024, 256, 0, s>>>(D, B, O);
+    kt.mark(nullptr, s);
+  }
+
+  void commit() { D.cur ^= 1; }
+
+  // capacity tier t: new rings of LA_CAPS[t] per key; with migrate the committed waits move over
+  // (else the caller overwrites them, e.g. a restore).  False when device memory is short.
+  bool set_tier(int t, bool migrate, hipStream_t s) {
+    if (t < 0 || t >= LA_TIERS) return false;
+    LabsDev Dn = D;
+    Dn.wcap = LA_CAPS[t];
+    const int64_t n = (int64_t)D.nk * Dn.wcap;
+    LaWait* q[3] = {nullptr, nullptr, nullptr};
+    for (int i = 0; i < 3; i++)
+      if (hipMalloc((void**)&q[i], (size_t)n * sizeof(LaWait)) != hipSuccess) {
+        for (LaWait* p : q)
+          if (p) (void)hipFree(p);
+        return false;
+      }
+    Dn.wq[0] = q[0];
+    Dn.wq[1] = q[1];
+    Dn.wtmp = q[2];
+    if (migrate) k_labs_migrate<<<(unsigned)((D.nk + 255) / 256), 256, 0, s>>>(Dn, D);
+    if (hipStreamSynchronize(s) != hipSuccess) return false;
+    for (LaWait* p : {D.wq[0], D.wq[1], D.wtmp})
+      if (p) (void)hipFree(p);
+    D = Dn;
+    tier = t;
+    return true;
+  }
+
+  void release() {
+    for (int c = 0; c < 2; c++) {
+      if (D.pend[c]) (void)hipFree(D.pend[c]);
+      if (D.wq[c]) (void)hipFree(D.wq[c]);
+    }
+    if (D.wtmp) (void)hipFree(D.wtmp);
+    void* qs[] = {D.aux, D.cm, D.om};
+    for (void* p : qs)
+      if (p) (void)hipFree(p);
+    D = LabsDev{};
+  }
+};
+
+}  // namespace shp

@@ -135,4 +135,32 @@ struct CseqShape {
   FPred f1, f2;
 };
 
+// Recognised shape for the logical-absent kernel (labs.h): the playback pattern
+// `every (x=X[fx] and y=Y[fy]) -> not Z[fz] for T [within W]` over three distinct streams, each
+// read through at most one predicate column; fx reads x, fy reads y, fz reads the Z event, x and y.
+struct LaOperand {
+  int8_t kind;   // 0 const, 1 var
+  int8_t state;  // var: state id
+  int8_t tag;    // value tag
+  int8_t pad;
+  int32_t col;   // var: program column
+  int64_t imm;
+};
+struct LaTermS {
+  int8_t cmp, ptype, pad[6];
+  LaOperand a, b;
+};
+struct LaPredS {
+  int32_t n, combine;
+  LaTermS t[2];
+};
+struct LabsShape {
+  int32_t ok;
+  int32_t sx, sy, sz;          // state ids of x, y and the absent state
+  int32_t stx, sty, stz;       // their streams
+  int32_t colx, coly, colz;    // their predicate column (-1: none)
+  int64_t wait, within;        // T, W (-1: no within)
+  LaPredS fx, fy, fz;
+};
+
 }  // namespace shp

@@ -81,6 +81,7 @@ constexpr int SWE_MONO = 1 << 21;   // ts decreases within a key (scan kernels o
 constexpr int SWE_RANGE = 1 << 23;  // ts outside base +- 2^49 ms
 constexpr int SWE_AGGNULL = 1 << 24; // SHP_LAYOUT_AGG: a closing event's aggregated value is null
 constexpr int SWE_P32 = 1 << 25;     // SHP_LAYOUT_PAIRS32: e2 seq - e1 seq >= 2^32
+constexpr int SWE_LEAN = 1 << 26;    // k_sw_lean handed the push to k_sw_solve (not an error)
 
 // 16-byte record.  kt: [63:56] local key (0xFF = none), [55] carried, [54] null,
 // [49:0] ts - base + 2^49.  ref: batch index (events) or carry slot (carried).
@@ -1408,7 +1409,9 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
 // full match records from the (i, j) pairs (shp_push_batch / shp_fetch_matches).  p32: the
 // pairs are SHP_LAYOUT_PAIRS32 (e2 batch index, e2 seq - e1 seq), staged by the caller in O.pos
 // (8 bytes per match); thread i reads its pair before it writes O.pos[i].
-__global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchOut O, int p32) {
+__global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchOut O, int p32, const int* err) {
+  // a push k_sw_lean handed back has reserved slots it never wrote: the exact re-run expands
+  if (err && (*err & SWE_LEAN)) return;
   const int64_t m = min((int64_t)*O.count, O.cap);
   if (blockIdx.x == 0 && threadIdx.x == 0) O.count[1] = 2ull * (unsigned long long)m;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1416,17 +1419,20 @@ __global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchO
     if (p32) {  // (e2's batch index, e2 seq - e1 seq)
       const uint2 pr = reinterpret_cast<const uint2*>(O.pos)[i];
       g = (int64_t)pr.x;
+      if (g >= B.n) continue;
       j = bseq(B, g);
       O.refs[2 * i] = j - (int64_t)pr.y;
       O.refs[2 * i + 1] = j;
     } else if (B.seq) {  // (e1 seq, e2's batch index): the FULL layout with a seq column
       g = O.refs[2 * i + 1];
+      if (g < 0 || g >= B.n) continue;
       j = B.seq[g];
       O.refs[2 * i + 1] = j;
     } else {  // (e1 seq, e2 seq)
       j = O.refs[2 * i + 1];
       g = j - B.seq0;
     }
+    if (g < 0 || g >= B.n) continue;  // not a pair of this push (never written)
     O.key[i] = B.partitioned ? key[g] : 0;
     O.ts[i] = B.ts[g];
     O.type[i] = 0;
@@ -1783,11 +1789,11 @@ struct SweepState {
   }
 
   void expand(const BatchView& B, const int32_t* key, const MatchOut& O, hipStream_t s, KTimer& kt,
-              int64_t m_host = -1) {
+              int64_t m_host = -1, const int* err = nullptr) {
     if (D.p32 && m_host > 0)  // stage the 8-byte pairs where k_sw_expand reads them
       (void)hipMemcpyAsync(O.pos, O.refs, (size_t)m_host * 8, hipMemcpyDeviceToDevice, s);
     kt.mark("sw_expand", s);
-    k_sw_expand<<<2048, 256, 0, s>>>(B, key, O, D.p32);
+    k_sw_expand<<<2048, 256, 0, s>>>(B, key, O, D.p32, err);
     kt.mark(nullptr, s);
   }
 };

@@ -1,0 +1,184 @@
+"""The logical-absent path (siddhi_amd/csrc/labs.h, opt-in force_general = 4), C4's shape:
+`every (e1=S1[f] and e2=S2[f]) -> not S3[price > e1.price] for T within W` in playback.
+
+CPU: the per-key rule labs.h implements, restated in Python (pend = the logical partial, waits =
+completed pairs in completion order, each firing at the first event whose playback clock reaches
+completion ts + T), against the oracle's object-level restatement of the Logical / AbsentStream
+processors and the playback Scheduler (oracle/oracle.cpp) -- the C4 stream at several key counts,
+and dense random streams with ties in no due time (cross-key scheduler ties are parity-unpinned,
+SURVEY.md §8c).  GPU (`-m gpu`): k_labs + k_labs_pos against the oracle, split pushes, a clock
+advanced with no event, snapshot/restore, and the refusal of out-of-order timestamps.
+"""
+from collections import deque
+
+import numpy as np
+import pytest
+
+from diff_util import compare, per_key, program_for, run, small_stream
+from oracle.oracle import OracleEngine
+
+W, WAIT = 10_000, 5_000
+
+
+def model(ts, key, st, pr):
+    """labs.h's rule over one playback stream (streams 0 = S1 (e1), 1 = S2 (e2), 2 = S3)."""
+    out, S = {}, {}
+    clock = 0
+    for g in range(len(ts)):
+        t, k, s, p = int(ts[g]), int(key[g]), int(st[g]), float(pr[g])
+        clock = max(clock, t)
+        for kk, stt in S.items():  # timers the clock reached, per key in completion order
+            wq = stt["waits"]
+            while wq and wq[0][0] <= clock:
+                due, e1, e2 = wq.popleft()
+                if abs(e1[1] - due) <= W and abs(e2[1] - due) <= W:
+                    out.setdefault(kk, []).append((due, 0, g, ((e2[0],), (e1[0],), ())))
+        stt = S.setdefault(k, {"pend": {"e1": None, "e2": None}, "waits": deque()})
+        pend = stt["pend"]
+        if any(ev is not None and abs(ev[1] - t) > W for ev in pend.values()):
+            stt["pend"] = pend = {"e1": None, "e2": None}
+        if s in (0, 1):
+            slot, other = ("e1", "e2") if s == 0 else ("e2", "e1")
+            if p > 20 and pend[slot] is None:
+                pend[slot] = (g, t, p)
+                if pend[other] is not None:
+                    stt["waits"].append((t + WAIT, pend["e1"], pend["e2"]))
+                    stt["pend"] = {"e1": None, "e2": None}
+        elif s == 2:
+            stt["waits"] = deque(w for w in stt["waits"] if not p > w[1][2])
+    return out
+
+
+def _oracle(cq, ts, key, st, pr, batch):
+    e = OracleEngine(cq.program_json(), 0)
+    for lo in range(0, len(ts), batch):
+        hi = min(len(ts), lo + batch)
+        e.push(ts[lo:hi], key[lo:hi], st[lo:hi], [pr[lo:hi]] * 3, [None] * 3)
+    return per_key(e.fetch())
+
+
+@pytest.mark.parametrize("keys,n", [(20, 100_000), (200, 200_000), (1000, 300_000)])
+def test_model_matches_oracle_c4_stream(keys, n):
+    cq = program_for(4)
+    g = small_stream(4, n, keys)
+    pr = g["price"].astype(np.float32)
+    want = _oracle(cq, g["ts"], g["key"], g["stream"], pr, 65_537)
+    got = model(g["ts"], g["key"], g["stream"], pr)
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 0
+
+
+@pytest.mark.parametrize("keys,step", [(2, 1), (5, 3), (20, 7), (100, 2)])
+def test_model_matches_oracle_dense_random(keys, step):
+    rng = np.random.default_rng(keys * 11 + step)
+    n = 40_000
+    ts = (np.arange(n) * step).astype(np.int64) + 1000
+    key = rng.integers(0, keys, n).astype(np.int32)
+    st = rng.integers(0, 3, n).astype(np.int32)
+    pr = (rng.integers(0, 10000, n) / 100.0).astype(np.float32)
+    want = _oracle(program_for(4), ts, key, st, pr, n)
+    got = model(ts, key, st, pr)
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 5
+
+
+# ---------------------------------------------------------------- GPU (k_labs)
+
+def _hip(cq, keys, batch, **kw):
+    from siddhi_amd.native import HipEngine
+    return HipEngine(cq.program_json(), 0, max_keys=keys, max_batch=batch, force_general=4, **kw)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("keys,n,batch", [(1, 40_000, 9_973), (200, 300_000, 65_537), (1000, 600_000, 200_003)],
+                         ids=["1key", "200keys", "1000keys"])
+def test_c4_labs_vs_oracle(keys, n, batch):
+    cq = program_for(4)
+    g = small_stream(4, n, keys)
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g, batch))
+    eng = _hip(cq, keys, batch)
+    assert eng.path == 4
+    got = per_key(run(eng, cq, g, batch))
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > (0 if keys == 1 else 20)
+
+
+@pytest.mark.gpu
+def test_labs_equals_general_lanes_and_advance():
+    """Pushes, then a clock advanced with no event (shp_advance_clock fires the waiting pairs):
+    the same records from k_labs and from the general lanes, and from the oracle."""
+    cq = program_for(4)
+    g = small_stream(4, 150_000, 300)
+    end = int(g["ts"][-1]) + 60_000
+    outs = []
+    for mk in (lambda: OracleEngine(cq.program_json(), 0), lambda: _hip(cq, 300, 1 << 16),
+               lambda: __import__("siddhi_amd.native", fromlist=["HipEngine"]).HipEngine(
+                   cq.program_json(), 0, max_keys=300, max_batch=1 << 16, force_general=1)):
+        e = mk()
+        n = len(g["ts"])
+        for lo in range(0, n, 50_000):
+            hi = min(n, lo + 50_000)
+            e.push(g["ts"][lo:hi], g["key"][lo:hi], g["stream"][lo:hi], [g["price"][lo:hi].astype(np.float32)] * 3,
+                   [None] * 3)
+        e.advance(end)
+        outs.append(per_key(e.fetch()))
+    assert compare(outs[0], outs[1]) is None, compare(outs[0], outs[1])
+    assert compare(outs[0], outs[2]) is None, compare(outs[0], outs[2])
+
+
+@pytest.mark.gpu
+def test_labs_snapshot_restore_continues():
+    cq = program_for(4)
+    g = small_stream(4, 120_000, 200)
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    half = {k: v[:60_000] for k, v in g.items()}
+    rest = {k: v[60_000:] for k, v in g.items()}
+    a = _hip(cq, 200, 1 << 16)
+    first = run(a, cq, half)
+    blob = a.snapshot()
+    assert "absent" in str(a.describe(blob))
+    b = _hip(cq, 200, 1 << 16)
+    b.restore(blob)
+    second = run(b, cq, rest)
+    from siddhi_amd.native import _concat
+    got = per_key(_concat([first, second], None, a.S))
+    assert compare(want, got) is None, compare(want, got)
+
+
+@pytest.mark.gpu
+def test_labs_refuses_unordered_timestamps_and_keeps_state():
+    from siddhi_amd.native import ShpError
+    cq = program_for(4)
+    g = small_stream(4, 20_000, 50)
+    from siddhi_amd.native import _concat
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    eng = _hip(cq, 50, 1 << 15)
+    first = run(eng, cq, {k: v[:10_000] for k, v in g.items()})
+    bad = {k: v[10_000:].copy() for k, v in g.items()}
+    bad["ts"][100] -= 5_000
+    with pytest.raises(ShpError):
+        run(eng, cq, bad)
+    # the refused push left the engine as it was: the ordered remainder continues exactly
+    second = run(eng, cq, {k: v[10_000:] for k, v in g.items()})
+    got = per_key(_concat([first, second], None, eng.S))
+    assert compare(want, got) is None, compare(want, got)
+
+
+@pytest.mark.gpu
+def test_labs_rings_grow_and_snapshot_carries_the_tier():
+    """One key with dense events: hundreds of pairs wait on the absent state at once, beyond the
+    16-entry LDS ring, so the engine moves to the HBM rings (256, 4096) and re-runs the push; a
+    snapshot taken there restores into a fresh engine (tier 0) and continues exactly."""
+    from siddhi_amd.native import _concat
+    cq = program_for(4)
+    g = small_stream(4, 80_000, 1)
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    a = _hip(cq, 1, 1 << 16)
+    first = run(a, cq, {k: v[:40_000] for k, v in g.items()})
+    blob = a.snapshot()
+    b = _hip(cq, 1, 1 << 16)
+    b.restore(blob)
+    second = run(b, cq, {k: v[40_000:] for k, v in g.items()})
+    got = per_key(_concat([first, second], None, a.S))
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 0

@@ -128,7 +128,7 @@ def test_far_closers_and_many_open_candidates():
                 parts_ts.append(t)
                 parts_key.append(k)
                 parts_v.append(90.0 - 60.0 * i / run_len)
-            bg = rng.integers(0, keys, 4)
+            bg = rng.choice(np.setdiff1d(np.arange(keys), hot), 4)  # background keys never close a hot key's run
             for k in bg:
                 parts_ts.append(t)
                 parts_key.append(int(k))
