@@ -507,7 +507,7 @@ struct shp_engine {
     } else if (fast == 3) {
       cs.create(comp.P, comp.cseq, cfg.max_keys, stream);
     } else if (fast == 4) {
-      la.create(comp.P, comp.labs, cfg.max_keys, mcap, stream);
+      la.create(comp.P, comp.labs, cfg.max_keys, mcap, cap, stream);
     } else {
       Y.build(cfg.max_keys);
       // few keys: lanes in LDS, as many per workgroup as fit 64 KB (at most 16)

@@ -94,7 +94,28 @@ struct LabsDev {
   LaWait* wtmp;      // nk * wcap: the count pass's working rings (tiers >= 1)
   int64_t* aux;      // per record of the push: last batch index the timer can have fired at
   uint32_t *cm, *om; // nk: records per key (count pass), their exclusive scan
+  // the batch in key order (k_labs_gather): one thread per key then reads its events
+  // contiguously; random gathers from 16 waves were bound by address translation (5 us an event)
+  int64_t *s_ts, *s_clk;
+  int32_t* s_st;
+  uint32_t* s_v;
+  uint8_t* s_n;
 };
+
+// sorted position i <- batch event perm[i]: ts, clock, stream, and the value of its stream's column
+__global__ void k_labs_gather(LabsDev D, BatchView B, const uint32_t* __restrict__ perm, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = perm[i];
+    const int st = B.stream ? B.stream[g] : 0;
+    const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
+    const int c = role == 0 ? D.col[0] : (role == 1 ? D.col[1] : (role == 2 ? D.col[2] : -1));
+    D.s_ts[i] = B.ts[g];
+    D.s_clk[i] = B.rmax[g];
+    D.s_st[i] = st;
+    D.s_v[i] = c >= 0 ? ((const uint32_t*)B.cols[c])[g] : 0u;
+    D.s_n[i] = c < 0 || (B.nulls[c] && B.nulls[c][g]) ? 1 : 0;
+  }
+}
 
 __device__ __forceinline__ double la_val(uint32_t v, int8_t tag, bool flt) {
   if (tag == T_FLOAT) return (double)__uint_as_float(v);
@@ -102,26 +123,46 @@ __device__ __forceinline__ double la_val(uint32_t v, int8_t tag, bool flt) {
   return flt ? (double)(float)x : (double)x;
 }
 
-__device__ __forceinline__ bool la_term(const LaTermD& t, const uint32_t* v, const bool* nl, const int8_t* tag) {
+// The three role values (x, y, z) travel as scalars and are picked with selects: an indexed
+// local array would live in scratch memory (measured: k_labs ran 2.4 us per event).
+struct LaVals {
+  uint32_t v0, v1, v2;
+  bool n0, n1, n2;
+  int8_t t0, t1, t2;
+};
+__device__ __forceinline__ void la_pick(const LaVals& V, int kind, uint32_t& v, bool& n, int8_t& t) {
+  v = kind == 1 ? V.v0 : (kind == 2 ? V.v1 : V.v2);
+  n = kind == 1 ? V.n0 : (kind == 2 ? V.n1 : V.n2);
+  t = kind == 1 ? V.t0 : (kind == 2 ? V.t1 : V.t2);
+}
+__device__ __forceinline__ bool la_term(const LaTermD& t, const LaVals& V) {
   bool nul = false;
   double A = t.ac, B = t.bc;
   if (t.ak) {
-    A = la_val(v[t.ak - 1], tag[t.ak - 1], t.aflt);
-    nul |= nl[t.ak - 1];
+    uint32_t v;
+    bool n;
+    int8_t tg;
+    la_pick(V, t.ak, v, n, tg);
+    A = la_val(v, tg, t.aflt);
+    nul |= n;
   }
   if (t.bk) {
-    B = la_val(v[t.bk - 1], tag[t.bk - 1], t.bflt);
-    nul |= nl[t.bk - 1];
+    uint32_t v;
+    bool n;
+    int8_t tg;
+    la_pick(V, t.bk, v, n, tg);
+    B = la_val(v, tg, t.bflt);
+    nul |= n;
   }
   const int o3 = (A < B ? 1 : 0) | (A == B ? 2 : 0) | (A > B ? 4 : 0);
   return !nul && ((o3 | (o3 == 0 ? 8 : 0)) & t.mask) != 0;  // CompareConditionExpressionExecutor
 }
 
-__device__ __forceinline__ bool la_pred(const LaPredD& p, const uint32_t* v, const bool* nl, const int8_t* tag) {
+__device__ __forceinline__ bool la_pred(const LaPredD& p, const LaVals& V) {
   if (p.n == 0) return true;
-  const bool a = la_term(p.t[0], v, nl, tag);
+  const bool a = la_term(p.t[0], V);
   if (p.n == 1) return a;
-  const bool b = la_term(p.t[1], v, nl, tag);
+  const bool b = la_term(p.t[1], V);
   return p.combine ? (a || b) : (a && b);
 }
 
@@ -165,7 +206,8 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
     }
   }
   // one step per event of the key, plus a final step for the timers the batch's last clock reaches
-  auto step = [&](bool act, int64_t g, int64_t clk, int64_t ts, int stm, const uint32_t* evs, const bool* ens) {
+  auto step = [&](bool act, int64_t g, int64_t clk, int64_t ts, int stm, uint32_t ev0, uint32_t ev1, uint32_t ev2,
+                  bool en0, bool en1, bool en2) {
     const int64_t hi = g;
     // 1. timers the clock reached (FIFO: due times follow completion order)
     int nf = 0, ne = 0;
@@ -215,14 +257,19 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
     }
     const int role = stm == D.st[0] ? 0 : (stm == D.st[1] ? 1 : (stm == D.st[2] ? 2 : -1));
     if (role < 0) return;
-    uint32_t v[3] = {s.xv, s.yv, 0u};
-    bool nl[3] = {(s.fl & 1u) != 0, (s.fl & 2u) != 0, true};
-    const uint32_t ev = evs[role];
-    const bool en = ens[role];
+    LaVals V{s.xv, s.yv, 0u, (s.fl & 1u) != 0, (s.fl & 2u) != 0, true, D.tag[0], D.tag[1], D.tag[2]};
+    const uint32_t ev = role == 0 ? ev0 : (role == 1 ? ev1 : ev2);
+    const bool en = role == 0 ? en0 : (role == 1 ? en1 : en2);
     if (role < 2) {
-      v[role] = ev;
-      nl[role] = en;
-      if (!la_pred(role == 0 ? D.fx : D.fy, v, nl, D.tag)) return;
+      if (role == 0) {
+        V.v0 = ev;
+        V.n0 = en;
+        if (!la_pred(D.fx, V)) return;
+      } else {
+        V.v1 = ev;
+        V.n1 = en;
+        if (!la_pred(D.fy, V)) return;
+      }
       const int64_t seqg = bseq(B, g);
       if (role == 0 && s.xseq < 0) {
         s.xseq = seqg;
@@ -255,52 +302,42 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
         s.fl = 0;
       }
     } else {  // a Z event drops every waiting pair its filter matches
-      v[2] = ev;
-      nl[2] = en;
+      V.v2 = ev;
+      V.n2 = en;
       int o = 0;
       for (int i = 0; i < s.nw; i++) {
         const LaWait w = wq[(s.wh + i) & msk];
-        v[0] = w.xv;
-        v[1] = w.yv;
-        nl[0] = (w.fl & 1u) != 0;
-        nl[1] = (w.fl & 2u) != 0;
-        if (!la_pred(D.fz, v, nl, D.tag)) wq[(s.wh + o++) & msk] = w;
+        V.v0 = w.xv;
+        V.v1 = w.yv;
+        V.n0 = (w.fl & 1u) != 0;
+        V.n1 = (w.fl & 2u) != 0;
+        if (!la_pred(D.fz, V)) wq[(s.wh + o++) & msk] = w;
       }
       s.nw = o;
     }
     };
   // the key's events in blocks of LA_D: every load of a block is issued before the block is
   // processed (one thread per key leaves the memory system idle: latency, not bandwidth, bounds it)
-  const uint32_t* c0 = D.col[0] >= 0 ? (const uint32_t*)B.cols[D.col[0]] : nullptr;
-  const uint32_t* c1 = D.col[1] >= 0 ? (const uint32_t*)B.cols[D.col[1]] : nullptr;
-  const uint32_t* c2 = D.col[2] >= 0 ? (const uint32_t*)B.cols[D.col[2]] : nullptr;
-  const uint8_t* n0 = D.col[0] >= 0 ? B.nulls[D.col[0]] : nullptr;
-  const uint8_t* n1 = D.col[1] >= 0 ? B.nulls[D.col[1]] : nullptr;
-  const uint8_t* n2 = D.col[2] >= 0 ? B.nulls[D.col[2]] : nullptr;
   for (uint32_t j0 = 0; live && j0 <= cnt; j0 += LA_D) {
     int64_t gq[LA_D], cq[LA_D], tq[LA_D];
     int32_t sq[LA_D];
-    uint32_t vq[LA_D][3];
-    bool nq[LA_D][3];
-#pragma unroll
-    for (int d = 0; d < LA_D; d++) gq[d] = j0 + d < cnt ? (int64_t)perm[beg + j0 + d] : B.n - 1;
+    uint32_t vq[LA_D];
+    bool nq[LA_D];
 #pragma unroll
     for (int d = 0; d < LA_D; d++) {
-      const int64_t g = gq[d];
-      const bool ev = j0 + d < cnt, any = j0 + d <= cnt && B.n > 0;
-      cq[d] = any ? B.rmax[g] : INT64_MIN;
-      tq[d] = ev ? B.ts[g] : 0;
-      sq[d] = ev ? (B.stream ? B.stream[g] : 0) : -1;
-      vq[d][0] = ev && c0 ? c0[g] : 0u;
-      vq[d][1] = ev && c1 ? c1[g] : 0u;
-      vq[d][2] = ev && c2 ? c2[g] : 0u;
-      nq[d][0] = !c0 || (n0 && ev && n0[g]);
-      nq[d][1] = !c1 || (n1 && ev && n1[g]);
-      nq[d][2] = !c2 || (n2 && ev && n2[g]);
+      const uint32_t j = j0 + d;
+      const bool ev = j < cnt;
+      const int64_t i = (int64_t)beg + j;
+      gq[d] = ev ? (int64_t)perm[i] : B.n - 1;
+      cq[d] = ev ? D.s_clk[i] : (j == cnt && B.n > 0 ? B.rmax[B.n - 1] : INT64_MIN);
+      tq[d] = ev ? D.s_ts[i] : 0;
+      sq[d] = ev ? D.s_st[i] : -1;
+      vq[d] = ev ? D.s_v[i] : 0u;
+      nq[d] = ev ? D.s_n[i] != 0 : true;
     }
 #pragma unroll
     for (int d = 0; d < LA_D; d++)
-      if (j0 + d <= cnt) step(j0 + d < cnt, gq[d], cq[d], tq[d], sq[d], vq[d], nq[d]);
+      if (j0 + d <= cnt) step(j0 + d < cnt, gq[d], cq[d], tq[d], sq[d], vq[d], vq[d], vq[d], nq[d], nq[d], nq[d]);
   }
   if (!EMIT) {
     if (live) D.cm[k] = nm;
@@ -399,7 +436,7 @@ struct LabsState {
       throw std::runtime_error("hipMalloc failed (logical-absent path)");
   }
 
-  void create(const DevProg& P, const LabsShape& sh, int32_t max_keys, int64_t mcap, hipStream_t s) {
+  void create(const DevProg& P, const LabsShape& sh, int32_t max_keys, int64_t mcap, int64_t cap, hipStream_t s) {
     if (!lower(sh.fx, sh, P, D.fx) || !lower(sh.fy, sh, P, D.fy) || !lower(sh.fz, sh, P, D.fz))
       throw std::runtime_error("logical-absent: predicate not lowerable");
     const int32_t st[3] = {sh.stx, sh.sty, sh.stz}, col[3] = {sh.colx, sh.coly, sh.colz},
@@ -421,6 +458,11 @@ struct LabsState {
     al(D.aux, mcap);
     al(D.cm, max_keys);
     al(D.om, max_keys);
+    al(D.s_ts, cap);
+    al(D.s_clk, cap);
+    al(D.s_st, cap);
+    al(D.s_v, cap);
+    al(D.s_n, cap);
     D.wcap = LA_CAPS[0];
     tier = 0;
     k_labs_init<<<(unsigned)((max_keys + 255) / 256), 256, 0, s>>>(D);
@@ -429,6 +471,8 @@ struct LabsState {
   void run(const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt,
            int* err, void* tmp, size_t tmp_bytes, hipStream_t s, KTimer& kt) {
     const unsigned gk = (unsigned)((D.nk + 63) / 64);
+    kt.mark("labs_gather", s);
+    if (B.n > 0) k_labs_gather<<<2048, 256, 0, s>>>(D, B, perm, B.n);
     kt.mark("labs_count", s);
     if (tier == 0) k_labs<false, false><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
     else k_labs<false, true><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
@@ -477,7 +521,7 @@ struct LabsState {
       if (D.wq[c]) (void)hipFree(D.wq[c]);
     }
     if (D.wtmp) (void)hipFree(D.wtmp);
-    void* qs[] = {D.aux, D.cm, D.om};
+    void* qs[] = {D.aux, D.cm, D.om, D.s_ts, D.s_clk, D.s_st, D.s_v, D.s_n};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = LabsDev{};

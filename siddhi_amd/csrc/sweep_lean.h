@@ -200,6 +200,20 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     }
   };
   int pPS = 0, pPE = 0, pcur = 0;  // this wave's range of the previous chunk, and its carry buffer
+#ifdef SHP_SW_STAMPS  // diagnostic build: wave cycles per phase (barrier waits count in the phase before)
+  unsigned long long stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t stp = clock64();
+#define SL_STAMP(k)                 \
+  do {                              \
+    const uint64_t t_ = clock64();  \
+    stc[k] += t_ - stp;             \
+    stp = t_;                       \
+  } while (0)
+#else
+#define SL_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
   __syncthreads();
   for (int64_t cb = rb; cb < re; cb += SL_CHUNK) {
     const int nchunk = (int)min((int64_t)SL_CHUNK, re - cb);
@@ -222,10 +236,12 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       }
     }
     __syncthreads();  // A
+    SL_STAMP(0);
     // flags raised by the previous chunk are read here, where no thread writes S.flag (all
     // threads take the same branch)
     if (S.flag) break;
     if (cb != rb) emit(pPS, pPE, pcur);  // the previous chunk's matches
+    SL_STAMP(1);
     const int E = S.cn[cur] + nchunk;
     // 2. key run offsets and the wave split (wave 0)
     if (w == 0) {
@@ -282,6 +298,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       }
     }
     __syncthreads();  // B
+    SL_STAMP(2);
     // 3. place records and carried candidates at their sorted positions
 #pragma unroll
     for (int s = 0; s < SL_R; s++) {
@@ -321,6 +338,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       if (nbk < re) tbk = D.recs[nbk].kt;
     }
     __syncthreads();  // C
+    SL_STAMP(3);
     // ---- from here each wave works alone on its key runs [PS, PE)
     const int PS = S.ps[w], PE = S.ps[w + 1];
     for (int b = (int)lane; b < nb; b += 64) S.wc[w][b] = 0;  // this wave's counters, next chunk
@@ -394,6 +412,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       if (nwl >= 64) nwl = drain(nwl);
     }
     while (nwl > 0) nwl = drain(nwl);
+    SL_STAMP(4);
     // 5. closes and open candidates per position (contiguous block per lane), output range and
     //    carry slots; open candidates compacted in key order; tv.x becomes the output offset
     const int nw = PE - PS;
@@ -475,6 +494,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     pPE = PE;
     pcur = cur;
     cur = nx;
+    SL_STAMP(5);
   }
   __syncthreads();
   if (S.flag) {
@@ -482,6 +502,18 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     return;
   }
   emit(pPS, pPE, pcur);  // the last chunk's matches
+#ifdef SHP_SW_STAMPS
+  SL_STAMP(1);
+  {
+    __shared__ unsigned long long sts[8];
+    if (tid < 8) sts[tid] = 0;
+    __syncthreads();
+    if (lane == 0)
+      for (int k = 0; k < 8; k++) atomicAdd(&sts[k], stc[k]);
+    __syncthreads();
+    if (tid < 8 && D.stamps) D.stamps[(int64_t)o * 8 + tid] = sts[tid];
+  }
+#endif
   // write back the carry in key order (k_sw_solve's layout) and the per-key flags (copy wr)
   {
     uint32_t total;

@@ -44,9 +44,17 @@ def main():
         mt = native.ShpMatches()
         rc = L.shp_push_batch_device(eng.h, ctypes.byref(b), ctypes.byref(mt))
         assert rc == 0, L.shp_last_error(eng.h)
-        ks = {k: eng.kernel_ms(k) for k in ("sw_count", "sw_scan", "sw_scatter", "sw_solve")}
+        ks = {k: eng.kernel_ms(k) for k in ("sw_count", "sw_scan", "sw_scatter", "sw_lean", "sw_solve")}
         print(f"rep {rep}: m={mt.m} " + " ".join(f"{k}={v:.3f}ms" for k, v in ks.items()), flush=True)
-        if stamps:
+        if stamps and ks["sw_lean"] > 0:  # k_sw_lean: wave cycles per phase, summed over the waves
+            buf = (ctypes.c_ulonglong * (1 << 20))()
+            nown = L.shp_debug_sw_stamps(eng.h, buf, 1 << 20)
+            st = np.frombuffer(buf, dtype=np.uint64, count=nown * 8).reshape(nown, 8).astype(np.float64)
+            names = ["rank+A", "emit(prev)", "scan+B", "place+C", "probe", "scanpass+carry", "-", "-"]
+            tot = st.sum()
+            for k in range(6):
+                print(f"    {names[k]:<16} {100 * st[:, k].sum() / tot:.1f}%  (mean wave-cycles/owner {st[:, k].mean():.3e})")
+        elif stamps:
             buf = (ctypes.c_ulonglong * (1 << 20))()
             nown = L.shp_debug_sw_stamps(eng.h, buf, 1 << 20)
             st = np.frombuffer(buf, dtype=np.uint64, count=nown * 8).reshape(nown, 8).astype(np.float64)
