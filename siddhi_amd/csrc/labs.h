@@ -45,10 +45,17 @@
 
 namespace shp {
 
-constexpr int LA_WCAP = 16;                      // waiting pairs per key held in LDS (tier 0)
+constexpr int LA_WCAP = 8;                       // waiting pairs per key held in LDS (tier 0)
 constexpr int LA_TIERS = 3;
-constexpr int32_t LA_CAPS[LA_TIERS] = {16, 256, 4096};
-constexpr int LA_D = 16;  // events loaded ahead per key
+constexpr int32_t LA_CAPS[LA_TIERS] = {8, 256, 4096};
+constexpr int LA_SB = 16;                        // events of a key staged in LDS per refill
+
+struct LaEv {  // one event of a key's run, staged in LDS
+  int64_t ts, clk;
+  uint32_t g, v;
+  int32_t st;
+  uint32_t n;
+};
 constexpr int LA_UNORDERED = 1 << 27;  // a key's timestamps decrease (this path needs them ordered)
 
 struct LaTermD {
@@ -130,30 +137,21 @@ struct LaVals {
   bool n0, n1, n2;
   int8_t t0, t1, t2;
 };
-__device__ __forceinline__ void la_pick(const LaVals& V, int kind, uint32_t& v, bool& n, int8_t& t) {
-  v = kind == 1 ? V.v0 : (kind == 2 ? V.v1 : V.v2);
-  n = kind == 1 ? V.n0 : (kind == 2 ? V.n1 : V.n2);
-  t = kind == 1 ? V.t0 : (kind == 2 ? V.t1 : V.t2);
+// one operand as a double: every role's value is converted and the kind picks one with selects
+// over scalars (a select over the fields of one object became an indexed scratch load)
+__device__ __forceinline__ double la_side(int kind, double c, int8_t flt, uint32_t v0, uint32_t v1, uint32_t v2,
+                                          int8_t t0, int8_t t1, int8_t t2) {
+  const uint32_t v = kind == 1 ? v0 : (kind == 2 ? v1 : v2);
+  const int8_t tg = kind == 1 ? t0 : (kind == 2 ? t1 : t2);
+  return kind == 0 ? c : la_val(v, tg, flt);
 }
 __device__ __forceinline__ bool la_term(const LaTermD& t, const LaVals& V) {
-  bool nul = false;
-  double A = t.ac, B = t.bc;
-  if (t.ak) {
-    uint32_t v;
-    bool n;
-    int8_t tg;
-    la_pick(V, t.ak, v, n, tg);
-    A = la_val(v, tg, t.aflt);
-    nul |= n;
-  }
-  if (t.bk) {
-    uint32_t v;
-    bool n;
-    int8_t tg;
-    la_pick(V, t.bk, v, n, tg);
-    B = la_val(v, tg, t.bflt);
-    nul |= n;
-  }
+  const uint32_t v0 = V.v0, v1 = V.v1, v2 = V.v2;
+  const bool n0 = V.n0, n1 = V.n1, n2 = V.n2;
+  const double A = la_side(t.ak, t.ac, t.aflt, v0, v1, v2, V.t0, V.t1, V.t2);
+  const double B = la_side(t.bk, t.bc, t.bflt, v0, v1, v2, V.t0, V.t1, V.t2);
+  const bool nul = (t.ak == 1 && n0) || (t.ak == 2 && n1) || (t.ak == 3 && n2) || (t.bk == 1 && n0) ||
+                   (t.bk == 2 && n1) || (t.bk == 3 && n2);
   const int o3 = (A < B ? 1 : 0) | (A == B ? 2 : 0) | (A > B ? 4 : 0);
   return !nul && ((o3 | (o3 == 0 ? 8 : 0)) & t.mask) != 0;  // CompareConditionExpressionExecutor
 }
@@ -168,12 +166,17 @@ __device__ __forceinline__ bool la_pred(const LaPredD& p, const LaVals& V) {
 
 // HBMQ: the waits ring is worked on in HBM (tiers >= 1: the committed ring is copied to the
 // pass's own ring first); otherwise in LDS (tier 0)
-template <bool EMIT, bool HBMQ>
+// KPB keys per 64-thread block: 64 (a lane per key), or 1 for few keys (a wave per key: the lanes
+// of a wave would otherwise run the three streams' branches one after another, and the SIMDs
+// beyond 1 / 64 of the keys sit idle)
+template <bool EMIT, bool HBMQ, int KPB>
 __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
                                              const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                              int* err) {
-  __shared__ LaWait W[HBMQ ? 1 : 64][HBMQ ? 1 : LA_WCAP];
-  const int k = blockIdx.x * 64 + threadIdx.x;
+  __shared__ LaWait W[HBMQ ? 1 : KPB][HBMQ ? 1 : LA_WCAP];
+  __shared__ LaEv SB[KPB][LA_SB];
+  if (threadIdx.x >= KPB) return;
+  const int k = blockIdx.x * KPB + threadIdx.x;
   const uint32_t lane = threadIdx.x;
   const bool live = k < D.nk;
   const int rd = D.cur, wr = D.cur ^ 1;
@@ -311,34 +314,42 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
         V.v1 = w.yv;
         V.n0 = (w.fl & 1u) != 0;
         V.n1 = (w.fl & 2u) != 0;
-        if (!la_pred(D.fz, V)) wq[(s.wh + o++) & msk] = w;
+        if (!la_pred(D.fz, V)) {
+          if (o != i) wq[(s.wh + o) & msk] = w;
+          o++;
+        }
       }
       s.nw = o;
     }
-    };
-  // the key's events in blocks of LA_D: every load of a block is issued before the block is
-  // processed (one thread per key leaves the memory system idle: latency, not bandwidth, bounds it)
-  for (uint32_t j0 = 0; live && j0 <= cnt; j0 += LA_D) {
-    int64_t gq[LA_D], cq[LA_D], tq[LA_D];
-    int32_t sq[LA_D];
-    uint32_t vq[LA_D];
-    bool nq[LA_D];
+  };
+  // the key's run (contiguous in the gathered columns) is staged in LDS LA_SB events at a time:
+  // the refill's loads are independent and in flight together (16 waves in all leave HBM latency
+  // exposed otherwise: ~4 us a step), and the step body is not unrolled (copies of it overflowed
+  // the instruction cache)
+  LaEv* sb = SB[lane];
+  for (uint32_t j0 = 0; live && j0 < cnt; j0 += LA_SB) {
 #pragma unroll
-    for (int d = 0; d < LA_D; d++) {
-      const uint32_t j = j0 + d;
-      const bool ev = j < cnt;
-      const int64_t i = (int64_t)beg + j;
-      gq[d] = ev ? (int64_t)perm[i] : B.n - 1;
-      cq[d] = ev ? D.s_clk[i] : (j == cnt && B.n > 0 ? B.rmax[B.n - 1] : INT64_MIN);
-      tq[d] = ev ? D.s_ts[i] : 0;
-      sq[d] = ev ? D.s_st[i] : -1;
-      vq[d] = ev ? D.s_v[i] : 0u;
-      nq[d] = ev ? D.s_n[i] != 0 : true;
+    for (int q = 0; q < LA_SB; q++) {
+      if (j0 + q < cnt) {
+        const int64_t i = (int64_t)beg + j0 + q;
+        LaEv x;
+        x.ts = D.s_ts[i];
+        x.clk = D.s_clk[i];
+        x.g = perm[i];
+        x.v = D.s_v[i];
+        x.st = D.s_st[i];
+        x.n = D.s_n[i];
+        sb[q] = x;
+      }
     }
-#pragma unroll
-    for (int d = 0; d < LA_D; d++)
-      if (j0 + d <= cnt) step(j0 + d < cnt, gq[d], cq[d], tq[d], sq[d], vq[d], vq[d], vq[d], nq[d], nq[d], nq[d]);
+    const uint32_t nq = min((uint32_t)LA_SB, cnt - j0);
+#pragma unroll 1
+    for (uint32_t q = 0; q < nq; q++) {
+      const LaEv x = sb[q];
+      step(true, (int64_t)x.g, x.clk, x.ts, x.st, x.v, x.v, x.v, x.n != 0, x.n != 0, x.n != 0);
+    }
   }
+  if (live) step(false, B.n - 1, B.n > 0 ? B.rmax[B.n - 1] : INT64_MIN, 0, -1, 0u, 0u, 0u, true, true, true);
   if (!EMIT) {
     if (live) D.cm[k] = nm;
     return;
@@ -468,20 +479,31 @@ struct LabsState {
     k_labs_init<<<(unsigned)((max_keys + 255) / 256), 256, 0, s>>>(D);
   }
 
+  template <bool EMIT>
+  void launch(unsigned gk, bool few, const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg,
+              const uint32_t* kcnt, int* err, hipStream_t s) {
+    if (few) {
+      if (tier == 0) k_labs<EMIT, false, 1><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+      else k_labs<EMIT, true, 1><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    } else {
+      if (tier == 0) k_labs<EMIT, false, 64><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+      else k_labs<EMIT, true, 64><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    }
+  }
+
   void run(const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt,
            int* err, void* tmp, size_t tmp_bytes, hipStream_t s, KTimer& kt) {
-    const unsigned gk = (unsigned)((D.nk + 63) / 64);
+    const bool few = D.nk <= 8192;  // a wave per key while that fills the CUs
+    const unsigned gk = few ? (unsigned)D.nk : (unsigned)((D.nk + 63) / 64);
     kt.mark("labs_gather", s);
     if (B.n > 0) k_labs_gather<<<2048, 256, 0, s>>>(D, B, perm, B.n);
     kt.mark("labs_count", s);
-    if (tier == 0) k_labs<false, false><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
-    else k_labs<false, true><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    launch<false>(gk, few, B, O, perm, kbeg, kcnt, err, s);
     kt.mark("labs_scan", s);
     size_t tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
     kt.mark("labs", s);
-    if (tier == 0) k_labs<true, false><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
-    else k_labs<true, true><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    launch<true>(gk, few, B, O, perm, kbeg, kcnt, err, s);
     kt.mark("labs_pos", s);
     k_labs_pos<<<1024, 256, 0, s>>>(D, B, O);
     kt.mark(nullptr, s);
