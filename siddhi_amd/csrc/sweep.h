@@ -1693,7 +1693,9 @@ struct SweepState {
     // k_sw_lean: one f2 term `e2.v OP B` in the column's own type (float / int32), one of the six
     // standard comparisons; the pair layouts without nulls are checked per push (run)
     lean_opc = 0;
-    if (D.f2.n == 1 && (ct == 1 || ct == 2) && !D.f2.t[0].flt && D.vtag != T_NULL && !getenv("SHP_NO_LEAN"))
+    // (batch indices below 2^31: e1's filter rides in the index's top bit)
+    if (D.f2.n == 1 && (ct == 1 || ct == 2) && !D.f2.t[0].flt && D.vtag != T_NULL && cap < (1ll << 31) &&
+        !getenv("SHP_NO_LEAN"))
       lean_opc = sw_opclass(D.f2.t[0].mask);
     int64_t ninit = std::max<int64_t>(nown, (int64_t)nown * SW_LK);
     k_sw_init<<<(unsigned)((ninit + 255) / 256), 256, 0, s>>>(D);

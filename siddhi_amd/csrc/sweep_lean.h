@@ -42,7 +42,8 @@ constexpr int SL_CHUNK = SL_THREADS * SL_R;   // 2048
 constexpr int SL_CCAP = 384;                  // carried candidates per owner (<= SWS_CCAP)
 constexpr int SL_EMAX = SL_CHUNK + SL_CCAP;
 constexpr int SL_PAD = 16;                    // sentinel positions past E (probe reads)
-constexpr int SL_WL = 128;                    // worklist entries per wave
+constexpr int SL_WL = 120;                    // worklist entries per wave (drained from SL_WLD on)
+constexpr int SL_WLD = 56;
 constexpr int SL_NEAR = 24;                   // closer distances kept as bits
 static_assert(SL_CCAP <= SWS_CCAP, "lean carry must fit the HBM carry arrays");
 
@@ -50,7 +51,8 @@ struct SwLeanSmem {
   int2 tv[SL_EMAX + SL_PAD];         // (ts - chunk base, value) by sorted position; later x = output offset
   uint32_t ref[SL_EMAX];             // batch index, or carry slot (carried)
   uint32_t cl[SL_EMAX];              // closers of this position: distance bits | far count << 24
-  uint16_t lkf[SL_EMAX + SL_PAD];    // local key | carried | e1's filter
+  uint32_t meta[SL_EMAX + SL_PAD];   // local key | key run end << 8 | first event of the run << 20
+                                     // (carried: position < first event; e1's filter: ref bit 31)
   int16_t m[SL_EMAX];                // >= 0 closing position, -1 expired, -2 open, -3 not a candidate
   uint16_t wc[SL_WAVES][256];        // per-wave rank counters, then write cursors
   uint32_t binoff[257];              // key run starts (then, at the end, key-order carry offsets)
@@ -69,6 +71,7 @@ struct SwLeanSmem {
   uint32_t wt[SL_WAVES], wb[SL_WAVES];  // matches per wave in the chunk, and their offsets
   unsigned long long gbase;           // the chunk's output range (one global atomic per chunk)
   int32_t done;                       // waves through the chunk's reservation step
+  int32_t scanner[2];                 // the wave that runs the scan step of even / odd chunks
   int32_t flag;
 };
 
@@ -140,6 +143,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   if (tid == 0) {
     S.flag = 0;
     S.done = 0;
+    S.scanner[0] = S.scanner[1] = 0;
     S.cn[0] = nc0;
     S.cn[1] = 0;
   }
@@ -182,8 +186,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         later = (uint32_t)__popc(c & 0xFFFFFFu);
         for (int p2 = p + 1; p2 < q - SL_NEAR; p2++) later += S.m[p2] == q ? 1u : 0u;
       }
-      const uint32_t r = S.ref[p], rq = S.ref[q];
-      const int64_t si = (S.lkf[p] & SW_LKF_CAR) ? S.cseq[pc][r] : bseq(B, r);
+      const uint32_t r = S.ref[p] & 0x7FFFFFFFu, rq = S.ref[q] & 0x7FFFFFFFu;
+      const int64_t si = p < (int)(S.meta[p] >> 20) ? S.cseq[pc][r] : bseq(B, r);
       const int64_t sq = bseq(B, rq);
       const uint64_t slot = gb + (uint32_t)S.tv[q].x + (sl_closes(c) - 1u - later);
       if (slot < (uint64_t)O.cap) {
@@ -215,7 +219,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   } while (0)
 #endif
   __syncthreads();
-  for (int64_t cb = rb; cb < re; cb += SL_CHUNK) {
+  int ci = 0;  // chunk counter (the scanner of a chunk is chosen by the one before)
+  for (int64_t cb = rb; cb < re; cb += SL_CHUNK, ci++) {
     const int nchunk = (int)min((int64_t)SL_CHUNK, re - cb);
     const int nx = cur ^ 1;
     const int32_t tb32 = (int32_t)(uint32_t)tbk;  // chunk base, batch-relative (|.| < 2^30)
@@ -243,8 +248,9 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     if (cb != rb) emit(pPS, pPE, pcur);  // the previous chunk's matches
     SL_STAMP(1);
     const int E = S.cn[cur] + nchunk;
-    // 2. key run offsets and the wave split (wave 0)
-    if (w == 0) {
+    // 2. key run offsets and the wave split (one wave: the one with the least to emit, the
+    //    previous chunk's scanner picked it from that chunk's split)
+    if ((int)w == S.scanner[ci & 1]) {
       uint32_t run = 0;
       int32_t psv[SL_WAVES];
 #pragma unroll
@@ -296,6 +302,20 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         for (int k = 1; k < SL_WAVES; k++) pv = (uint32_t)k == lane ? psv[k] : pv;
         S.ps[lane] = pv < 0 ? E : pv;
       }
+      if (lane == 0) {  // the next chunk's scanner: the wave with the smallest range of this chunk
+        int best = 0, bl = 1 << 30, prev = 0;
+#pragma unroll
+        for (int k = 0; k < SL_WAVES; k++) {
+          const int nxt = k + 1 < SL_WAVES ? (psv[k + 1] < 0 ? E : psv[k + 1]) : E;
+          const int len = nxt - prev;
+          if (len < bl) {
+            bl = len;
+            best = k;
+          }
+          prev = nxt;
+        }
+        S.scanner[(ci + 1) & 1] = best;
+      }
     }
     __syncthreads();  // B
     SL_STAMP(2);
@@ -307,8 +327,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       const int32_t rel = (int32_t)(uint32_t)pf[s].kt - tb32;
       if (rel > (int32_t)SW_TS_SPAN || rel < -(int32_t)SW_TS_SPAN) S.flag = 1;
       S.tv[p] = make_int2(rel, (int32_t)pf[s].v);
-      S.lkf[p] = (uint16_t)(bin[s] | ((pf[s].kt & SW_F1) ? SW_LKF_F1 : 0u));
-      S.ref[p] = pf[s].ref;
+      S.meta[p] = bin[s] | (S.binoff[bin[s] + 1] << 8) | ((uint32_t)S.fe[bin[s]] << 20);
+      S.ref[p] = pf[s].ref | ((pf[s].kt & SW_F1) ? 0x80000000u : 0u);
     }
     {
       const int ncur = S.cn[cur];
@@ -319,13 +339,13 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         if (r > SW_TS_SPAN) S.flag = 1;  // later than the chunk's span: the exact kernel
         const int32_t crel = r < (int64_t)SW_TS_FLOOR ? SW_TS_FLOOR : (int32_t)r;
         S.tv[p] = make_int2(crel, (int32_t)S.cv[cur][x]);
-        S.lkf[p] = (uint16_t)(lk | SW_LKF_CAR);
+        S.meta[p] = lk | (S.binoff[lk + 1] << 8) | ((uint32_t)S.fe[lk] << 20);
         S.ref[p] = (uint32_t)x;
       }
     }
     if (tid < SL_PAD) {
       S.tv[E + tid] = make_int2(0, 0);
-      S.lkf[E + tid] = (uint16_t)SW_LKF_NONE;
+      S.meta[E + tid] = SW_LKF_NONE;
     }
     if (tid == 0) S.cn[nx] = 0;
     {  // prefetch the next chunk while this one is solved
@@ -368,8 +388,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
           p = (int)(ent & 0xFFFFu);
           qn = ent >> 16;
           const int2 a = S.tv[p];
-          const uint32_t lk = S.lkf[p] & 0xFFu;
-          const int end = (int)S.binoff[lk + 1];
+          const int end = (int)((S.meta[p] >> 8) & 0xFFFu);
           const T bv = bconst ? bc : sw_val<CT>((uint32_t)a.y, 0.0, 0.0, false);
           res = sl_probe<CT, OPC, SW_P2>(S.tv, (int)qn, end, a.x, W, bv);
           qn += SW_P2;
@@ -389,14 +408,20 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       int res = -3;
       uint32_t qn = 0;
       if (p < PE) {
-        const uint32_t f = S.lkf[p];
+        // all of a position's facts in independent loads: its meta word (key, run end, first
+        // event), its (ts, value), its ref (e1's filter in bit 31) and the previous position's
+        const uint32_t mt = S.meta[p];
         const int2 a = S.tv[p];
-        const uint32_t lk = f & 0xFFu;
-        const int beg = (int)S.binoff[lk], end = (int)S.binoff[lk + 1], fe = (int)S.fe[lk];
-        if (p == beg) S.ncar[lk] = 0;  // recounted by the carry step below
-        if (p == end - 1 && p >= fe) S.lastc[lk] = (f & SW_LKF_F1) ? 1 : 0;
-        if (p > beg && S.tv[p - 1].x > a.x) S.flag = 1;  // ts decrease within the key: exact kernel
-        if (f & (SW_LKF_CAR | SW_LKF_F1)) {
+        const bool f1 = (S.ref[p] >> 31) != 0;
+        const uint32_t mprev = p > 0 ? S.meta[p - 1] : 0xFFFFFFFFu;
+        const int tprev = p > 0 ? S.tv[p - 1].x : 0;
+        const uint32_t lk = mt & 0xFFu;
+        const int end = (int)((mt >> 8) & 0xFFFu), fe = (int)(mt >> 20);
+        const bool first = (mprev & 0xFFu) != lk;  // the key run starts here
+        if (first) S.ncar[lk] = 0;  // recounted by the carry step below
+        if (p == end - 1 && p >= fe) S.lastc[lk] = f1 ? 1 : 0;
+        if (!first && tprev > a.x) S.flag = 1;  // ts decrease within the key: exact kernel
+        if (p < fe || f1) {  // carried, or e1's filter
           const T bv = bconst ? bc : sw_val<CT>((uint32_t)a.y, 0.0, 0.0, false);
           const int q0 = max(p + 1, fe);
           res = sl_probe<CT, OPC, SW_P1>(S.tv, q0, end, a.x, W, bv);
@@ -409,7 +434,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       if (unres) wl[nwl + (uint32_t)__popcll(um & lt)] = (uint32_t)p | (qn << 16);
       else if (p < PE) record(p, res);
       nwl += (uint32_t)__popcll(um);
-      if (nwl >= 64) nwl = drain(nwl);
+      if (nwl >= SL_WLD) nwl = drain(nwl);
     }
     while (nwl > 0) nwl = drain(nwl);
     SL_STAMP(4);
@@ -459,9 +484,9 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         if (S.m[q] == -2) {
           const int x = cbase + (int)oo;
           if (x < SL_CCAP) {
-            const uint32_t f = S.lkf[q];
-            const uint32_t r = S.ref[q];
-            if (f & SW_LKF_CAR) {
+            const uint32_t f = S.meta[q];
+            const uint32_t r = S.ref[q] & 0x7FFFFFFFu;
+            if (q < (int)(f >> 20)) {  // carried
               S.cts[nx][x] = S.cts[cur][r];
               S.cv[nx][x] = S.cv[cur][r];
               S.cseq[nx][x] = S.cseq[cur][r];
