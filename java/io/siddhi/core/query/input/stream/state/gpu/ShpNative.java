@@ -76,6 +76,8 @@ final class ShpNative {
     static final MethodHandle SNAPSHOT_DESCRIBE = fn("shp_snapshot_describe", JAVA_LONG, ADDRESS, ADDRESS, JAVA_LONG,
             ADDRESS, JAVA_LONG);
     static final MethodHandle NUM_STATES = fn("shp_engine_num_states", JAVA_INT, ADDRESS);
+    static final MethodHandle ENGINE_PATH = fn("shp_engine_path", JAVA_INT, ADDRESS);
+    static final MethodHandle ENGINE_STAT = fn("shp_engine_stat", JAVA_LONG, ADDRESS, ADDRESS);  // monitoring counters
     static final MethodHandle LAST_ERROR = fn("shp_last_error", ADDRESS, ADDRESS);
     static final MethodHandle ENGINE_DESTROY = fnVoid("shp_engine_destroy", ADDRESS);
 
