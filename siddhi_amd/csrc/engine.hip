@@ -345,7 +345,7 @@ struct shp_engine {
   int lds_lanes = 0;
   double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
   int64_t last_m = 0;
-  int64_t pushes = 0, lean_pushes = 0, lean_fallbacks = 0;  // shp_engine_stat
+  int64_t pushes = 0, lean_pushes = 0, lean_fallbacks = 0, labs_fallbacks = 0;  // shp_engine_stat
 
   ~shp_engine() { release(); }
 
@@ -662,6 +662,20 @@ struct shp_engine {
       HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
       sw.solve(B, O, d_err, stream, kt);
       if (cfg.match_layout == SHP_LAYOUT_FULL) sw.expand(B, x_key, O, stream, kt);
+      HIP_OK(hipEventRecord(ev2, stream));
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      std::memcpy(&herr, h_status + 2, sizeof(int));
+    }
+    if (fast == 4 && (herr & LA_SLOW) && !(herr & SWE_KEYS)) {
+      // k_labs_w handed the push back (a key with more than 64 pairs waiting at once): k_labs
+      // re-runs it over the same partition from the same committed state
+      labs_fallbacks++;
+      HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
+      la.slow = true;
+      la.run(B, O, d_perm, d_kbeg, d_kcnt, d_err, d_tmp, tmp_bytes, stream, kt);
+      la.slow = false;
       HIP_OK(hipEventRecord(ev2, stream));
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
@@ -1423,6 +1437,7 @@ int64_t shp_engine_stat(const shp_engine* e, const char* which) {
   if (w == "pushes") return e->pushes;
   if (w == "lean_pushes") return e->lean_pushes;
   if (w == "lean_fallbacks") return e->lean_fallbacks;
+  if (w == "labs_fallbacks") return e->labs_fallbacks;
   return -1;
 }
 

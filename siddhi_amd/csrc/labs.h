@@ -365,6 +365,268 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
   if (e) atomicOr(err, e);
 }
 
+// ------------------------------------------------------------------ k_labs_w: a wave per key
+// The same rule with the key's events taken 64 at a time (one per lane), for filters of x and y
+// that read only their own event (LabsState::wave_ok; C4's `S1[price>20]`, `S2[price>20]`):
+//   pend    wave-uniform scalars stepped from event to event with ballots: from an empty partial
+//           the next qualifying X or Y fills its slot; from a half partial filled at t0 the pair
+//           completes at the next qualifying partner unless an event later than t0 + W comes first
+//           (that event resets the partial and is then taken from empty) -- one loop trip per
+//           fill, completion or reset, not per event;
+//   waits   one lane per waiting pair (FIFO in LDS, at most 64): the pair fires at the first event
+//           after its completion whose clock reaches the due time (monotone clock: a scan of the
+//           64 clocks), and dies at a Z event between completion and firing whose filter holds.
+//           Firing follows completion order, so the emitted records keep the FIFO order.
+// More than 64 waiting pairs in a key raise LA_SLOW: the engine re-runs the push with k_labs.
+constexpr int LA_SLOW = 1 << 28;
+
+__device__ __forceinline__ int64_t la_rl64(int64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
+                                               const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
+                                               int* err) {
+  __shared__ LaWait A[64];  // waiting pairs, completion order
+  __shared__ int32_t Ac[64];  // completing lane in the current block (-1: an earlier block)
+  const int k = blockIdx.x;
+  if (k >= D.nk) return;
+  const int lane = (int)threadIdx.x;
+  const uint64_t lt = sw_lanemask_lt();
+  const int rd = D.cur, wr = rd ^ 1;
+  const int cap = D.wcap, msk = cap - 1;
+  const LaPend s0 = D.pend[rd][k];
+  int nal = s0.nw;
+  if (nal > 64) {
+    if (lane == 0) atomicOr(err, LA_SLOW);
+    return;
+  }
+  if (lane < nal) {
+    A[lane] = D.wq[rd][(int64_t)k * cap + ((s0.wh + lane) & msk)];
+    Ac[lane] = -1;
+  }
+  const uint32_t beg = kbeg[k], cnt = kcnt[k];
+  const bool useW = D.within >= 0;
+  const int64_t Wn = D.within, Tw = D.wait;
+  const int8_t t0g = D.tag[0], t1g = D.tag[1], t2g = D.tag[2];
+  int e = 0;
+  int64_t mi = 0;
+  uint32_t nm = 0;
+  if (EMIT) {
+    mi = D.om[k];
+    if (k == D.nk - 1 && lane == 0) {
+      O.count[0] = (unsigned long long)(mi + D.cm[k]);
+      O.count[1] = 2ull * (unsigned long long)(mi + D.cm[k]);
+    }
+  }
+  // the logical partial (wave-uniform)
+  bool hx = s0.xseq >= 0, hy = s0.yseq >= 0;
+  int64_t xseq = s0.xseq, xts = s0.xts, yseq = s0.yseq, yts = s0.yts;
+  uint32_t xv = s0.xv, yv = s0.yv, fl = s0.fl;
+  int64_t last = s0.last;
+  int64_t lo = 0;  // first batch index a timer can fire at (after the key's previous event)
+  // one waiting pair per lane: fire (f < nv: at event f of the block; f == 64: the push's end)
+  // unless killed, then compact the survivors
+  auto settle = [&](bool fired, bool killed, int64_t flo, int64_t fhi, const LaWait& w) {
+    const bool ok = lane < nal && fired && !killed &&
+                    (!useW || (llabs(w.xts - w.due) <= Wn && llabs(w.yts - w.due) <= Wn));
+    const uint64_t em = __ballot(ok);
+    if (EMIT && ok) {
+      const int64_t m = mi + __popcll(em & lt);
+      if (m >= O.cap || 2 * m + 2 > O.refcap) {
+        e |= E_OUT;
+      } else {
+        O.key[m] = B.partitioned ? k : 0;
+        O.ts[m] = w.due;
+        O.type[m] = 0;
+        O.pos[m] = flo;
+        D.aux[m] = fhi;
+        O.ref_off[m] = 2 * m;
+        int64_t r = 2 * m;
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          const bool isx = q == D.sid[0], isy = q == D.sid[1];
+          O.slot_len[m * MAXS + q] = (int16_t)((isx || isy) ? 1 : 0);
+          if (isx) O.refs[r++] = w.xseq;
+          if (isy) O.refs[r++] = w.yseq;
+        }
+      }
+    }
+    mi += __popcll(em);
+    nm += (uint32_t)__popcll(em);
+    const bool surv = lane < nal && !fired && !killed;
+    const uint64_t sm = __ballot(surv);
+    __syncthreads();  // every lane holds its pair before the compaction writes
+    if (surv) {
+      const int d = __popcll(sm & lt);
+      A[d] = w;
+      Ac[d] = -1;
+    }
+    nal = __popcll(sm);
+    __syncthreads();
+  };
+  for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
+    const int nv = (int)min(64u, cnt - j0);
+    const bool valid = lane < nv;
+    const int64_t i = (int64_t)beg + j0 + lane;
+    const int64_t ts = valid ? D.s_ts[i] : 0, clk = valid ? D.s_clk[i] : 0;
+    const uint32_t g = valid ? perm[i] : 0u, v = valid ? D.s_v[i] : 0u;
+    const int32_t st = valid ? D.s_st[i] : -1;
+    const bool en = valid ? D.s_n[i] != 0 : true;
+    const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
+    {  // timestamps must not decrease within the key
+      const int64_t tp = __shfl_up(ts, 1, 64);
+      const int64_t prev = lane == 0 ? last : tp;
+      if (valid && prev != INT64_MIN && ts < prev) e |= LA_UNORDERED;
+    }
+    const int64_t seqg = bseq(B, g);
+    const LaVals V0{v, v, 0u, en, en, true, t0g, t1g, t2g};
+    const uint64_t QX = __ballot(valid && role == 0 && la_pred(D.fx, V0));
+    const uint64_t QY = __ballot(valid && role == 1 && la_pred(D.fy, V0));
+    // 1. the partial, fill by fill
+    int p = 0;
+    while (p < nv) {
+      const uint64_t ge = ~0ull << p;
+      if (!hx && !hy) {
+        const uint64_t m = (QX | QY) & ge;
+        if (!m) break;
+        const int a = __builtin_ctzll(m);
+        const uint32_t an = (uint32_t)__builtin_amdgcn_readlane((int)en, a);
+        if ((QX >> a) & 1ull) {
+          hx = true;
+          xseq = la_rl64(seqg, a);
+          xts = la_rl64(ts, a);
+          xv = (uint32_t)__builtin_amdgcn_readlane((int)v, a);
+          fl = (fl & ~1u) | (an ? 1u : 0u);
+        } else {
+          hy = true;
+          yseq = la_rl64(seqg, a);
+          yts = la_rl64(ts, a);
+          yv = (uint32_t)__builtin_amdgcn_readlane((int)v, a);
+          fl = (fl & ~2u) | (an ? 2u : 0u);
+        }
+        p = a + 1;
+      } else {
+        const int64_t tf = hx ? xts : yts;
+        const uint64_t Em = useW ? (__ballot(valid && ts - tf > Wn) & ge) : 0ull;
+        const uint64_t Om = (hx ? QY : QX) & ge;
+        const int z = Em ? __builtin_ctzll(Em) : 64, b = Om ? __builtin_ctzll(Om) : 64;
+        if (b < z) {  // the partner: the pair completes and waits on the absent state
+          if (nal >= 64) {
+            if (lane == 0) atomicOr(err, LA_SLOW);
+            return;
+          }
+          const uint32_t bn = (uint32_t)__builtin_amdgcn_readlane((int)en, b);
+          const int64_t bseqv = la_rl64(seqg, b), bts = la_rl64(ts, b);
+          const uint32_t bv = (uint32_t)__builtin_amdgcn_readlane((int)v, b);
+          if (hx) {
+            yseq = bseqv;
+            yts = bts;
+            yv = bv;
+            fl = (fl & ~2u) | (bn ? 2u : 0u);
+          } else {
+            xseq = bseqv;
+            xts = bts;
+            xv = bv;
+            fl = (fl & ~1u) | (bn ? 1u : 0u);
+          }
+          if (lane == 0) {
+            LaWait w;
+            w.due = bts + Tw;
+            w.xseq = xseq;
+            w.xts = xts;
+            w.yseq = yseq;
+            w.yts = yts;
+            w.xv = xv;
+            w.yv = yv;
+            w.fl = fl;
+            w.pad = 0;
+            A[nal] = w;
+            Ac[nal] = b;
+          }
+          nal++;
+          hx = hy = false;
+          xseq = yseq = -1;
+          fl = 0;
+          p = b + 1;
+        } else if (z < 64) {  // expired (StreamPreStateProcessor.expireEvents): event z starts afresh
+          hx = hy = false;
+          xseq = yseq = -1;
+          fl = 0;
+          p = z;
+        } else {
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    // 2. the waiting pairs against this block's events
+    if (nal > 0) {
+      LaWait w{};
+      int c = 64;
+      if (lane < nal) {
+        w = A[lane];
+        c = Ac[lane];
+      }
+      int f = 64;  // first event after c whose clock reaches the due time
+      for (int q = 0; q < nv; q++) {
+        const int64_t cq = la_rl64(clk, q);
+        if (f == 64 && q > c && cq >= w.due) f = q;
+      }
+      bool killed = false;
+      uint64_t zm = __ballot(valid && role == 2);
+      while (zm) {
+        const int z = __builtin_ctzll(zm);
+        zm &= zm - 1;
+        const uint32_t zv = (uint32_t)__builtin_amdgcn_readlane((int)v, z);
+        const bool zn = __builtin_amdgcn_readlane((int)en, z) != 0;
+        if (lane < nal && !killed && z > c && z < f) {
+          const LaVals V{w.xv, w.yv, zv, (w.fl & 1u) != 0, (w.fl & 2u) != 0, zn, t0g, t1g, t2g};
+          killed = la_pred(D.fz, V);
+        }
+      }
+      const bool fired = f < 64;
+      const int64_t gp = (int64_t)(uint32_t)__shfl(g, f > 0 ? f - 1 : 0, 64);
+      const int64_t gf = (int64_t)(uint32_t)__shfl(g, f < 64 ? f : 0, 64);
+      settle(fired, killed, f == 0 ? lo : gp + 1, gf, w);
+    }
+    lo = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)g, nv - 1) + 1;
+    last = la_rl64(ts, nv - 1);
+  }
+  // the timers the push's last clock reaches
+  if (nal > 0) {
+    LaWait w{};
+    if (lane < nal) w = A[lane];
+    const int64_t lastclk = B.n > 0 ? B.rmax[B.n - 1] : INT64_MIN;
+    settle(lane < nal && w.due <= lastclk, false, lo, B.n - 1, w);
+  }
+  if (!EMIT) {
+    if (lane == 0) D.cm[k] = nm;
+    if (e) atomicOr(err, e);
+    return;
+  }
+  if (nal > cap) e |= E_LIST;
+  else if (lane < nal) D.wq[wr][(int64_t)k * cap + lane] = A[lane];
+  if (lane == 0) {
+    LaPend s{};
+    s.xseq = hx ? xseq : -1;
+    s.yseq = hy ? yseq : -1;
+    s.xts = xts;
+    s.yts = yts;
+    s.xv = xv;
+    s.yv = yv;
+    s.fl = fl;
+    s.nw = nal;
+    s.wh = 0;
+    s.last = last;
+    D.pend[wr][k] = s;
+  }
+  if (e) atomicOr(err, e);
+}
+
 // the event that fired each timer record of the push: the first batch index in [pos, aux] whose
 // running clock reaches the record's due time (the playback clock is non-decreasing)
 __global__ void k_labs_pos(LabsDev D, BatchView B, MatchOut O) {
@@ -407,6 +669,8 @@ __global__ void k_labs_init(LabsDev D) {
 struct LabsState {
   LabsDev D{};
   int tier = 0;
+  bool wave_ok = false;  // k_labs_w applies: x's and y's filters read only their own event
+  bool slow = false;     // this push re-runs on k_labs (k_labs_w raised LA_SLOW)
 
   static bool lower_term(const LaTermS& t, const LabsShape& sh, const DevProg& P, LaTermD& o) {
     static const int32_t masks[6] = {4, 6, 1, 3, 2, 13};  // gt ge lt le eq ne
@@ -476,6 +740,13 @@ struct LabsState {
     al(D.s_n, cap);
     D.wcap = LA_CAPS[0];
     tier = 0;
+    auto own = [](const LaPredD& p, int kind) {
+      for (int i = 0; i < p.n; i++)
+        for (int8_t kk : {p.t[i].ak, p.t[i].bk})
+          if (kk != 0 && kk != kind) return false;
+      return true;
+    };
+    wave_ok = own(D.fx, 1) && own(D.fy, 2) && !getenv("SHP_NO_LABS_W");
     k_labs_init<<<(unsigned)((max_keys + 255) / 256), 256, 0, s>>>(D);
   }
 
@@ -497,13 +768,16 @@ struct LabsState {
     const unsigned gk = few ? (unsigned)D.nk : (unsigned)((D.nk + 63) / 64);
     kt.mark("labs_gather", s);
     if (B.n > 0) k_labs_gather<<<2048, 256, 0, s>>>(D, B, perm, B.n);
+    const bool wv = wave_ok && !slow;
     kt.mark("labs_count", s);
-    launch<false>(gk, few, B, O, perm, kbeg, kcnt, err, s);
+    if (wv) k_labs_w<false><<<(unsigned)D.nk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    else launch<false>(gk, few, B, O, perm, kbeg, kcnt, err, s);
     kt.mark("labs_scan", s);
     size_t tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
     kt.mark("labs", s);
-    launch<true>(gk, few, B, O, perm, kbeg, kcnt, err, s);
+    if (wv) k_labs_w<true><<<(unsigned)D.nk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    else launch<true>(gk, few, B, O, perm, kbeg, kcnt, err, s);
     kt.mark("labs_pos", s);
     k_labs_pos<<<1024, 256, 0, s>>>(D, B, O);
     kt.mark(nullptr, s);

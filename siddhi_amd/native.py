@@ -261,7 +261,7 @@ class HipEngine:
         return lib().shp_last_kernel_ms(self.h, which.encode())
 
     def stat(self, which):
-        """shp_engine_stat: "pushes" or "lean_fallbacks"."""
+        """shp_engine_stat: "pushes", "lean_pushes", "lean_fallbacks" or "labs_fallbacks"."""
         return int(lib().shp_engine_stat(self.h, which.encode()))
 
     def close(self):

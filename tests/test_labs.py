@@ -6,8 +6,10 @@ completed pairs in completion order, each firing at the first event whose playba
 completion ts + T), against the oracle's object-level restatement of the Logical / AbsentStream
 processors and the playback Scheduler (oracle/oracle.cpp) -- the C4 stream at several key counts,
 and dense random streams with ties in no due time (cross-key scheduler ties are parity-unpinned,
-SURVEY.md §8c).  GPU (`-m gpu`): k_labs + k_labs_pos against the oracle, split pushes, a clock
-advanced with no event, snapshot/restore, and the refusal of out-of-order timestamps.
+SURVEY.md §8c), and k_labs_w's block-at-a-time formulation against that rule.  GPU (`-m gpu`):
+k_labs_w / k_labs + k_labs_pos against the oracle, split pushes, a clock advanced with no event,
+snapshot/restore, the hand-back of keys with more than 64 waiting pairs, and the refusal of
+out-of-order timestamps.
 """
 from collections import deque
 
@@ -49,6 +51,81 @@ def model(ts, key, st, pr):
     return out
 
 
+def wave_model(ts, key, st, pr, block=64):
+    """k_labs_w's formulation of the same rule (labs.h): per key, events taken `block` at a time;
+    the partial jumps fill -> completion / reset with first-set-bit searches over the block, and
+    each waiting pair fires at the first later event whose clock reaches its due time unless a Z
+    event before that kills it.  Must equal `model` exactly."""
+    n = len(ts)
+    clock = np.maximum.accumulate(np.asarray(ts, np.int64))
+    runs = {}
+    for g in range(n):
+        runs.setdefault(int(key[g]), []).append(g)
+    out = {}
+    for k, idx in runs.items():
+        pend = {"e1": None, "e2": None}
+        alive = []  # [due, e1, e2, c]
+        lo = 0
+        recs = out.setdefault(k, [])
+
+        def settle(fires):
+            nonlocal alive
+            keep = []
+            for w, (f, killed, flo, fhi) in zip(alive, fires):
+                if f and not killed:
+                    due, e1, e2, _ = w
+                    if abs(e1[1] - due) <= W and abs(e2[1] - due) <= W:
+                        g = next(x for x in range(flo, fhi + 1) if clock[x] >= due)
+                        recs.append((due, 0, g, ((e2[0],), (e1[0],), ())))
+                elif not f and not killed:
+                    keep.append([w[0], w[1], w[2], -1])
+            alive = keep
+
+        for j0 in range(0, len(idx), block):
+            blk = idx[j0:j0 + block]
+            nv = len(blk)
+            qx = [int(st[g]) == 0 and float(pr[g]) > 20 for g in blk]
+            qy = [int(st[g]) == 1 and float(pr[g]) > 20 for g in blk]
+            p = 0
+            while p < nv:
+                if pend["e1"] is None and pend["e2"] is None:
+                    a = next((q for q in range(p, nv) if qx[q] or qy[q]), None)
+                    if a is None:
+                        break
+                    g = blk[a]
+                    pend["e1" if qx[a] else "e2"] = (g, int(ts[g]), float(pr[g]))
+                    p = a + 1
+                else:
+                    slot, other, q_o = ("e1", "e2", qy) if pend["e1"] is not None else ("e2", "e1", qx)
+                    t0 = pend[slot][1]
+                    z = next((q for q in range(p, nv) if int(ts[blk[q]]) - t0 > W), nv)
+                    b = next((q for q in range(p, nv) if q_o[q]), nv)
+                    if b < z:
+                        g = blk[b]
+                        pend[other] = (g, int(ts[g]), float(pr[g]))
+                        alive.append([int(ts[g]) + WAIT, pend["e1"], pend["e2"], b])
+                        pend = {"e1": None, "e2": None}
+                        p = b + 1
+                    elif z < nv:
+                        pend = {"e1": None, "e2": None}
+                        p = z
+                    else:
+                        break
+            fires = []
+            for due, e1, e2, c in alive:
+                f = next((q for q in range(c + 1, nv) if clock[blk[q]] >= due), None)
+                end = nv if f is None else f
+                killed = any(int(st[blk[q]]) == 2 and float(pr[blk[q]]) > e1[2] for q in range(c + 1, end))
+                flo = (lo if f == 0 else blk[f - 1] + 1) if f is not None else 0
+                fires.append((f is not None, killed, flo, blk[f] if f is not None else 0))
+            settle(fires)
+            lo = blk[-1] + 1
+        settle([(due <= clock[n - 1], False, lo, n - 1) for due, *_ in alive])
+        if not recs:
+            del out[k]
+    return out
+
+
 def _oracle(cq, ts, key, st, pr, batch):
     e = OracleEngine(cq.program_json(), 0)
     for lo in range(0, len(ts), batch):
@@ -82,6 +159,34 @@ def test_model_matches_oracle_dense_random(keys, step):
     assert sum(len(x) for x in want.values()) > 5
 
 
+@pytest.mark.parametrize("block", [64, 5])
+@pytest.mark.parametrize("keys,step", [(1, 400), (3, 2), (20, 7), (100, 1)])
+def test_wave_formulation_matches_model(keys, step, block):
+    """k_labs_w's block-at-a-time formulation (fills/completions/resets by first-set-bit searches,
+    fire and kill per waiting pair) reproduces the event-by-event rule, at the kernel's 64-event
+    blocks and at 5-event blocks (many block boundaries)."""
+    rng = np.random.default_rng(keys * 7 + step + block)
+    n = 20_000
+    ts = (np.arange(n) * step).astype(np.int64) + 1000
+    if keys > 1:  # runs of equal ts, and gaps beyond W (partials reset)
+        ts = np.sort(ts - rng.integers(0, 3, n) + np.cumsum(rng.random(n) < 0.002) * 30_000)
+    key = rng.integers(0, keys, n).astype(np.int32)
+    st = rng.integers(0, 3, n).astype(np.int32)
+    pr = (rng.integers(0, 10000, n) / 100.0).astype(np.float32)
+    want = model(ts, key, st, pr)
+    got = wave_model(ts, key, st, pr, block)
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > (0 if keys == 1 else 5)
+
+
+def test_wave_formulation_c4_stream():
+    g = small_stream(4, 60_000, 50)
+    pr = g["price"].astype(np.float32)
+    want = model(g["ts"], g["key"], g["stream"], pr)
+    got = wave_model(g["ts"], g["key"], g["stream"], pr)
+    assert compare(want, got) is None, compare(want, got)
+
+
 # ---------------------------------------------------------------- GPU (k_labs)
 
 def _hip(cq, keys, batch, **kw):
@@ -101,6 +206,21 @@ def test_c4_labs_vs_oracle(keys, n, batch):
     got = per_key(run(eng, cq, g, batch))
     assert compare(want, got) is None, compare(want, got)
     assert sum(len(x) for x in want.values()) > (0 if keys == 1 else 20)
+    if keys > 1:  # k_labs_w ran every push (no key had more than 64 pairs waiting)
+        assert eng.stat("labs_fallbacks") == 0
+
+
+@pytest.mark.gpu
+def test_c4_wave_kernel_equals_thread_kernel(monkeypatch):
+    """k_labs_w (a wave per key) and k_labs (SHP_NO_LABS_W: a thread per key) write the same
+    records on the C4 stream, split over pushes."""
+    cq = program_for(4)
+    g = small_stream(4, 400_000, 500)
+    a = per_key(run(_hip(cq, 500, 65_537), cq, g, 65_537))
+    monkeypatch.setenv("SHP_NO_LABS_W", "1")
+    b = per_key(run(_hip(cq, 500, 65_537), cq, g, 65_537))
+    assert compare(a, b) is None, compare(a, b)
+    assert sum(len(x) for x in a.values()) > 100
 
 
 @pytest.mark.gpu
@@ -182,3 +302,21 @@ def test_labs_rings_grow_and_snapshot_carries_the_tier():
     got = per_key(_concat([first, second], None, a.S))
     assert compare(want, got) is None, compare(want, got)
     assert sum(len(x) for x in want.values()) > 0
+
+
+@pytest.mark.gpu
+def test_labs_hands_back_keys_with_many_waiting_pairs():
+    """No Z event and a pair every 2 ms on one key: ~2500 pairs wait at once, beyond k_labs_w's
+    64, so the pushes go to k_labs (and its rings grow to the 4096 tier); still exact."""
+    cq = program_for(4)
+    n = 30_000
+    rng = np.random.default_rng(5)
+    g = {"ts": np.arange(n, dtype=np.int64) + 10_000, "key": np.zeros(n, np.int32),
+         "stream": rng.integers(0, 2, n).astype(np.int32),
+         "price": (50 + rng.integers(0, 1000, n) / 100.0).astype(np.float32)}
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g, 10_000))
+    eng = _hip(cq, 1, 10_000)
+    got = per_key(run(eng, cq, g, 10_000))
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 5000
+    assert eng.stat("labs_fallbacks") > 0
