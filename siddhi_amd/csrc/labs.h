@@ -76,6 +76,13 @@ struct __attribute__((aligned(8))) LaWait {
   uint32_t pad;
 };
 
+// one record of k_labs_w, in the key's region of LabsDev::rec (ceil(kbeg / 2) + 65 k: a key's
+// push completes at most ceil(cnt / 2) pairs, and at most 64 were waiting before it)
+struct __attribute__((aligned(8))) LaRec {
+  int64_t due, xseq, yseq;
+  uint32_t flo, fhi;  // the fire event is the first batch index in [flo, fhi] whose clock reaches due
+};
+
 struct LaPend {
   int64_t xseq, xts, yseq, yts;  // seq -1: slot empty
   uint32_t xv, yv;
@@ -107,6 +114,7 @@ struct LabsDev {
   int32_t* s_st;
   uint32_t* s_v;
   uint8_t* s_n;
+  LaRec* rec;        // k_labs_w's records, per key region (la_region)
 };
 
 // sorted position i <- batch event perm[i]: ts, clock, stream, and the value of its stream's column
@@ -386,8 +394,47 @@ __device__ __forceinline__ int64_t la_rl64(int64_t x, int l) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-template <bool EMIT>
-__global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
+__host__ __device__ __forceinline__ int64_t la_region(uint32_t kb, int k) { return (int64_t)((kb + 1u) >> 1) + 65ll * k; }
+
+// fz for one waiting pair: the x / y sides of each term converted once (per block), the z side per Z
+struct LaKill {
+  double a[2], b[2];
+  bool nul[2];
+};
+__device__ __forceinline__ LaKill la_kill_pre(const LaPredD& p, const LaWait& w, int8_t t0, int8_t t1, int8_t t2) {
+  LaKill K{};
+  const bool xn = (w.fl & 1u) != 0, yn = (w.fl & 2u) != 0;
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    if (i < p.n) {
+      const LaTermD& t = p.t[i];
+      K.a[i] = la_side(t.ak, t.ac, t.aflt, w.xv, w.yv, 0u, t0, t1, t2);
+      K.b[i] = la_side(t.bk, t.bc, t.bflt, w.xv, w.yv, 0u, t0, t1, t2);
+      K.nul[i] = (t.ak == 1 && xn) || (t.ak == 2 && yn) || (t.bk == 1 && xn) || (t.bk == 2 && yn);
+    }
+  }
+  return K;
+}
+__device__ __forceinline__ bool la_kill(const LaPredD& p, const LaKill& K, double zd0, double zd1, bool zn) {
+  if (p.n == 0) return true;
+  bool r[2] = {false, false};
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    if (i < p.n) {
+      const LaTermD& t = p.t[i];
+      const double A = t.ak == 3 ? (t.aflt ? zd1 : zd0) : K.a[i];
+      const double Bv = t.bk == 3 ? (t.bflt ? zd1 : zd0) : K.b[i];
+      const bool nul = K.nul[i] || ((t.ak == 3 || t.bk == 3) && zn);
+      const int o3 = (A < Bv ? 1 : 0) | (A == Bv ? 2 : 0) | (A > Bv ? 4 : 0);
+      r[i] = !nul && ((o3 | (o3 == 0 ? 8 : 0)) & t.mask) != 0;
+    }
+  }
+  return p.n == 1 ? r[0] : (p.combine ? (r[0] || r[1]) : (r[0] && r[1]));
+}
+
+// one pass: records into the key's region of D.rec, the key's count into D.cm, the state into
+// copy wr; k_labs_out then writes the push's records contiguously
+__global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
                                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                                int* err) {
   __shared__ LaWait A[64];  // waiting pairs, completion order
@@ -409,53 +456,33 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, MatchOut 
     Ac[lane] = -1;
   }
   const uint32_t beg = kbeg[k], cnt = kcnt[k];
+  LaRec* rec = D.rec + la_region(beg, k);
   const bool useW = D.within >= 0;
   const int64_t Wn = D.within, Tw = D.wait;
   const int8_t t0g = D.tag[0], t1g = D.tag[1], t2g = D.tag[2];
   int e = 0;
-  int64_t mi = 0;
   uint32_t nm = 0;
-  if (EMIT) {
-    mi = D.om[k];
-    if (k == D.nk - 1 && lane == 0) {
-      O.count[0] = (unsigned long long)(mi + D.cm[k]);
-      O.count[1] = 2ull * (unsigned long long)(mi + D.cm[k]);
-    }
-  }
   // the logical partial (wave-uniform)
   bool hx = s0.xseq >= 0, hy = s0.yseq >= 0;
   int64_t xseq = s0.xseq, xts = s0.xts, yseq = s0.yseq, yts = s0.yts;
   uint32_t xv = s0.xv, yv = s0.yv, fl = s0.fl;
   int64_t last = s0.last;
   int64_t lo = 0;  // first batch index a timer can fire at (after the key's previous event)
-  // one waiting pair per lane: fire (f < nv: at event f of the block; f == 64: the push's end)
-  // unless killed, then compact the survivors
+  // the waiting pairs (one per lane) fire (fired: in [flo, fhi]) unless killed; the survivors
+  // are compacted in order
   auto settle = [&](bool fired, bool killed, int64_t flo, int64_t fhi, const LaWait& w) {
     const bool ok = lane < nal && fired && !killed &&
                     (!useW || (llabs(w.xts - w.due) <= Wn && llabs(w.yts - w.due) <= Wn));
     const uint64_t em = __ballot(ok);
-    if (EMIT && ok) {
-      const int64_t m = mi + __popcll(em & lt);
-      if (m >= O.cap || 2 * m + 2 > O.refcap) {
-        e |= E_OUT;
-      } else {
-        O.key[m] = B.partitioned ? k : 0;
-        O.ts[m] = w.due;
-        O.type[m] = 0;
-        O.pos[m] = flo;
-        D.aux[m] = fhi;
-        O.ref_off[m] = 2 * m;
-        int64_t r = 2 * m;
-#pragma unroll
-        for (int q = 0; q < 3; q++) {
-          const bool isx = q == D.sid[0], isy = q == D.sid[1];
-          O.slot_len[m * MAXS + q] = (int16_t)((isx || isy) ? 1 : 0);
-          if (isx) O.refs[r++] = w.xseq;
-          if (isy) O.refs[r++] = w.yseq;
-        }
-      }
+    if (ok) {
+      LaRec r;
+      r.due = w.due;
+      r.xseq = w.xseq;
+      r.yseq = w.yseq;
+      r.flo = (uint32_t)flo;
+      r.fhi = (uint32_t)fhi;
+      rec[nm + (uint32_t)__popcll(em & lt)] = r;
     }
-    mi += __popcll(em);
     nm += (uint32_t)__popcll(em);
     const bool surv = lane < nal && !fired && !killed;
     const uint64_t sm = __ballot(surv);
@@ -468,14 +495,30 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, MatchOut 
     nal = __popcll(sm);
     __syncthreads();
   };
+  // the key's events 64 at a time; the next block's loads are issued before this one is worked
+  int64_t n_ts = 0, n_clk = 0;
+  uint32_t n_g = 0, n_v = 0, n_n = 1;
+  int32_t n_st = -1;
+  auto fetch = [&](uint32_t j0) {
+    if (j0 + (uint32_t)lane < cnt) {
+      const int64_t i = (int64_t)beg + j0 + lane;
+      n_ts = D.s_ts[i];
+      n_clk = D.s_clk[i];
+      n_g = perm[i];
+      n_v = D.s_v[i];
+      n_st = D.s_st[i];
+      n_n = D.s_n[i];
+    }
+  };
+  fetch(0);
   for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
     const int nv = (int)min(64u, cnt - j0);
     const bool valid = lane < nv;
-    const int64_t i = (int64_t)beg + j0 + lane;
-    const int64_t ts = valid ? D.s_ts[i] : 0, clk = valid ? D.s_clk[i] : 0;
-    const uint32_t g = valid ? perm[i] : 0u, v = valid ? D.s_v[i] : 0u;
-    const int32_t st = valid ? D.s_st[i] : -1;
-    const bool en = valid ? D.s_n[i] != 0 : true;
+    const int64_t ts = n_ts, clk = n_clk;
+    const uint32_t g = n_g, v = n_v;
+    const int32_t st = valid ? n_st : -1;
+    const bool en = n_n != 0;
+    if (j0 + 64 < cnt) fetch(j0 + 64);
     const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
     {  // timestamps must not decrease within the key
       const int64_t tp = __shfl_up(ts, 1, 64);
@@ -571,22 +614,28 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, MatchOut 
         w = A[lane];
         c = Ac[lane];
       }
-      int f = 64;  // first event after c whose clock reaches the due time
-      for (int q = 0; q < nv; q++) {
-        const int64_t cq = la_rl64(clk, q);
-        if (f == 64 && q > c && cq >= w.due) f = q;
+      // fire event: the first event after c whose clock reaches the due time.  Due times and
+      // completions follow the pair order, so the fire events do too: the first pair that does
+      // not fire in this block ends the search.
+      int f = 64;
+      for (int l = 0; l < nal; l++) {
+        const int64_t dl = la_rl64(w.due, l);
+        const int cl = __builtin_amdgcn_readlane(c, l);
+        const uint64_t m = __ballot(valid && lane > cl && clk >= dl);
+        if (!m) break;
+        if (lane == l) f = __builtin_ctzll(m);
       }
+      // killed: a Z event between completion and firing whose filter holds
       bool killed = false;
+      const LaKill K = la_kill_pre(D.fz, w, t0g, t1g, t2g);
       uint64_t zm = __ballot(valid && role == 2);
       while (zm) {
         const int z = __builtin_ctzll(zm);
         zm &= zm - 1;
         const uint32_t zv = (uint32_t)__builtin_amdgcn_readlane((int)v, z);
         const bool zn = __builtin_amdgcn_readlane((int)en, z) != 0;
-        if (lane < nal && !killed && z > c && z < f) {
-          const LaVals V{w.xv, w.yv, zv, (w.fl & 1u) != 0, (w.fl & 2u) != 0, zn, t0g, t1g, t2g};
-          killed = la_pred(D.fz, V);
-        }
+        const double zd0 = la_val(zv, t2g, false), zd1 = la_val(zv, t2g, true);
+        if (z > c && z < f) killed = killed || la_kill(D.fz, K, zd0, zd1, zn);
       }
       const bool fired = f < 64;
       const int64_t gp = (int64_t)(uint32_t)__shfl(g, f > 0 ? f - 1 : 0, 64);
@@ -603,14 +652,10 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, MatchOut 
     const int64_t lastclk = B.n > 0 ? B.rmax[B.n - 1] : INT64_MIN;
     settle(lane < nal && w.due <= lastclk, false, lo, B.n - 1, w);
   }
-  if (!EMIT) {
-    if (lane == 0) D.cm[k] = nm;
-    if (e) atomicOr(err, e);
-    return;
-  }
   if (nal > cap) e |= E_LIST;
   else if (lane < nal) D.wq[wr][(int64_t)k * cap + lane] = A[lane];
   if (lane == 0) {
+    D.cm[k] = nm;
     LaPend s{};
     s.xseq = hx ? xseq : -1;
     s.yseq = hy ? yseq : -1;
@@ -623,6 +668,51 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, MatchOut 
     s.wh = 0;
     s.last = last;
     D.pend[wr][k] = s;
+  }
+  if (e) atomicOr(err, e);
+}
+
+// k_labs_w's records of each key (its region of D.rec) to the push's output at the key's offset,
+// with the fire event found as k_labs_pos does
+__global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ kbeg,
+                                                  int* err) {
+  const int k = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (k >= D.nk) return;
+  const int lane = (int)(threadIdx.x & 63);
+  const int64_t mi = D.om[k];
+  const uint32_t nm = D.cm[k];
+  if (k == D.nk - 1 && lane == 0) {
+    O.count[0] = (unsigned long long)(mi + nm);
+    O.count[1] = 2ull * (unsigned long long)(mi + nm);
+  }
+  const LaRec* rec = D.rec + la_region(kbeg[k], k);
+  int e = 0;
+  for (uint32_t r = (uint32_t)lane; r < nm; r += 64) {
+    const int64_t m = mi + r;
+    if (m >= O.cap || 2 * m + 2 > O.refcap) {
+      e |= E_OUT;
+      break;
+    }
+    const LaRec x = rec[r];
+    int64_t a = x.flo, b = x.fhi;
+    while (a < b) {
+      const int64_t mid = a + ((b - a) >> 1);
+      if (B.rmax[mid] >= x.due) b = mid;
+      else a = mid + 1;
+    }
+    O.key[m] = B.partitioned ? k : 0;
+    O.ts[m] = x.due;
+    O.type[m] = 0;
+    O.pos[m] = bseq(B, a);
+    O.ref_off[m] = 2 * m;
+    int64_t q = 2 * m;
+#pragma unroll
+    for (int s = 0; s < 3; s++) {
+      const bool isx = s == D.sid[0], isy = s == D.sid[1];
+      O.slot_len[m * MAXS + s] = (int16_t)((isx || isy) ? 1 : 0);
+      if (isx) O.refs[q++] = x.xseq;
+      if (isy) O.refs[q++] = x.yseq;
+    }
   }
   if (e) atomicOr(err, e);
 }
@@ -747,6 +837,7 @@ struct LabsState {
       return true;
     };
     wave_ok = own(D.fx, 1) && own(D.fy, 2) && !getenv("SHP_NO_LABS_W");
+    if (wave_ok) al(D.rec, la_region((uint32_t)std::min<int64_t>(cap, 0xFFFFFFFFll), max_keys) + 1);
     k_labs_init<<<(unsigned)((max_keys + 255) / 256), 256, 0, s>>>(D);
   }
 
@@ -768,16 +859,24 @@ struct LabsState {
     const unsigned gk = few ? (unsigned)D.nk : (unsigned)((D.nk + 63) / 64);
     kt.mark("labs_gather", s);
     if (B.n > 0) k_labs_gather<<<2048, 256, 0, s>>>(D, B, perm, B.n);
-    const bool wv = wave_ok && !slow;
+    if (wave_ok && !slow) {  // one pass, then the records to their offsets
+      kt.mark("labs", s);
+      k_labs_w<<<(unsigned)D.nk, 64, 0, s>>>(D, B, perm, kbeg, kcnt, err);
+      kt.mark("labs_scan", s);
+      size_t tb = tmp_bytes;
+      (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
+      kt.mark("labs_out", s);
+      k_labs_out<<<(unsigned)((D.nk + 3) / 4), 256, 0, s>>>(D, B, O, kbeg, err);
+      kt.mark(nullptr, s);
+      return;
+    }
     kt.mark("labs_count", s);
-    if (wv) k_labs_w<false><<<(unsigned)D.nk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
-    else launch<false>(gk, few, B, O, perm, kbeg, kcnt, err, s);
+    launch<false>(gk, few, B, O, perm, kbeg, kcnt, err, s);
     kt.mark("labs_scan", s);
     size_t tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
     kt.mark("labs", s);
-    if (wv) k_labs_w<true><<<(unsigned)D.nk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
-    else launch<true>(gk, few, B, O, perm, kbeg, kcnt, err, s);
+    launch<true>(gk, few, B, O, perm, kbeg, kcnt, err, s);
     kt.mark("labs_pos", s);
     k_labs_pos<<<1024, 256, 0, s>>>(D, B, O);
     kt.mark(nullptr, s);
@@ -817,7 +916,7 @@ struct LabsState {
       if (D.wq[c]) (void)hipFree(D.wq[c]);
     }
     if (D.wtmp) (void)hipFree(D.wtmp);
-    void* qs[] = {D.aux, D.cm, D.om, D.s_ts, D.s_clk, D.s_st, D.s_v, D.s_n};
+    void* qs[] = {D.aux, D.cm, D.om, D.s_ts, D.s_clk, D.s_st, D.s_v, D.s_n, D.rec};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = LabsDev{};
