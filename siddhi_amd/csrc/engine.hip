@@ -117,6 +117,12 @@ __global__ void k_key_bounds(const uint32_t* __restrict__ sk, int64_t n, uint32_
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t k = sk[i];
+    // keys with no event start where they would (kbeg = kend): per-key output regions derived
+    // from kbeg (the logical-absent path) stay disjoint
+    const uint32_t k0 = i == 0 ? 0u : min(sk[i - 1] + 1u, nk);
+    for (uint32_t a = k0; a < min(k, nk); a++) kbeg[a] = kend[a] = (uint32_t)i;
+    if (i + 1 == n)
+      for (uint32_t a = min(k + 1u, nk); a < nk; a++) kbeg[a] = kend[a] = (uint32_t)n;
     if (k >= nk) continue;
     if (i == 0 || sk[i - 1] != k) kbeg[k] = (uint32_t)i;
     if (i + 1 == n || sk[i + 1] != k) kend[k] = (uint32_t)(i + 1);
@@ -716,6 +722,7 @@ struct shp_engine {
       if (fast == 4 && herr == E_LIST && la.tier + 1 < LA_TIERS && la.set_tier(la.tier + 1, true, stream))
         return run(n, clock_only, in, staged_clk, staged_seq);
       if (herr & SWE_KEYS) return fail(SHP_ERR_KEYS, "partition key id >= max_keys");
+      if (fast == 4 && (herr & LA_BOUND)) return fail(SHP_ERR_DEVICE, "logical-absent path: a key's records overflowed its region");
       if (fast == 4 && (herr & LA_UNORDERED))
         return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the logical-absent path (force_general 4); "
                                          "the general lanes (force_general 1) replay such streams");
@@ -1452,6 +1459,11 @@ double shp_last_kernel_ms(const shp_engine* e, const char* which) {
 
 #ifdef SHP_SW_STAMPS
 // diagnostic build only: per-owner solve phase cycles of the last push (nown * 8)
+int shp_debug_la_stamps(shp_engine* e, unsigned long long* host, int64_t n) {
+  if (!e || e->fast != 4 || !e->la.D.stamps) return SHP_ERR_ARG;
+  int64_t k = std::min<int64_t>(n, (int64_t)e->la.D.nk * 8);
+  return hipMemcpy(host, e->la.D.stamps, k * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)(k / 8) : SHP_ERR_DEVICE;
+}
 int shp_debug_sw_stamps(shp_engine* e, unsigned long long* host, int64_t n) {
   if (!e || e->fast != 2 || !e->sw.D.stamps) return SHP_ERR_ARG;
   int64_t k = std::min<int64_t>(n, (int64_t)e->sw.D.nown * 8);

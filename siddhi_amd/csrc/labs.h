@@ -114,6 +114,7 @@ struct LabsDev {
   int32_t* s_st;
   uint32_t* s_v;
   uint8_t* s_n;
+  unsigned long long* stamps;  // diagnostic build (SHP_SW_STAMPS): k_labs_w phase cycles per key
   LaRec* rec;        // k_labs_w's records, per key region (la_region)
 };
 
@@ -387,6 +388,7 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
 //           Firing follows completion order, so the emitted records keep the FIFO order.
 // More than 64 waiting pairs in a key raise LA_SLOW: the engine re-runs the push with k_labs.
 constexpr int LA_SLOW = 1 << 28;
+constexpr int LA_BOUND = 1 << 29;  // a key's records would leave its region (a broken invariant: fail, never write)
 
 __device__ __forceinline__ int64_t la_rl64(int64_t x, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
@@ -448,7 +450,10 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
   const LaPend s0 = D.pend[rd][k];
   int nal = s0.nw;
   if (nal > 64) {
-    if (lane == 0) atomicOr(err, LA_SLOW);
+    if (lane == 0) {
+      D.cm[k] = 0;  // k_labs_out runs before the host sees LA_SLOW
+      atomicOr(err, LA_SLOW);
+    }
     return;
   }
   if (lane < nal) {
@@ -457,6 +462,7 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
   }
   const uint32_t beg = kbeg[k], cnt = kcnt[k];
   LaRec* rec = D.rec + la_region(beg, k);
+  const uint32_t rcap = (cnt + 1u) / 2u + 64u;  // the region's records (la_region)
   const bool useW = D.within >= 0;
   const int64_t Wn = D.within, Tw = D.wait;
   const int8_t t0g = D.tag[0], t1g = D.tag[1], t2g = D.tag[2];
@@ -470,11 +476,12 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
   int64_t lo = 0;  // first batch index a timer can fire at (after the key's previous event)
   // the waiting pairs (one per lane) fire (fired: in [flo, fhi]) unless killed; the survivors
   // are compacted in order
-  auto settle = [&](bool fired, bool killed, int64_t flo, int64_t fhi, const LaWait& w) {
+  auto settle = [&](bool fired, bool killed, int64_t flo, int64_t fhi, LaWait w) {
     const bool ok = lane < nal && fired && !killed &&
                     (!useW || (llabs(w.xts - w.due) <= Wn && llabs(w.yts - w.due) <= Wn));
     const uint64_t em = __ballot(ok);
-    if (ok) {
+    if (nm + (uint32_t)__popcll(em) > rcap) e |= LA_BOUND;
+    else if (ok) {
       LaRec r;
       r.due = w.due;
       r.xseq = w.xseq;
@@ -495,6 +502,24 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
     nal = __popcll(sm);
     __syncthreads();
   };
+#ifdef SHP_SW_STAMPS  // diagnostic build: wave cycles per phase, and counts (trips, pairs, Z events)
+  unsigned long long lst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t lsp = clock64();
+#define LA_STAMP(x)               \
+  do {                            \
+    const uint64_t t_ = clock64(); \
+    lst[x] += t_ - lsp;           \
+    lsp = t_;                     \
+  } while (0)
+#define LA_COUNT(x, v) lst[x] += (v)
+#else
+#define LA_STAMP(x) \
+  do {              \
+  } while (0)
+#define LA_COUNT(x, v) \
+  do {                 \
+  } while (0)
+#endif
   // the key's events 64 at a time; the next block's loads are issued before this one is worked
   int64_t n_ts = 0, n_clk = 0;
   uint32_t n_g = 0, n_v = 0, n_n = 1;
@@ -529,9 +554,11 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
     const LaVals V0{v, v, 0u, en, en, true, t0g, t1g, t2g};
     const uint64_t QX = __ballot(valid && role == 0 && la_pred(D.fx, V0));
     const uint64_t QY = __ballot(valid && role == 1 && la_pred(D.fy, V0));
+    LA_STAMP(0);
     // 1. the partial, fill by fill
     int p = 0;
     while (p < nv) {
+      LA_COUNT(5, 1);
       const uint64_t ge = ~0ull << p;
       if (!hx && !hy) {
         const uint64_t m = (QX | QY) & ge;
@@ -559,7 +586,10 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
         const int z = Em ? __builtin_ctzll(Em) : 64, b = Om ? __builtin_ctzll(Om) : 64;
         if (b < z) {  // the partner: the pair completes and waits on the absent state
           if (nal >= 64) {
-            if (lane == 0) atomicOr(err, LA_SLOW);
+            if (lane == 0) {
+              D.cm[k] = 0;
+              atomicOr(err, LA_SLOW);
+            }
             return;
           }
           const uint32_t bn = (uint32_t)__builtin_amdgcn_readlane((int)en, b);
@@ -606,6 +636,8 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
       }
     }
     __syncthreads();
+    LA_STAMP(1);
+    LA_COUNT(6, nal);
     // 2. the waiting pairs against this block's events
     if (nal > 0) {
       LaWait w{};
@@ -625,6 +657,7 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
         if (!m) break;
         if (lane == l) f = __builtin_ctzll(m);
       }
+      LA_STAMP(2);
       // killed: a Z event between completion and firing whose filter holds
       bool killed = false;
       const LaKill K = la_kill_pre(D.fz, w, t0g, t1g, t2g);
@@ -637,10 +670,12 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
         const double zd0 = la_val(zv, t2g, false), zd1 = la_val(zv, t2g, true);
         if (z > c && z < f) killed = killed || la_kill(D.fz, K, zd0, zd1, zn);
       }
+      LA_STAMP(3);
       const bool fired = f < 64;
       const int64_t gp = (int64_t)(uint32_t)__shfl(g, f > 0 ? f - 1 : 0, 64);
       const int64_t gf = (int64_t)(uint32_t)__shfl(g, f < 64 ? f : 0, 64);
       settle(fired, killed, f == 0 ? lo : gp + 1, gf, w);
+      LA_STAMP(4);
     }
     lo = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)g, nv - 1) + 1;
     last = la_rl64(ts, nv - 1);
@@ -652,10 +687,17 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
     const int64_t lastclk = B.n > 0 ? B.rmax[B.n - 1] : INT64_MIN;
     settle(lane < nal && w.due <= lastclk, false, lo, B.n - 1, w);
   }
+#ifdef SHP_SW_STAMPS
+  LA_COUNT(7, cnt);
+  if (lane == 0 && D.stamps)
+    for (int x = 0; x < 8; x++) D.stamps[(int64_t)k * 8 + x] = lst[x];
+#endif
+#undef LA_STAMP
+#undef LA_COUNT
   if (nal > cap) e |= E_LIST;
   else if (lane < nal) D.wq[wr][(int64_t)k * cap + lane] = A[lane];
   if (lane == 0) {
-    D.cm[k] = nm;
+    D.cm[k] = min(nm, rcap);
     LaPend s{};
     s.xseq = hx ? xseq : -1;
     s.yseq = hy ? yseq : -1;
@@ -675,12 +717,12 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
 // k_labs_w's records of each key (its region of D.rec) to the push's output at the key's offset,
 // with the fire event found as k_labs_pos does
 __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ kbeg,
-                                                  int* err) {
+                                                  const uint32_t* __restrict__ kcnt, int* err) {
   const int k = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   if (k >= D.nk) return;
   const int lane = (int)(threadIdx.x & 63);
   const int64_t mi = D.om[k];
-  const uint32_t nm = D.cm[k];
+  const uint32_t nm = min(D.cm[k], (kcnt[k] + 1u) / 2u + 64u);
   if (k == D.nk - 1 && lane == 0) {
     O.count[0] = (unsigned long long)(mi + nm);
     O.count[1] = 2ull * (unsigned long long)(mi + nm);
@@ -694,7 +736,7 @@ __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B, MatchO
       break;
     }
     const LaRec x = rec[r];
-    int64_t a = x.flo, b = x.fhi;
+    int64_t a = x.flo, b = min((int64_t)x.fhi, B.n - 1);
     while (a < b) {
       const int64_t mid = a + ((b - a) >> 1);
       if (B.rmax[mid] >= x.due) b = mid;
@@ -838,6 +880,9 @@ struct LabsState {
     };
     wave_ok = own(D.fx, 1) && own(D.fy, 2) && !getenv("SHP_NO_LABS_W");
     if (wave_ok) al(D.rec, la_region((uint32_t)std::min<int64_t>(cap, 0xFFFFFFFFll), max_keys) + 1);
+#ifdef SHP_SW_STAMPS
+    al(D.stamps, (int64_t)max_keys * 8);
+#endif
     k_labs_init<<<(unsigned)((max_keys + 255) / 256), 256, 0, s>>>(D);
   }
 
@@ -866,7 +911,7 @@ struct LabsState {
       size_t tb = tmp_bytes;
       (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
       kt.mark("labs_out", s);
-      k_labs_out<<<(unsigned)((D.nk + 3) / 4), 256, 0, s>>>(D, B, O, kbeg, err);
+      k_labs_out<<<(unsigned)((D.nk + 3) / 4), 256, 0, s>>>(D, B, O, kbeg, kcnt, err);
       kt.mark(nullptr, s);
       return;
     }
@@ -916,7 +961,7 @@ struct LabsState {
       if (D.wq[c]) (void)hipFree(D.wq[c]);
     }
     if (D.wtmp) (void)hipFree(D.wtmp);
-    void* qs[] = {D.aux, D.cm, D.om, D.s_ts, D.s_clk, D.s_st, D.s_v, D.s_n, D.rec};
+    void* qs[] = {D.aux, D.cm, D.om, D.s_ts, D.s_clk, D.s_st, D.s_v, D.s_n, D.rec, D.stamps};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = LabsDev{};
