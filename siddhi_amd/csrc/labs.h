@@ -555,84 +555,173 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
     const uint64_t QX = __ballot(valid && role == 0 && la_pred(D.fx, V0));
     const uint64_t QY = __ballot(valid && role == 1 && la_pred(D.fy, V0));
     LA_STAMP(0);
-    // 1. the partial, fill by fill
-    int p = 0;
-    while (p < nv) {
+    // 1. the partial.  A half partial carried into the block resolves first (its partner, or the
+    //    first event beyond W).  Then, from an empty partial at lane p, the next step depends on
+    //    the block alone: the first qualifying event a >= p fills a slot; the first qualifying
+    //    partner b > a completes the pair if ts_b - ts_a <= W (no event between them is later
+    //    than ts_b), else the first event beyond ts_a + W resets the partial and starts afresh.
+    //    Every lane computes that step for p = itself, and the chain from the block's first empty
+    //    position is walked with one readlane per step.
+    int p0 = 0;
+    if (hx || hy) {
       LA_COUNT(5, 1);
-      const uint64_t ge = ~0ull << p;
-      if (!hx && !hy) {
-        const uint64_t m = (QX | QY) & ge;
-        if (!m) break;
-        const int a = __builtin_ctzll(m);
-        const uint32_t an = (uint32_t)__builtin_amdgcn_readlane((int)en, a);
-        if ((QX >> a) & 1ull) {
-          hx = true;
-          xseq = la_rl64(seqg, a);
-          xts = la_rl64(ts, a);
-          xv = (uint32_t)__builtin_amdgcn_readlane((int)v, a);
-          fl = (fl & ~1u) | (an ? 1u : 0u);
-        } else {
-          hy = true;
-          yseq = la_rl64(seqg, a);
-          yts = la_rl64(ts, a);
-          yv = (uint32_t)__builtin_amdgcn_readlane((int)v, a);
-          fl = (fl & ~2u) | (an ? 2u : 0u);
-        }
-        p = a + 1;
-      } else {
-        const int64_t tf = hx ? xts : yts;
-        const uint64_t Em = useW ? (__ballot(valid && ts - tf > Wn) & ge) : 0ull;
-        const uint64_t Om = (hx ? QY : QX) & ge;
-        const int z = Em ? __builtin_ctzll(Em) : 64, b = Om ? __builtin_ctzll(Om) : 64;
-        if (b < z) {  // the partner: the pair completes and waits on the absent state
-          if (nal >= 64) {
-            if (lane == 0) {
-              D.cm[k] = 0;
-              atomicOr(err, LA_SLOW);
-            }
-            return;
-          }
-          const uint32_t bn = (uint32_t)__builtin_amdgcn_readlane((int)en, b);
-          const int64_t bseqv = la_rl64(seqg, b), bts = la_rl64(ts, b);
-          const uint32_t bv = (uint32_t)__builtin_amdgcn_readlane((int)v, b);
-          if (hx) {
-            yseq = bseqv;
-            yts = bts;
-            yv = bv;
-            fl = (fl & ~2u) | (bn ? 2u : 0u);
-          } else {
-            xseq = bseqv;
-            xts = bts;
-            xv = bv;
-            fl = (fl & ~1u) | (bn ? 1u : 0u);
-          }
+      const int64_t tf = hx ? xts : yts;
+      const uint64_t Em = useW ? __ballot(valid && ts - tf > Wn) : 0ull;
+      const uint64_t Om = hx ? QY : QX;
+      const int z = Em ? __builtin_ctzll(Em) : 64, b = Om ? __builtin_ctzll(Om) : 64;
+      if (b < z) {  // the partner: the pair completes and waits on the absent state
+        if (nal >= 64) {
           if (lane == 0) {
-            LaWait w;
-            w.due = bts + Tw;
-            w.xseq = xseq;
-            w.xts = xts;
-            w.yseq = yseq;
-            w.yts = yts;
-            w.xv = xv;
-            w.yv = yv;
-            w.fl = fl;
-            w.pad = 0;
-            A[nal] = w;
-            Ac[nal] = b;
+            D.cm[k] = 0;
+            atomicOr(err, LA_SLOW);
           }
-          nal++;
-          hx = hy = false;
-          xseq = yseq = -1;
-          fl = 0;
-          p = b + 1;
-        } else if (z < 64) {  // expired (StreamPreStateProcessor.expireEvents): event z starts afresh
-          hx = hy = false;
-          xseq = yseq = -1;
-          fl = 0;
-          p = z;
-        } else {
-          break;
+          return;
         }
+        const uint32_t bn = (uint32_t)__builtin_amdgcn_readlane((int)en, b);
+        const int64_t bseqv = la_rl64(seqg, b), bts = la_rl64(ts, b);
+        const uint32_t bv = (uint32_t)__builtin_amdgcn_readlane((int)v, b);
+        if (hx) {
+          yseq = bseqv;
+          yts = bts;
+          yv = bv;
+          fl = (fl & ~2u) | (bn ? 2u : 0u);
+        } else {
+          xseq = bseqv;
+          xts = bts;
+          xv = bv;
+          fl = (fl & ~1u) | (bn ? 1u : 0u);
+        }
+        if (lane == 0) {
+          LaWait w;
+          w.due = bts + Tw;
+          w.xseq = xseq;
+          w.xts = xts;
+          w.yseq = yseq;
+          w.yts = yts;
+          w.xv = xv;
+          w.yv = yv;
+          w.fl = fl;
+          w.pad = 0;
+          A[nal] = w;
+          Ac[nal] = b;
+        }
+        nal++;
+        hx = hy = false;
+        xseq = yseq = -1;
+        fl = 0;
+        p0 = b + 1;
+      } else if (z < 64) {  // expired (StreamPreStateProcessor.expireEvents): event z starts afresh
+        hx = hy = false;
+        xseq = yseq = -1;
+        fl = 0;
+        p0 = z;
+      } else {
+        p0 = 64;
+      }
+    }
+    // the step from an empty partial at p = this lane
+    const uint64_t mq = (QX | QY) & (~0ull << lane);
+    const int a = mq ? __builtin_ctzll(mq) : 64;
+    const int ac = a < 64 ? a : 0;
+    const bool ax = ((QX >> ac) & 1ull) != 0;
+    const uint64_t opp = (ax ? QY : QX) & (a < 63 ? (~0ull << (a + 1)) : 0ull);
+    const int b = opp ? __builtin_ctzll(opp) : 64;
+    const int bc = b < 64 ? b : 0;
+    const int64_t tsa = __shfl(ts, ac, 64), tsb = __shfl(ts, bc, 64);
+    int zq = nv;  // the first lane after a whose ts is beyond ts_a + W (ts ascend within the block)
+    if (useW) {
+      int l2 = a + 1, h2 = nv;
+#pragma unroll
+      for (int it = 0; it < 7; it++) {
+        const int mid = (l2 + h2) >> 1;
+        const int64_t tm = __shfl(ts, mid < 64 ? mid : 0, 64);
+        if (l2 < h2) {
+          if (mid < nv && tm - tsa > Wn) h2 = mid;
+          else l2 = mid + 1;
+        }
+      }
+      zq = l2;
+    }
+    // kind: 0 nothing fills a slot in [p, nv); 1 pair (a, b), empty at b + 1; 2 reset at zq;
+    // 3 a half partial (a) at the block's end
+    int kind, J;
+    if (a >= nv) {
+      kind = 0;
+      J = 64;
+    } else if (b < nv && (!useW || tsb - tsa <= Wn)) {
+      kind = 1;
+      J = b + 1;
+    } else if (zq < nv) {
+      kind = 2;
+      J = zq;
+    } else {
+      kind = 3;
+      J = 64;
+    }
+    const int KJ = J | (kind << 8);
+    uint64_t PM = 0;  // chain positions whose step completes a pair
+    int hk = -1;      // chain position that leaves a half partial
+    for (int p = p0; p < nv;) {
+      LA_COUNT(5, 1);
+      const int kj = __builtin_amdgcn_readlane(KJ, p);
+      const int kd = kj >> 8;
+      if (kd == 1) {
+        PM |= 1ull << p;
+        p = kj & 0xFF;
+      } else if (kd == 2) {
+        p = kj & 0xFF;
+      } else {
+        if (kd == 3) hk = p;
+        break;
+      }
+    }
+    if (PM) {  // the completed pairs, in completion order, join the waits
+      const int npm = __popcll(PM);
+      if (nal + npm > 64) {
+        if (lane == 0) {
+          D.cm[k] = 0;
+          atomicOr(err, LA_SLOW);
+        }
+        return;
+      }
+      const int xi = ax ? ac : bc, yi = ax ? bc : ac;
+      const int64_t sx = __shfl(seqg, xi, 64), sy = __shfl(seqg, yi, 64);
+      const int64_t tx = __shfl(ts, xi, 64), ty = __shfl(ts, yi, 64);
+      const uint32_t vx = (uint32_t)__shfl((int)v, xi, 64), vy = (uint32_t)__shfl((int)v, yi, 64);
+      const int nx = __shfl((int)en, xi, 64), ny = __shfl((int)en, yi, 64);
+      if ((PM >> lane) & 1ull) {
+        const int d = nal + __popcll(PM & lt);
+        LaWait w;
+        w.due = tsb + Tw;
+        w.xseq = sx;
+        w.xts = tx;
+        w.yseq = sy;
+        w.yts = ty;
+        w.xv = vx;
+        w.yv = vy;
+        w.fl = (nx ? 1u : 0u) | (ny ? 2u : 0u);
+        w.pad = 0;
+        A[d] = w;
+        Ac[d] = b;
+      }
+      nal += npm;
+    }
+    if (hk >= 0) {  // the slot event a of the chain's last step
+      const int ha = __builtin_amdgcn_readlane(a, hk);
+      const bool hxs = __builtin_amdgcn_readlane((int)ax, hk) != 0;
+      const uint32_t an = (uint32_t)__builtin_amdgcn_readlane((int)en, ha);
+      if (hxs) {
+        hx = true;
+        xseq = la_rl64(seqg, ha);
+        xts = la_rl64(ts, ha);
+        xv = (uint32_t)__builtin_amdgcn_readlane((int)v, ha);
+        fl = (fl & ~1u) | (an ? 1u : 0u);
+      } else {
+        hy = true;
+        yseq = la_rl64(seqg, ha);
+        yts = la_rl64(ts, ha);
+        yv = (uint32_t)__builtin_amdgcn_readlane((int)v, ha);
+        fl = (fl & ~2u) | (an ? 2u : 0u);
       }
     }
     __syncthreads();
@@ -658,17 +747,29 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
         if (lane == l) f = __builtin_ctzll(m);
       }
       LA_STAMP(2);
-      // killed: a Z event between completion and firing whose filter holds
+      // killed: a Z event between completion and firing whose filter holds.  Each pair walks the
+      // Z events of its window (c, f) with first-set-bit jumps; the walk ends at the first kill.
       bool killed = false;
-      const LaKill K = la_kill_pre(D.fz, w, t0g, t1g, t2g);
-      uint64_t zm = __ballot(valid && role == 2);
-      while (zm) {
-        const int z = __builtin_ctzll(zm);
-        zm &= zm - 1;
-        const uint32_t zv = (uint32_t)__builtin_amdgcn_readlane((int)v, z);
-        const bool zn = __builtin_amdgcn_readlane((int)en, z) != 0;
-        const double zd0 = la_val(zv, t2g, false), zd1 = la_val(zv, t2g, true);
-        if (z > c && z < f) killed = killed || la_kill(D.fz, K, zd0, zd1, zn);
+      const uint64_t zm = __ballot(valid && role == 2);
+      if (zm) {
+        const LaKill K = la_kill_pre(D.fz, w, t0g, t1g, t2g);
+        auto nextz = [&](int x) -> int {
+          if (x >= 64) return 64;
+          const uint64_t r = zm >> x;
+          return r ? x + __builtin_ctzll(r) : 64;
+        };
+        int q = nextz(c + 1);
+        bool act = lane < nal && q < f;
+        while (__ballot(act)) {
+          const int qs = q < 64 ? q : 0;
+          const uint32_t zv = (uint32_t)__shfl((int)v, qs, 64);
+          const bool zn = __shfl((int)en, qs, 64) != 0;
+          if (act) {
+            killed = la_kill(D.fz, K, la_val(zv, t2g, false), la_val(zv, t2g, true), zn);
+            q = nextz(q + 1);
+            act = !killed && q < f;
+          }
+        }
       }
       LA_STAMP(3);
       const bool fired = f < 64;

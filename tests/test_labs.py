@@ -86,31 +86,54 @@ def wave_model(ts, key, st, pr, block=64):
             nv = len(blk)
             qx = [int(st[g]) == 0 and float(pr[g]) > 20 for g in blk]
             qy = [int(st[g]) == 1 and float(pr[g]) > 20 for g in blk]
-            p = 0
-            while p < nv:
-                if pend["e1"] is None and pend["e2"] is None:
-                    a = next((q for q in range(p, nv) if qx[q] or qy[q]), None)
-                    if a is None:
-                        break
-                    g = blk[a]
-                    pend["e1" if qx[a] else "e2"] = (g, int(ts[g]), float(pr[g]))
-                    p = a + 1
+            tsb = [int(ts[g]) for g in blk]
+            p0 = 0
+            if pend["e1"] is not None or pend["e2"] is not None:  # a half partial carried in
+                slot, other, q_o = ("e1", "e2", qy) if pend["e1"] is not None else ("e2", "e1", qx)
+                t0 = pend[slot][1]
+                z = next((q for q in range(nv) if tsb[q] - t0 > W), 64)
+                b = next((q for q in range(nv) if q_o[q]), 64)
+                if b < z:
+                    g = blk[b]
+                    pend[other] = (g, tsb[b], float(pr[g]))
+                    alive.append([tsb[b] + WAIT, pend["e1"], pend["e2"], b])
+                    pend = {"e1": None, "e2": None}
+                    p0 = b + 1
+                elif z < 64:
+                    pend = {"e1": None, "e2": None}
+                    p0 = z
                 else:
-                    slot, other, q_o = ("e1", "e2", qy) if pend["e1"] is not None else ("e2", "e1", qx)
-                    t0 = pend[slot][1]
-                    z = next((q for q in range(p, nv) if int(ts[blk[q]]) - t0 > W), nv)
-                    b = next((q for q in range(p, nv) if q_o[q]), nv)
-                    if b < z:
-                        g = blk[b]
-                        pend[other] = (g, int(ts[g]), float(pr[g]))
-                        alive.append([int(ts[g]) + WAIT, pend["e1"], pend["e2"], b])
-                        pend = {"e1": None, "e2": None}
-                        p = b + 1
-                    elif z < nv:
-                        pend = {"e1": None, "e2": None}
-                        p = z
-                    else:
-                        break
+                    p0 = 64
+
+            def step(p):  # from an empty partial at p: (kind, next, a, b)
+                a = next((q for q in range(p, nv) if qx[q] or qy[q]), None)
+                if a is None:
+                    return 0, 64, None, None
+                q_o = qy if qx[a] else qx
+                b = next((q for q in range(a + 1, nv) if q_o[q]), None)
+                if b is not None and tsb[b] - tsb[a] <= W:
+                    return 1, b + 1, a, b
+                z = next((q for q in range(a + 1, nv) if tsb[q] - tsb[a] > W), None)
+                if z is not None:
+                    return 2, z, a, b
+                return 3, 64, a, b
+
+            p = p0
+            while p < nv:
+                kind, nxt, a, b = step(p)
+                if kind == 1:
+                    ga, gb = blk[a], blk[b]
+                    ea, eb = (ga, tsb[a], float(pr[ga])), (gb, tsb[b], float(pr[gb]))
+                    e1, e2 = (ea, eb) if qx[a] else (eb, ea)
+                    alive.append([tsb[b] + WAIT, e1, e2, b])
+                    p = nxt
+                elif kind == 2:
+                    p = nxt
+                else:
+                    if kind == 3:
+                        ga = blk[a]
+                        pend["e1" if qx[a] else "e2"] = (ga, tsb[a], float(pr[ga]))
+                    break
             fires = []
             for due, e1, e2, c in alive:
                 f = next((q for q in range(c + 1, nv) if clock[blk[q]] >= due), None)
