@@ -18,3 +18,6 @@ done
 timeout -k 10 400 python -u bench.py --config 4 --path labs --steps 3 --warmup 1 --latency-batches 0 > gpurun_out/bench_c4.log 2>&1 || { tail -20 gpurun_out/bench_c4.log; exit 1; }
 grep '^{' gpurun_out/bench_c4.log > gpurun_out/bench_c4.json
 python3 -c "import json; d=json.load(open('gpurun_out/bench_c4.json')); print('C4', d['value']/1e9, d['ms_per_step'], d['cpu_baseline']['value'] if d['cpu_baseline'] else None)"
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats_c4 -o run -- python3 -u bench.py --config 4 --path labs --steps 3 --warmup 1 --no-cpu-baseline --latency-batches 0 > gpurun_out/stats_c4.log 2>&1 || { tail -20 gpurun_out/stats_c4.log; exit 1; }
+echo "c4 stats done"
