@@ -628,7 +628,10 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
     const int bc = b < 64 ? b : 0;
     const int64_t tsa = __shfl(ts, ac, 64), tsb = __shfl(ts, bc, 64);
     int zq = nv;  // the first lane after a whose ts is beyond ts_a + W (ts ascend within the block)
-    if (useW) {
+    // searched only when some lane's step can reset: no partner within W, and a later event beyond W
+    const int64_t tsl = la_rl64(ts, nv - 1);
+    const bool need = useW && a < nv && !(b < nv && tsb - tsa <= Wn) && tsl - tsa > Wn;
+    if (__ballot(need)) {
       int l2 = a + 1, h2 = nv;
 #pragma unroll
       for (int it = 0; it < 7; it++) {
@@ -738,12 +741,18 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
       // completions follow the pair order, so the fire events do too: the first pair that does
       // not fire in this block ends the search.
       int f = 64;
-      for (int l = 0; l < nal; l++) {
-        const int64_t dl = la_rl64(w.due, l);
-        const int cl = __builtin_amdgcn_readlane(c, l);
-        const uint64_t m = __ballot(valid && lane > cl && clk >= dl);
-        if (!m) break;
-        if (lane == l) f = __builtin_ctzll(m);
+      {  // per pair, a search over the block's clocks (ascending) after c
+        int l2 = c + 1, h2 = nv;  // the answer lies in [l2, h2]; h2 = nv: not in this block
+#pragma unroll
+        for (int it = 0; it < 7; it++) {
+          const int mid = (l2 + h2) >> 1;
+          const int64_t cm = __shfl(clk, mid < 64 ? mid : 0, 64);
+          if (l2 < h2) {
+            if (mid < nv && cm >= w.due) h2 = mid;
+            else l2 = mid + 1;
+          }
+        }
+        if (lane < nal && l2 < nv) f = l2;
       }
       LA_STAMP(2);
       // killed: a Z event between completion and firing whose filter holds.  Each pair walks the
