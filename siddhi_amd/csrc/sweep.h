@@ -145,7 +145,7 @@ struct SweepDev {
   int32_t maybe_null;    // some pushed batch carried a null bitmap (sticky; the carry may hold nulls)
   int64_t st_len;
   int32_t cur;           // which copy of the double-buffered per-owner state the next push reads
-  int32_t pad_;
+  int32_t f1ct;          // e1's filter in the scatter: typed compare class (1 float, 2 int; 0 generic doubles)
   const uint8_t* lk8;    // key -> local key id within its owner (the owner is sw_owner(key))
   int32_t lk_lds;        // scatter stages lk8 in LDS (max_keys <= SW_LKTAB)
   uint32_t* cnt;         // nown * nst + 1: counts, scanned into off
@@ -484,11 +484,15 @@ __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchVie
         if (!sw_rel_ok(rel)) e |= SWE_RANGE;
         wide |= rel >= (1ll << 30) || rel < -(1ll << 30);
         const bool nl = (kk[s] & 0x40000000) != 0;
-        double af, ai;
-        sw_conv(rec[s].v, vflt, af, ai);
+        double af = 0.0, ai = 0.0;
+        if (D.f1ct == 0) sw_conv(rec[s].v, vflt, af, ai);
         const bool an = vnull || nl;
-        bool c1 = true;  // e1's filter, generic (exact) double compares: this pass has ALU to spare
-        if (D.f1.n == 1) {
+        bool c1 = true;  // e1's filter: typed where the solve's is (exact for Java's promotion), else doubles
+        if (D.f1ct == 1) {
+          c1 = D.f1.n == 1 ? sw_open<1, 1>(D.f1, rec[s].v, an) : (D.f1.n == 2 ? sw_open<2, 1>(D.f1, rec[s].v, an) : true);
+        } else if (D.f1ct == 2) {
+          c1 = D.f1.n == 1 ? sw_open<1, 2>(D.f1, rec[s].v, an) : (D.f1.n == 2 ? sw_open<2, 2>(D.f1, rec[s].v, an) : true);
+        } else if (D.f1.n == 1) {
           c1 = sw_term(D.f1.t[0], af, ai, an, 0.0, 0.0, true);
         } else if (D.f1.n == 2) {
           const bool x = sw_term(D.f1.t[0], af, ai, an, 0.0, 0.0, true);
@@ -1692,6 +1696,7 @@ struct SweepState {
       throw std::runtime_error("hipMalloc failed (sweep scan scratch)");
     // k_sw_lean: one f2 term `e2.v OP B` in the column's own type (float / int32), one of the six
     // standard comparisons; the pair layouts without nulls are checked per push (run)
+    D.f1ct = ct != 0 && !getenv("SHP_SCATTER_GENERIC") ? ct : 0;
     lean_opc = 0;
     // (batch indices below 2^31: e1's filter rides in the index's top bit)
     if (D.f2.n == 1 && (ct == 1 || ct == 2) && !D.f2.t[0].flt && D.vtag != T_NULL && cap < (1ll << 31) &&
