@@ -247,6 +247,24 @@ def test_c4_wave_kernel_equals_thread_kernel(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_labs_pushes_missing_half_the_keys():
+    """Pushes alternate between all keys and only the even keys: the odd keys' waiting pairs fire
+    in pushes that hold none of their events (their record regions come from the key runs' would-be
+    starts, k_key_bounds), exactly as the oracle."""
+    cq = program_for(4)
+    g = small_stream(4, 360_000, 200)
+    keep = np.ones(len(g["ts"]), bool)
+    blk = np.arange(len(g["ts"])) // 60_000  # odd blocks: ~30k events of even keys only
+    keep[(blk % 2 == 1) & (g["key"] % 2 == 1)] = False
+    g = {k: v[keep] for k, v in g.items()}
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g, 25_000))
+    eng = _hip(cq, 200, 25_000)
+    got = per_key(run(eng, cq, g, 25_000))
+    assert compare(want, got) is None, compare(want, got)
+    assert eng.stat("labs_fallbacks") == 0
+
+
+@pytest.mark.gpu
 def test_labs_equals_general_lanes_and_advance():
     """Pushes, then a clock advanced with no event (shp_advance_clock fires the waiting pairs):
     the same records from k_labs and from the general lanes, and from the oracle."""
