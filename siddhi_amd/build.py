@@ -1,15 +1,29 @@
-"""Build libsiddhi_hip.so for gfx950 (hipcc), in-tree so it travels with the repo snapshot."""
+"""Build libsiddhi_hip.so for gfx950 (hipcc), in-tree so it travels with the repo snapshot.
+
+Each translation unit is compiled to its own object (in parallel) and relinked, so a change to
+one file recompiles that file only; an object is stale when its source or any shared header is
+newer than it."""
 from __future__ import annotations
 
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libsiddhi_hip.so")
 SRC = os.path.join(HERE, "csrc")
-DEPS = ["engine.hip", "synth.hip", "shard.hip", "group.hip", "nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h", "sweep.h", "sweep_lean.h", "cseq.h", "labs.h"]
+OBJ = os.path.join(HERE, "build_obj")
+HEADERS = ["nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h", "sweep.h", "sweep_lean.h",
+           "cseq.h", "labs.h"]
+UNITS = ["engine.hip", "synth.hip", "shard.hip", "group.hip", "siddhiql.cpp"]
+DEPS = HEADERS + UNITS
+
+
+def _hdr_time() -> float:
+    hs = [os.path.join(SRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "siddhi_hip.h")]
+    return max(os.path.getmtime(h) for h in hs if os.path.exists(h))
 
 
 def _stale(lib: str = LIB) -> bool:
@@ -29,11 +43,27 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
     if not force and not _stale(lib):
         return lib
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-o", lib + ".tmp", os.path.join(SRC, "engine.hip"), os.path.join(SRC, "synth.hip"),
-           os.path.join(SRC, "shard.hip"), os.path.join(SRC, "group.hip"), "-lrccl"]
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"]
     if stamps:
-        cmd.insert(3, "-DSHP_SW_STAMPS")
+        flags.append("-DSHP_SW_STAMPS")
+    odir = OBJ + ("_stamps" if stamps else "")
+    os.makedirs(odir, exist_ok=True)
+    ht = _hdr_time()
+
+    def obj(u: str) -> str:
+        src = os.path.join(SRC, u)
+        o = os.path.join(odir, u + ".o")
+        if force or not os.path.exists(o) or os.path.getmtime(o) < max(ht, os.path.getmtime(src)):
+            cmd = [hipcc] + flags + ["-c", "-o", o + ".tmp", src]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.check_call(cmd)
+            os.replace(o + ".tmp", o)
+        return o
+
+    with ThreadPoolExecutor(max_workers=len(UNITS)) as ex:
+        objs = list(ex.map(obj, UNITS))
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-lrccl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

@@ -582,7 +582,7 @@ struct shp_engine {
       lastKey = x_key;
       expanded = false;
       if (cfg.match_layout == SHP_LAYOUT_FULL) {
-        sw.expand(B, x_key, O, stream, kt, -1, d_err);
+        sw.expand(B, x_key, O, d_err, stream, kt);
         expanded = true;
       }
       HIP_OK(hipMemcpyAsync(h_tsmax, sw.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
@@ -667,7 +667,7 @@ struct shp_engine {
       lean_fallbacks++;
       HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
       sw.solve(B, O, d_err, stream, kt);
-      if (cfg.match_layout == SHP_LAYOUT_FULL) sw.expand(B, x_key, O, stream, kt);
+      if (cfg.match_layout == SHP_LAYOUT_FULL) sw.expand(B, x_key, O, d_err, stream, kt);
       HIP_OK(hipEventRecord(ev2, stream));
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
@@ -722,6 +722,7 @@ struct shp_engine {
       if (fast == 4 && herr == E_LIST && la.tier + 1 < LA_TIERS && la.set_tier(la.tier + 1, true, stream))
         return run(n, clock_only, in, staged_clk, staged_seq);
       if (herr & SWE_KEYS) return fail(SHP_ERR_KEYS, "partition key id >= max_keys");
+      if (herr & SWE_BOUND) return fail(SHP_ERR_DEVICE, "internal: a match pair names an event outside its push (SWE_BOUND)");
       if (fast == 4 && (herr & LA_BOUND)) return fail(SHP_ERR_DEVICE, "logical-absent path: a key's records overflowed its region");
       if (fast == 4 && (herr & LA_UNORDERED))
         return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the logical-absent path (force_general 4); "
@@ -1163,8 +1164,12 @@ struct shp_engine {
   void ensure_expanded() {
     if (fast != 2 || expanded || cfg.match_layout == SHP_LAYOUT_AGG) return;
     MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs, d_magg};
-    sw.expand(lastB, lastKey, O, stream, kt, last_m);
+    HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), stream));
+    sw.expand(lastB, lastKey, O, d_err, stream, kt, last_m);
+    int herr = 0;
+    HIP_OK(hipMemcpyAsync(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
+    if (herr & SWE_BOUND) throw DevError("internal: a match pair names an event outside its push (SWE_BOUND)");
     expanded = true;
   }
 
@@ -1331,6 +1336,22 @@ int shp_engine_create(const char* json, const shp_config* cfg, shp_engine** out)
   }
   *out = e;
   return SHP_OK;
+}
+
+int shp_engine_create_siddhiql(const char* app_text, const char* query_name, shp_dict* dict, const shp_config* cfg,
+                               shp_engine** out) {
+  if (!app_text || !dict || !cfg || !out) return SHP_ERR_ARG;
+  const int64_t n = shp_compile_siddhiql(app_text, query_name, dict, nullptr, 0);
+  if (n < 0) {
+    fprintf(stderr, "shp_engine_create_siddhiql: %s\n", shp_compile_last_error());
+    *out = nullptr;
+    return (int)n;
+  }
+  std::string prog((size_t)n + 1, '\0');
+  // the dictionary already holds this query's constants: the second lowering interns nothing new
+  if (shp_compile_siddhiql(app_text, query_name, dict, &prog[0], prog.size()) != n) return SHP_ERR_ARG;
+  prog.resize((size_t)n);
+  return shp_engine_create(prog.c_str(), cfg, out);
 }
 
 // The engine's HIP calls run on its own device whatever thread calls in: HIP's current device

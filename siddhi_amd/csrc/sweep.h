@@ -82,6 +82,8 @@ constexpr int SWE_RANGE = 1 << 23;  // ts outside base +- 2^49 ms
 constexpr int SWE_AGGNULL = 1 << 24; // SHP_LAYOUT_AGG: a closing event's aggregated value is null
 constexpr int SWE_P32 = 1 << 25;     // SHP_LAYOUT_PAIRS32: e2 seq - e1 seq >= 2^32
 constexpr int SWE_LEAN = 1 << 26;    // k_sw_lean handed the push to k_sw_solve (not an error)
+constexpr int SWE_BOUND = 1 << 30;   // a match pair names an event outside the push (a broken
+                                     // invariant: the expansion skips it and the push fails)
 
 // 16-byte record.  kt: [63:56] local key (0xFF = none), [55] carried, [54] null,
 // [49:0] ts - base + 2^49.  ref: batch index (events) or carry slot (carried).
@@ -1413,9 +1415,17 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
 // full match records from the (i, j) pairs (shp_push_batch / shp_fetch_matches).  p32: the
 // pairs are SHP_LAYOUT_PAIRS32 (e2 batch index, e2 seq - e1 seq), staged by the caller in O.pos
 // (8 bytes per match); thread i reads its pair before it writes O.pos[i].
-__global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchOut O, int p32, const int* err) {
+//
+// Round-2 fault (tests/test_lean_sweep.py::test_fallback_and_back_keeps_state_exact, "illegal
+// memory access"): this kernel used to run right after a k_sw_lean push that handed back with
+// SWE_LEAN.  The lean kernel had already reserved output slots (O.count) it never wrote, so the
+// expansion read stale pair words as batch indices g and loaded B.ts[g] / key[g] far out of
+// bounds.  Now a handed-back push is not expanded (the exact re-run expands its own output), and
+// any pair whose index falls outside the push sets SWE_BOUND instead of being dereferenced.
+__global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchOut O, int p32, int* err) {
   // a push k_sw_lean handed back has reserved slots it never wrote: the exact re-run expands
-  if (err && (*err & SWE_LEAN)) return;
+  if (*err & SWE_LEAN) return;
+  int bad = 0;
   const int64_t m = min((int64_t)*O.count, O.cap);
   if (blockIdx.x == 0 && threadIdx.x == 0) O.count[1] = 2ull * (unsigned long long)m;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1423,20 +1433,29 @@ __global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchO
     if (p32) {  // (e2's batch index, e2 seq - e1 seq)
       const uint2 pr = reinterpret_cast<const uint2*>(O.pos)[i];
       g = (int64_t)pr.x;
-      if (g >= B.n) continue;
+      if (g >= B.n) {
+        bad = SWE_BOUND;
+        continue;
+      }
       j = bseq(B, g);
       O.refs[2 * i] = j - (int64_t)pr.y;
       O.refs[2 * i + 1] = j;
     } else if (B.seq) {  // (e1 seq, e2's batch index): the FULL layout with a seq column
       g = O.refs[2 * i + 1];
-      if (g < 0 || g >= B.n) continue;
+      if (g < 0 || g >= B.n) {
+        bad = SWE_BOUND;
+        continue;
+      }
       j = B.seq[g];
       O.refs[2 * i + 1] = j;
     } else {  // (e1 seq, e2 seq)
       j = O.refs[2 * i + 1];
       g = j - B.seq0;
     }
-    if (g < 0 || g >= B.n) continue;  // not a pair of this push (never written)
+    if (g < 0 || g >= B.n) {  // not a pair of this push (never written)
+      bad = SWE_BOUND;
+      continue;
+    }
     O.key[i] = B.partitioned ? key[g] : 0;
     O.ts[i] = B.ts[g];
     O.type[i] = 0;
@@ -1445,6 +1464,7 @@ __global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchO
     O.slot_len[i * MAXS] = 1;
     O.slot_len[i * MAXS + 1] = 1;
   }
+  if (bad) atomicOr(err, bad);
 }
 
 __global__ void k_sw_init(SweepDev D) {
@@ -1795,8 +1815,8 @@ struct SweepState {
     kt.mark(nullptr, s);
   }
 
-  void expand(const BatchView& B, const int32_t* key, const MatchOut& O, hipStream_t s, KTimer& kt,
-              int64_t m_host = -1, const int* err = nullptr) {
+  void expand(const BatchView& B, const int32_t* key, const MatchOut& O, int* err, hipStream_t s, KTimer& kt,
+              int64_t m_host = -1) {
     if (D.p32 && m_host > 0)  // stage the 8-byte pairs where k_sw_expand reads them
       (void)hipMemcpyAsync(O.pos, O.refs, (size_t)m_host * 8, hipMemcpyDeviceToDevice, s);
     kt.mark("sw_expand", s);

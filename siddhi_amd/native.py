@@ -30,7 +30,9 @@ SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_
            "shp_shard_partition", "shp_shard_unpack", "shp_shard_partition_soa", "shp_comm_id",
            "shp_group_create", "shp_group_create_rank", "shp_group_push", "shp_group_stage", "shp_group_run",
            "shp_group_fetch_matches",
-           "shp_group_local_engines", "shp_group_engine", "shp_group_last_error", "shp_group_destroy"]
+           "shp_group_local_engines", "shp_group_engine", "shp_group_last_error", "shp_group_destroy",
+           "shp_dict_create", "shp_dict_intern", "shp_dict_size", "shp_dict_string", "shp_dict_destroy",
+           "shp_compile_siddhiql", "shp_siddhiql_queries", "shp_compile_last_error", "shp_engine_create_siddhiql"]
 
 
 class ShpConfig(ctypes.Structure):
@@ -125,6 +127,23 @@ def lib():
         L.shp_group_last_error.restype = ctypes.c_char_p
         L.shp_group_last_error.argtypes = [ctypes.c_void_p]
         L.shp_group_destroy.argtypes = [ctypes.c_void_p]
+        L.shp_dict_create.restype = ctypes.c_void_p
+        L.shp_dict_create.argtypes = [ctypes.c_int32]
+        L.shp_dict_intern.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]
+        L.shp_dict_intern.restype = ctypes.c_int32
+        L.shp_dict_size.argtypes = [ctypes.c_void_p]
+        L.shp_dict_size.restype = ctypes.c_int32
+        L.shp_dict_string.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t]
+        L.shp_dict_string.restype = ctypes.c_int64
+        L.shp_dict_destroy.argtypes = [ctypes.c_void_p]
+        L.shp_compile_siddhiql.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_char_p,
+                                           ctypes.c_size_t]
+        L.shp_compile_siddhiql.restype = ctypes.c_int64
+        L.shp_siddhiql_queries.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+        L.shp_siddhiql_queries.restype = ctypes.c_int64
+        L.shp_compile_last_error.restype = ctypes.c_char_p
+        L.shp_engine_create_siddhiql.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p,
+                                                 ctypes.POINTER(ShpConfig), ctypes.POINTER(ctypes.c_void_p)]
         _lib = L
     return _lib
 
@@ -169,20 +188,76 @@ def _check_columns(cols, nulls, col_bytes, n):
             raise ValueError(f"null array {i}: need {n} elements, got {len(m)}")
 
 
+class NativeDictionary:
+    """A string dictionary held by the library (shp_dict): the SiddhiQL lowering interns filter
+    constants in it, and the host encodes string column values with the same ids.  Callable like
+    query.compiler.Dictionary (str -> id)."""
+
+    def __init__(self, max_ids: int = 0):
+        self.h = lib().shp_dict_create(int(max_ids))
+
+    def __call__(self, s: str) -> int:
+        b = s.encode()
+        i = lib().shp_dict_intern(self.h, b, len(b))
+        if i < 0:
+            raise ShpError(i, "string dictionary full")
+        return i
+
+    @property
+    def strings(self):
+        L = lib()
+        out = []
+        for i in range(L.shp_dict_size(self.h)):
+            n = L.shp_dict_string(self.h, i, None, 0)
+            b = ctypes.create_string_buffer(n + 1)
+            L.shp_dict_string(self.h, i, b, n + 1)
+            out.append(b.raw[:n].decode())
+        return out
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().shp_dict_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def compile_siddhiql(app_text: str, query_name, ndict: NativeDictionary) -> str:
+    """The library's lowering of one query of a SiddhiQL app to its program JSON."""
+    L = lib()
+    q = None if query_name is None else query_name.encode()
+    n = L.shp_compile_siddhiql(app_text.encode(), q, ndict.h, None, 0)
+    if n < 0:
+        raise ShpError(int(n), L.shp_compile_last_error().decode())
+    buf = ctypes.create_string_buffer(n + 1)
+    L.shp_compile_siddhiql(app_text.encode(), q, ndict.h, buf, n + 1)
+    return buf.raw[:n].decode()
+
+
 class HipEngine:
     """One engine per query (libsiddhi_hip.so). Same interface as the test oracle."""
 
     def __init__(self, program_json: str, start_clock: int = 0, max_keys: int = 1 << 16,
                  max_batch: int = 1 << 20, max_matches: int = 0, device: int = 0, force_general: int = 0,
-                 profile_kernels: bool = False, match_layout: int = LAYOUT_FULL):
-        """force_general: 0 auto path, 1 general NFA lanes only, 2 no sweep path, 3 sweep whenever possible."""
+                 profile_kernels: bool = False, match_layout: int = LAYOUT_FULL, siddhiql=None):
+        """force_general: 0 auto path, 1 general NFA lanes only, 2 no sweep path, 3 sweep whenever possible.
+        siddhiql = (app_text, query_name, NativeDictionary): the engine is created from the SiddhiQL text
+        through shp_engine_create_siddhiql (the library lowers it); program_json is then ignored."""
         L = lib()
         cfg = ShpConfig(device, max_keys, max_batch, max_matches, int(start_clock), int(force_general),
                         int(profile_kernels), int(match_layout))
         h = ctypes.c_void_p()
-        rc = L.shp_engine_create(program_json.encode(), ctypes.byref(cfg), ctypes.byref(h))
+        if siddhiql is not None:
+            app_text, qname, ndict = siddhiql
+            program_json = compile_siddhiql(app_text, qname, ndict)
+            rc = L.shp_engine_create_siddhiql(app_text.encode(), None if qname is None else qname.encode(), ndict.h,
+                                              ctypes.byref(cfg), ctypes.byref(h))
+        else:
+            rc = L.shp_engine_create(program_json.encode(), ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:
             raise ShpError(rc, "shp_engine_create failed (see stderr)")
+        self.program_json = program_json
         self.h = h
         self.S = L.shp_engine_num_states(h)
         self.col_bytes = _column_bytes(program_json)

@@ -96,8 +96,17 @@ class _QueryRun:
 
 class SiddhiAppRuntime:
     def __init__(self, text: str, engine_factory: Callable, start_clock: Optional[int] = None,
-                 batch_size: int = 1 << 20):
-        self.strings = Dictionary()
+                 batch_size: int = 1 << 20, native_lowering: bool = False):
+        """native_lowering: engines are created from the SiddhiQL text by the library
+        (shp_engine_create_siddhiql), as the Java host does; string values then use the library's
+        dictionary, shared with the lowering's filter constants."""
+        self.text = text
+        self.native_lowering = native_lowering
+        if native_lowering:
+            from .native import NativeDictionary
+            self.strings = NativeDictionary()
+        else:
+            self.strings = Dictionary()
         self.keydict = Dictionary()
         self.app, self.compiled, _ = compile_app(text, self.strings)
         self._events: List[tuple] = []  # app event id -> (stream idx, ts, data)
@@ -142,7 +151,12 @@ class SiddhiAppRuntime:
             return
         start = self._start_clock if self._start_clock is not None else (0 if self.app.playback else self._t0)
         for cq in self.compiled:
-            eng = self._engine_factory(cq.program_json(), start)
+            if self.native_lowering:
+                eng = self._engine_factory(cq.program_json(), start, siddhiql=(self.text, cq.name, self.strings))
+                if eng.program_json != cq.program_json():
+                    raise AssertionError(f"native lowering of {cq.name} differs from query.compiler")
+            else:
+                eng = self._engine_factory(cq.program_json(), start)
             self.queries[cq.name] = _QueryRun(self, cq, eng)
 
     def _enqueue(self, stream: str, ts: int, data: list):

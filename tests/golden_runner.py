@@ -55,9 +55,10 @@ def rows_equal(r1, r2):
     return len(r1) == len(r2) and all(_eq(a, b) for a, b in zip(r1, r2))
 
 
-def run_fixture(fx, engine_factory):
+def run_fixture(fx, engine_factory, native_lowering=False):
     mgr = SiddhiManager(engine_factory)
-    rt = mgr.createSiddhiAppRuntime(fx["app"], start_clock=fx["start_clock"], batch_size=1)
+    rt = mgr.createSiddhiAppRuntime(fx["app"], start_clock=fx["start_clock"], batch_size=1,
+                                    native_lowering=native_lowering)
     rows = []
     cb = fx["callback"]["name"]
     rt.addCallback(cb, lambda ts, ins, rem: rows.extend(list(e.data) for e in (ins or [])))

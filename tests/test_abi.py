@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     src = open(os.path.join(ROOT, "include", "siddhi_hip.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|void\*?|double|const char\*|shp_engine\*)\s+(shp_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|void\*?|double|const char\*|shp_engine\*|shp_dict\*)\s+(shp_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_the_boundary():

@@ -22,8 +22,8 @@ FIXTURES = [f for f in load_fixtures() if f["name"] not in OUT_OF_SCOPE]
 def hip(force_general, max_keys=256, max_batch=1 << 16, **kw):
     from siddhi_amd.native import HipEngine
 
-    def make(pj, start):
-        return HipEngine(pj, start, max_keys=max_keys, max_batch=max_batch, force_general=force_general, **kw)
+    def make(pj, start, **extra):
+        return HipEngine(pj, start, max_keys=max_keys, max_batch=max_batch, force_general=force_general, **kw, **extra)
     return make
 
 
@@ -47,6 +47,14 @@ for _f in FIXTURES:
 @pytest.mark.parametrize("fx", FAST_FIXTURES, ids=[f["name"] for f in FAST_FIXTURES])
 def test_golden_default_path(fx):
     ok, msg, _ = run_fixture(fx, hip(False))
+    assert ok, f'{fx["source"]}: {msg}'
+
+
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["name"] for f in FIXTURES])
+def test_golden_siddhiql_entry_point(fx):
+    """Engines created only through shp_engine_create_siddhiql: the library lowers the app text
+    (the Java host's path), string values share the library's dictionary with the constants."""
+    ok, msg, _ = run_fixture(fx, hip(False), native_lowering=True)
     assert ok, f'{fx["source"]}: {msg}'
 
 
