@@ -18,9 +18,7 @@ import java.lang.foreign.MemorySegment;
 import java.lang.foreign.ValueLayout;
 import java.util.ArrayDeque;
 import java.util.ArrayList;
-import java.util.HashMap;
 import java.util.List;
-import java.util.Map;
 
 import static java.lang.foreign.ValueLayout.ADDRESS;
 import static java.lang.foreign.ValueLayout.JAVA_BYTE;
@@ -54,7 +52,7 @@ final class ColumnarBatch {
     private final MemorySegment ts, key, stream;
     private final MemorySegment[] cols, nulls;
     private final MemorySegment colPtrs, nullPtrs, descriptor;
-    private final Map<String, Integer> strings;       // string-attribute dictionary (shared with the filters)
+    private final NativeDictionary strings;           // string-attribute dictionary (shared with the filters)
     private long n;
     private long seq0;                                // sequence number of row 0 of this batch
     // rows of earlier batches still referenced by open partial matches: the engine reports match
@@ -65,7 +63,7 @@ final class ColumnarBatch {
     private final List<Object[]> rows = new ArrayList<>();
     private final List<long[]> rowMeta = new ArrayList<>();  // {ts, stream}
 
-    ColumnarBatch(Arena arena, long capacity, Column[] columns, Map<String, Integer> strings, int historyBatches) {
+    ColumnarBatch(Arena arena, long capacity, Column[] columns, NativeDictionary strings, int historyBatches) {
         this.arena = arena;
         this.capacity = capacity;
         this.columns = columns;
@@ -116,8 +114,7 @@ final class ColumnarBatch {
                 case 'f': cols[c].setAtIndex(JAVA_FLOAT, n, ((Number) v).floatValue()); break;
                 case 'd': cols[c].setAtIndex(JAVA_DOUBLE, n, ((Number) v).doubleValue()); break;
                 case 'b': cols[c].set(JAVA_BYTE, n, (byte) (((Boolean) v) ? 1 : 0)); break;
-                default: cols[c].setAtIndex(JAVA_INT, n, strings.computeIfAbsent(v.toString(),
-                        s -> strings.size())); break;
+                default: cols[c].setAtIndex(JAVA_INT, n, strings.id(v.toString())); break;
             }
         }
         rows.add(data);
@@ -138,7 +135,15 @@ final class ColumnarBatch {
         return descriptor;
     }
 
-    /** After a push: the rows move to the history (matches of later pushes may name them). */
+    /** After a failed push: the engine did not take the rows (its sequence counter did not move),
+     * so they are dropped and row 0 of the next batch keeps this batch's seq0. */
+    void discard() {
+        n = 0;
+        rows.clear();
+        rowMeta.clear();
+    }
+
+    /** After a successful push: the rows move to the history (matches of later pushes may name them). */
     void clear() {
         history.addLast(rows.toArray(new Object[0][]));
         long[] meta = new long[rows.size() * 2 + 1];
@@ -188,10 +193,6 @@ final class ColumnarBatch {
 
     long nextSeq() {
         return seq0 + n;
-    }
-
-    static Map<String, Integer> newDictionary() {
-        return new HashMap<>();
     }
 
     @SuppressWarnings("unused")

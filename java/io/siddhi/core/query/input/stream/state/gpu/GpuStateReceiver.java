@@ -3,8 +3,10 @@
  * 172-190) subscribes to a stream's junction for a GPU state query.  Replaces the
  * Pattern/Sequence{Single,Multi}ProcessStreamReceivers (core/query/input/stream/state/receiver/*):
  * instead of running the processor chain per event under synchronized(patternSyncObject), each
- * receive appends the event to the runtime's columnar batch; a synchronous send flushes on return,
- * so callbacks fire before InputHandler.send returns, as in the reference.
+ * receive appends the event to the runtime's columnar batch.  Under FlushPolicy.SYNC the batch is
+ * pushed when the receive call returns (callbacks fire before InputHandler.send returns, as in the
+ * reference; a send(Event[]) is one push); under DEFERRED it is pushed when full or by the
+ * runtime's flusher (GpuStateStreamRuntime.FlushPolicy).
  * Source only: no JDK in this repository's image (DESIGN.md §6).
  */
 package io.siddhi.core.query.input.stream.state.gpu;
@@ -35,7 +37,7 @@ public final class GpuStateReceiver extends ProcessStreamReceiver {
      * host maps the string to a dense id (0 when not partitioned). */
     private int keyId() {
         String key = queryContext.getSiddhiAppContext().getPartitionFlowId();
-        return key == null ? 0 : PartitionKeys.id(key);
+        return key == null ? 0 : runtime.keyId(key);
     }
 
     @Override
@@ -43,13 +45,13 @@ public final class GpuStateReceiver extends ProcessStreamReceiver {
         for (ComplexEvent e = complexEvent; e != null; e = e.getNext()) {
             runtime.append(e.getTimestamp(), keyId(), streamIndex, e.getOutputData());
         }
-        runtime.flush();
+        runtime.endOfReceive();
     }
 
     @Override
     public void receive(Event event) {
         runtime.append(event.getTimestamp(), keyId(), streamIndex, event.getData());
-        runtime.flush();
+        runtime.endOfReceive();
     }
 
     @Override
@@ -57,7 +59,7 @@ public final class GpuStateReceiver extends ProcessStreamReceiver {
         for (Event e : events) {
             runtime.append(e.getTimestamp(), keyId(), streamIndex, e.getData());
         }
-        runtime.flush();
+        runtime.endOfReceive();
     }
 
     @Override
@@ -65,32 +67,24 @@ public final class GpuStateReceiver extends ProcessStreamReceiver {
         for (Event e : events) {
             runtime.append(e.getTimestamp(), keyId(), streamIndex, e.getData());
         }
-        runtime.flush();
+        runtime.endOfReceive();
     }
 
     @Override
     public void receive(long timestamp, Object[] data) {
         runtime.append(timestamp, keyId(), streamIndex, data);
-        runtime.flush();
+        runtime.endOfReceive();
     }
 
     /** The partitioned path batched (PartitionStreamReceiver.java:176-216 appends here instead of
-     * one send() per key; the caller flushes once per incoming chunk). */
-    public void append(long timestamp, int keyId, Object[] data) {
-        runtime.append(timestamp, keyId, streamIndex, data);
+     * one send() per key; the caller calls endOfChunk() once per incoming chunk).  key: the
+     * partition key string (ValuePartitionExecutor.execute(...).toString()), mapped to a dense id
+     * by the runtime's own bounded dictionary (one per query runtime, not JVM-wide). */
+    public void append(long timestamp, String key, Object[] data) {
+        runtime.append(timestamp, key == null ? 0 : runtime.keyId(key), streamIndex, data);
     }
 
-    public void flush() {
-        runtime.flush();
-    }
-
-    /** Dense partition-key ids (the engine's cfg.max_keys bounds them). */
-    static final class PartitionKeys {
-        private static final java.util.concurrent.ConcurrentHashMap<String, Integer> IDS =
-                new java.util.concurrent.ConcurrentHashMap<>();
-
-        static int id(String key) {
-            return IDS.computeIfAbsent(key, k -> IDS.size());
-        }
+    public void endOfChunk() {
+        runtime.endOfReceive();
     }
 }

@@ -6,14 +6,17 @@
  * SiddhiAppRuntime, InputHandler.send, QuerySelector and the callbacks unchanged.
  *
  * Wiring (reference side):
- *   core/util/parser/InputStreamParser.java:88-93 — for a StateInputStream whose program the
- *     host can lower (the JSON siddhi_amd/query/compiler.py emits), return
- *     `new GpuStateStreamRuntime(...)` instead of StateInputStreamParser.parseInputStream(...).
+ *   core/util/parser/InputStreamParser.java:88-93 — for a StateInputStream, return
+ *     `GpuStateStreamRuntime.fromSiddhiQL(appText, queryName, ...)` instead of
+ *     StateInputStreamParser.parseInputStream(...): the library lowers the query text itself
+ *     (shp_engine_create_siddhiql; SHP_ERR_UNSUPPORTED = a construct outside the state path, and
+ *     the host keeps the reference runtime for that query).
  *   core/util/SiddhiAppRuntimeBuilder.java:172-190 — unchanged: it subscribes the receivers
  *     getSingleStreamRuntimes() returns (GpuStateReceiver, one per distinct stream).
  *   core/partition/PartitionStreamReceiver.java:176-283 — for a partitioned GPU query, append
- *     (key dictionary id, event) to the same batch instead of one send() per key
- *     (GpuStateReceiver.receive(long, Object[], int keyId)); the engine partitions on the device.
+ *     (key string, event) to the same batch instead of one send() per key
+ *     (GpuStateReceiver.append(ts, key, data), then endOfChunk()); the runtime maps the key to a
+ *     dense id with its own bounded dictionary and the engine partitions on the device.
  *
  * Concurrency: the reference serialises a query with synchronized(patternSyncObject)
  * (SingleProcessStreamReceiver.java:52); every entry point here takes `lock`.
@@ -40,7 +43,10 @@ import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
 import java.util.ArrayList;
 import java.util.List;
-import java.util.Map;
+import java.util.concurrent.Executors;
+import java.util.concurrent.ScheduledExecutorService;
+import java.util.concurrent.ScheduledFuture;
+import java.util.concurrent.TimeUnit;
 import java.util.concurrent.locks.ReentrantLock;
 
 import static java.lang.foreign.ValueLayout.ADDRESS;
@@ -50,6 +56,16 @@ import static java.lang.foreign.ValueLayout.JAVA_LONG;
 import static java.lang.foreign.ValueLayout.JAVA_SHORT;
 
 public final class GpuStateStreamRuntime implements StreamRuntime {
+
+    /** When appended events reach the engine (and so when callbacks fire).
+     * SYNC: at the end of every receive(...) call -- one push per InputHandler.send, callbacks
+     *   fire before send returns, as in the reference (a send(Event[]) is one push).
+     * DEFERRED: when the batch is full, every maxDelayMillis on a flusher thread, and before any
+     *   point that observes state (advanceClock, snapshot, shutdown); callbacks then fire on the
+     *   flusher (or the filling sender's) thread, as with an @async junction
+     *   (core/stream/StreamJunction.java:101-131).  Synchronous single-event senders then share one
+     *   push instead of paying a full push (sort, kernels, status read) per event. */
+    public enum FlushPolicy { SYNC, DEFERRED }
 
     private final Arena arena = Arena.ofShared();
     private final ReentrantLock lock = new ReentrantLock();
@@ -61,11 +77,40 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
     private final int outputDataSize;
     private final List<SingleStreamRuntime> singleStreamRuntimes = new ArrayList<>();
     private Processor selector;                    // QuerySelector (setCommonProcessor)
+    private final NativeDictionary strings;        // string values, shared with the filters' constants
+    private final NativeDictionary keys;           // partition keys, bounded by max_keys
+    private final FlushPolicy policy;
+    private final ScheduledExecutorService flusher;
+    private final ScheduledFuture<?> flushTask;
 
     /**
-     * @param programJson  the flattened processor graph (siddhi_amd/query/compiler.py's format:
-     *                     processors, next/every/partner links, within, start states, filters as
-     *                     predicate bytecode) the host lowers from the StateInputStream
+     * The Java host's entry point: the library lowers the query from the app text
+     * (shp_engine_create_siddhiql), so nothing on the Java side builds a program.
+     *
+     * @param appText    the SiddhiQL app (what SiddhiManager.createSiddhiAppRuntime was given)
+     * @param queryName  the query's @info(name=...) (or "query<N>" by position in the app)
+     */
+    public static GpuStateStreamRuntime fromSiddhiQL(String appText, String queryName, int maxKeys, long maxBatch,
+                                                     int device, long startClock, MetaStateEvent metaStateEvent,
+                                                     SiddhiQueryContext queryContext, FlushPolicy policy,
+                                                     long maxDelayMillis) {
+        NativeDictionary strings = new NativeDictionary(0, "string values");
+        String program;
+        try {
+            program = ShpNative.compileSiddhiQL(appText, queryName, strings);
+        } catch (IllegalArgumentException e) {
+            strings.close();
+            throw new SiddhiAppCreationException("shp_compile_siddhiql: " + e.getMessage(), e);
+        }
+        ProgramInfo info = ProgramInfo.parse(program);
+        return new GpuStateStreamRuntime(appText, queryName, info.streams, info.columns,
+                info.partitioned ? maxKeys : 1, maxBatch, device, startClock, metaStateEvent, queryContext, strings,
+                policy, maxDelayMillis);
+    }
+
+    /**
+     * @param appText      the SiddhiQL app; the library lowers query `queryName` of it
+     *                     (shp_engine_create_siddhiql), interning string constants in `strings`
      * @param streamIds    the program's streams, in program["streams"] order
      * @param columns      program["columns"]
      * @param maxKeys      partition-key dictionary capacity (1 when the query is not partitioned)
@@ -73,11 +118,14 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
      * @param device       HIP device ordinal
      * @param startClock   the event-time clock at start() (0 in playback mode)
      */
-    public GpuStateStreamRuntime(String programJson, String[] streamIds, ColumnarBatch.Column[] columns,
-                                 int maxKeys, long maxBatch, int device, long startClock,
-                                 MetaStateEvent metaStateEvent, SiddhiQueryContext queryContext,
-                                 Map<String, Integer> stringDictionary) {
+    GpuStateStreamRuntime(String appText, String queryName, String[] streamIds, ColumnarBatch.Column[] columns,
+                          int maxKeys, long maxBatch, int device, long startClock,
+                          MetaStateEvent metaStateEvent, SiddhiQueryContext queryContext,
+                          NativeDictionary strings, FlushPolicy policy, long maxDelayMillis) {
         this.metaStateEvent = metaStateEvent;
+        this.strings = strings;
+        this.keys = new NativeDictionary(maxKeys, "partition keys (max_keys = " + maxKeys + ")");
+        this.policy = policy;
         this.outputDataSize = metaStateEvent.getOutputDataAttributes() == null ? 0
                 : metaStateEvent.getOutputDataAttributes().size();
         MemorySegment cfg = arena.allocate(ShpNative.CONFIG);
@@ -92,14 +140,15 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
         MemorySegment out = arena.allocate(ADDRESS);
         int rc;
         try {
-            rc = (int) ShpNative.ENGINE_CREATE.invokeExact(arena.allocateFrom(programJson), cfg, out);
+            rc = (int) ShpNative.ENGINE_CREATE_SIDDHIQL.invokeExact(arena.allocateFrom(appText),
+                    queryName == null ? MemorySegment.NULL : arena.allocateFrom(queryName), strings.handle(), cfg, out);
         } catch (Throwable t) {
-            throw new SiddhiAppCreationException("shp_engine_create failed: " + t, t);
+            throw new SiddhiAppCreationException("shp_engine_create_siddhiql failed: " + t, t);
         }
         if (rc != ShpNative.OK) {
             // SHP_ERR_UNSUPPORTED = a construct outside the state path: the host falls back to
             // StateInputStreamParser (the reference runtime) for this query
-            throw new SiddhiAppCreationException("shp_engine_create: " + ShpNative.codeName(rc));
+            throw new SiddhiAppCreationException("shp_engine_create_siddhiql: " + ShpNative.codeName(rc));
         }
         engine = out.get(ADDRESS, 0);
         matches = arena.allocate(ShpNative.MATCHES);
@@ -108,11 +157,35 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
         } catch (Throwable t) {
             throw new SiddhiAppCreationException("shp_engine_num_states failed", t);
         }
-        batch = new ColumnarBatch(arena, maxBatch, columns, stringDictionary, 64);
+        batch = new ColumnarBatch(arena, maxBatch, columns, strings, 64);
         for (int s = 0; s < streamIds.length; s++) {
             GpuStateReceiver r = new GpuStateReceiver(streamIds[s], s, this, queryContext);
             singleStreamRuntimes.add(new SingleStreamRuntime(r, null, ProcessingMode.BATCH,
                     metaStateEvent.getMetaStreamEvent(s)));
+        }
+        if (policy == FlushPolicy.DEFERRED) {
+            flusher = Executors.newSingleThreadScheduledExecutor(r -> {
+                Thread t = new Thread(r, "siddhi-gpu-flush");
+                t.setDaemon(true);
+                return t;
+            });
+            long d = Math.max(1, maxDelayMillis);
+            flushTask = flusher.scheduleWithFixedDelay(this::flush, d, d, TimeUnit.MILLISECONDS);
+        } else {
+            flusher = null;
+            flushTask = null;
+        }
+    }
+
+    /** Dense id of a partition key string (the key of the current partition flow). */
+    int keyId(String key) {
+        return keys.id(key);
+    }
+
+    /** A receive(...) call returned: SYNC pushes now (callbacks before InputHandler.send returns). */
+    void endOfReceive() {
+        if (policy == FlushPolicy.SYNC) {
+            flush();
         }
     }
 
@@ -167,13 +240,18 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
             try {
                 rc = (int) ShpNative.PUSH_BATCH.invokeExact(engine, batch.descriptor(), matches);
             } catch (Throwable t) {
+                batch.discard();
                 throw new SiddhiAppRuntimeException("shp_push_batch failed: " + t, t);
             }
-            batch.clear();
             if (rc != ShpNative.OK) {
+                // the engine left its state (and its sequence counter) as before the push: drop the
+                // rows without advancing the batch's seq0, so later matches keep resolving to the
+                // right rows
+                batch.discard();
                 throw new SiddhiAppRuntimeException("shp_push_batch: " + ShpNative.codeName(rc) + ": "
                         + ShpNative.lastError(engine));
             }
+            batch.clear();
             deliver();
         } finally {
             lock.unlock();
@@ -299,10 +377,16 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
 
     /** SiddhiAppRuntime.shutdown for the query. */
     public void shutdown() {
+        if (flushTask != null) {
+            flushTask.cancel(false);
+            flusher.shutdown();
+        }
         lock.lock();
         try {
             flush();
             ShpNative.ENGINE_DESTROY.invokeExact(engine);
+            keys.close();
+            strings.close();
         } catch (Throwable t) {
             throw new SiddhiAppRuntimeException("shp_engine_destroy failed: " + t, t);
         } finally {

@@ -81,6 +81,18 @@ final class ShpNative {
     static final MethodHandle LAST_ERROR = fn("shp_last_error", ADDRESS, ADDRESS);
     static final MethodHandle ENGINE_DESTROY = fnVoid("shp_engine_destroy", ADDRESS);
 
+    // ---- SiddhiQL lowering inside the library (StateInputStreamParser.parse + ExpressionParser)
+    static final MethodHandle DICT_CREATE = fn("shp_dict_create", ADDRESS, JAVA_INT);
+    static final MethodHandle DICT_INTERN = fn("shp_dict_intern", JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG);
+    static final MethodHandle DICT_SIZE = fn("shp_dict_size", JAVA_INT, ADDRESS);
+    static final MethodHandle DICT_DESTROY = fnVoid("shp_dict_destroy", ADDRESS);
+    static final MethodHandle COMPILE_SIDDHIQL = fn("shp_compile_siddhiql", JAVA_LONG, ADDRESS, ADDRESS, ADDRESS,
+            ADDRESS, JAVA_LONG);
+    static final MethodHandle SIDDHIQL_QUERIES = fn("shp_siddhiql_queries", JAVA_LONG, ADDRESS, ADDRESS, JAVA_LONG);
+    static final MethodHandle COMPILE_LAST_ERROR = fn("shp_compile_last_error", ADDRESS);
+    static final MethodHandle ENGINE_CREATE_SIDDHIQL = fn("shp_engine_create_siddhiql", JAVA_INT, ADDRESS, ADDRESS,
+            ADDRESS, ADDRESS, ADDRESS);
+
     // ---- page-locked receive memory for match payloads
     static final MethodHandle HOST_REGISTER = fn("shp_host_register", JAVA_INT, ADDRESS, JAVA_LONG);
     static final MethodHandle HOST_UNREGISTER = fn("shp_host_unregister", JAVA_INT, ADDRESS);
@@ -120,6 +132,36 @@ final class ShpNative {
             return s.reinterpret(1 << 16).getString(0);
         } catch (Throwable t) {
             return "shp_last_error failed: " + t;
+        }
+    }
+
+    /** The calling thread's last lowering error (shp_compile_last_error). */
+    static String compileLastError() {
+        try {
+            MemorySegment s = (MemorySegment) COMPILE_LAST_ERROR.invokeExact();
+            return s.reinterpret(1 << 16).getString(0);
+        } catch (Throwable t) {
+            return "shp_compile_last_error failed: " + t;
+        }
+    }
+
+    /** The program JSON of one query of a SiddhiQL app, lowered by the library (shp_compile_siddhiql);
+     * string constants are interned in `dict`. */
+    static String compileSiddhiQL(String appText, String queryName, NativeDictionary dict) {
+        try (Arena a = Arena.ofConfined()) {
+            MemorySegment app = a.allocateFrom(appText);
+            MemorySegment q = queryName == null ? MemorySegment.NULL : a.allocateFrom(queryName);
+            long n = (long) COMPILE_SIDDHIQL.invokeExact(app, q, dict.handle(), MemorySegment.NULL, 0L);
+            if (n < 0) {
+                throw new IllegalArgumentException(codeName((int) n) + ": " + compileLastError());
+            }
+            MemorySegment out = a.allocate(n + 1);
+            long got = (long) COMPILE_SIDDHIQL.invokeExact(app, q, dict.handle(), out, n + 1);
+            return out.getString(0);
+        } catch (RuntimeException e) {
+            throw e;
+        } catch (Throwable t) {
+            throw new IllegalStateException("shp_compile_siddhiql failed: " + t, t);
         }
     }
 

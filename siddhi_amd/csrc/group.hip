@@ -457,6 +457,16 @@ int stage_impl(shp_group& g, const shp_batch* slices) {
     base[r + 1] = base[r] + all[(size_t)r * (G + 2) + G];
     seed[r + 1] = std::max(seed[r], all[(size_t)r * (G + 2) + G + 1]);
   }
+  // every rank's receive total from the all-gathered counts (identical on every rank): if any
+  // rank would overflow, every rank fails here, before any exchange is posted (a rank that failed
+  // alone would leave its peers blocked in ncclSend / ncclRecv to it)
+  for (int d = 0; d < G; d++) {
+    int64_t tot = 0;
+    for (int s = 0; s < G; s++) tot += cnt(s, d);
+    if (tot + 1 > g.cfg.max_batch)
+      return g.fail(SHP_ERR_CAPACITY, "rank " + std::to_string(d) + " would receive " + std::to_string(tot) +
+                                          " events (> max_batch)");
+  }
   for (int i = 0; i < g.nlocal; i++) {
     shp_group::Local::Slot& r = g.L[i].slot[sl];
     r.recv_cnt.assign(G, 0);
