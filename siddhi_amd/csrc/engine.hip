@@ -110,27 +110,26 @@ __global__ void k_sort_keys_chk(const int32_t* key, const int32_t* stream, int64
   if (e) atomicOr(err, e);
 }
 
-// each key's run in the key-sorted batch: kbeg = its first position, kend = one past its last
-// (both zero for a key without events); one coalesced pass instead of a histogram of global
-// atomics (3.7 ms per 100M events at 1M keys)
-__global__ void k_key_bounds(const uint32_t* __restrict__ sk, int64_t n, uint32_t* kbeg, uint32_t* kend, uint32_t nk) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t k = sk[i];
-    // keys with no event start where they would (kbeg = kend): per-key output regions derived
-    // from kbeg (the logical-absent path) stay disjoint
-    const uint32_t k0 = i == 0 ? 0u : min(sk[i - 1] + 1u, nk);
-    for (uint32_t a = k0; a < min(k, nk); a++) kbeg[a] = kend[a] = (uint32_t)i;
-    if (i + 1 == n)
-      for (uint32_t a = min(k + 1u, nk); a < nk; a++) kbeg[a] = kend[a] = (uint32_t)n;
-    if (k >= nk) continue;
-    if (i == 0 || sk[i - 1] != k) kbeg[k] = (uint32_t)i;
-    if (i + 1 == n || sk[i + 1] != k) kend[k] = (uint32_t)(i + 1);
+// each key's run in the key-sorted batch: kbeg = its first position, kcnt = its length (a key
+// without events starts where it would: kbeg = lower bound, kcnt = 0, so per-key output regions
+// derived from kbeg -- the logical-absent path -- stay disjoint).  One thread per key, two binary
+// searches over the sorted keys: a push touching few keys of a large key range costs O(keys log n),
+// not a serial fill of the missing keys' bounds by the threads at key boundaries.
+__device__ __forceinline__ uint32_t key_lower_bound(const uint32_t* __restrict__ sk, int64_t n, uint32_t k) {
+  int64_t a = 0, b = n;
+  while (a < b) {
+    const int64_t m = a + ((b - a) >> 1);
+    if (sk[m] < k) a = m + 1;
+    else b = m;
   }
+  return (uint32_t)a;
 }
-__global__ void k_key_len(const uint32_t* kbeg, uint32_t* kcnt, int32_t nk) {
+__global__ void k_key_bounds(const uint32_t* __restrict__ sk, int64_t n, uint32_t* kbeg, uint32_t* kcnt, uint32_t nk) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < nk) kcnt[k] -= kbeg[k];
+  if (k >= nk) return;
+  const uint32_t a = key_lower_bound(sk, n, (uint32_t)k), b = key_lower_bound(sk, n, (uint32_t)k + 1u);
+  kbeg[k] = a;
+  kcnt[k] = b - a;
 }
 
 __global__ void k_clamp_clock(int64_t* rmax, int64_t n, int64_t clock0) {
@@ -352,6 +351,7 @@ struct shp_engine {
   double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
   int64_t last_m = 0;
   int64_t pushes = 0, lean_pushes = 0, lean_fallbacks = 0, labs_fallbacks = 0;  // shp_engine_stat
+  int64_t spill_reruns = 0;
 
   ~shp_engine() { release(); }
 
@@ -578,6 +578,7 @@ struct shp_engine {
       HIP_OK(hipEventRecord(ev1, stream));
       if (!clock_only && n > 0 && sw.lean_push_for(B)) lean_pushes++;
       if (!clock_only) sw.run(B, x_key, O, d_err, stream, kt);
+      if (!clock_only && n > 0) sw.spill(B, O, d_err, stream, kt);  // spilled owners (none: no launch)
       lastB = B;
       lastKey = x_key;
       expanded = false;
@@ -623,8 +624,8 @@ struct shp_engine {
       HIP_OK(rocprim::radix_sort_pairs(d_tmp, tb, d_skey, d_skey2, d_idx, d_perm, (size_t)n, 0, key_bits + 1, stream));
       if (bounds) {
         kt.mark("key_bounds", stream);
-        k_key_bounds<<<gb, 256, 0, stream>>>(d_skey2, n, d_kbeg, d_kcnt, (uint32_t)cfg.max_keys);
-        k_key_len<<<(unsigned)((cfg.max_keys + 255) / 256), 256, 0, stream>>>(d_kbeg, d_kcnt, cfg.max_keys);
+        k_key_bounds<<<(unsigned)((cfg.max_keys + 255) / 256), 256, 0, stream>>>(d_skey2, n, d_kbeg, d_kcnt,
+                                                                                (uint32_t)cfg.max_keys);
       }
       kt.mark(nullptr, stream);
       HIP_OK(hipEventRecord(ev1, stream));
@@ -667,6 +668,23 @@ struct shp_engine {
       lean_fallbacks++;
       HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
       sw.solve(B, O, d_err, stream, kt);
+      sw.spill(B, O, d_err, stream, kt);
+      if (cfg.match_layout == SHP_LAYOUT_FULL) sw.expand(B, x_key, O, d_err, stream, kt);
+      HIP_OK(hipEventRecord(ev2, stream));
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      std::memcpy(&herr, h_status + 2, sizeof(int));
+    }
+    if (fast == 2 && (herr & SWE_SPILL) && !(herr & (SWE_KEYS | SWE_RANGE))) {
+      // an owner's open candidates outgrew the LDS solves' carry (the reference's lists are
+      // unbounded): it becomes a spilled owner (sweep_spill.h) and the push re-runs from the same
+      // committed state, the spilled owners on k_sw_spill
+      spill_reruns++;
+      HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
+      sw.mark_spilled(stream);
+      sw.solve(B, O, d_err, stream, kt);
+      sw.spill(B, O, d_err, stream, kt);
       if (cfg.match_layout == SHP_LAYOUT_FULL) sw.expand(B, x_key, O, d_err, stream, kt);
       HIP_OK(hipEventRecord(ev2, stream));
       HIP_OK(hipGetLastError());
@@ -707,7 +725,10 @@ struct shp_engine {
       // succeeded advances them (a failed push leaves the sweep path's state as it was)
       if (tsmax != INT64_MIN && tsmax > clock) clock = tsmax;
       if (!clock_only) seq += n;
-      if (fast == 2) sw.commit();
+      if (fast == 2) {
+        sw.commit();
+        sw.spill_settle(stream);
+      }
       if (fast == 3) cs.commit();
       if (fast == 4) la.commit();
       if (fast == 0) std::swap(arena, arena2);
@@ -789,6 +810,16 @@ struct shp_engine {
         v.push_back({D.agg_s[c], (size_t)no * SW_LK * 8});
         v.push_back({D.agg_c[c], (size_t)no * SW_LK * 8});
       }
+      // spilled owners: flags, their pool segments, and the pool copy (its current capacity)
+      const size_t pc = (size_t)sw.pool_cap[c];
+      v.push_back({D.spilled[c], (size_t)no});
+      v.push_back({D.sp_n[c], (size_t)no * 4});
+      v.push_back({D.sp_base[c], (size_t)no * 8});
+      v.push_back({D.p_ts[c], pc * 8});
+      v.push_back({D.p_seq[c], pc * 8});
+      v.push_back({D.p_v[c], pc * 4});
+      v.push_back({D.p_lk[c], pc});
+      v.push_back({D.p_null[c], pc});
     } else if (fast == 4) {
       const LabsDev& L = la.D;
       v = {{L.pend[L.cur], (size_t)nk * sizeof(LaPend)}, {L.wq[L.cur], (size_t)nk * L.wcap * sizeof(LaWait)}};
@@ -832,7 +863,7 @@ struct shp_engine {
     snap.assign(sizeof(SnapHeader) + payload, 0);
     SnapHeader h{};
     memcpy(h.magic, "SHPSNAP1", 8);
-    h.version = 2;
+    h.version = 3;
     h.path = fast;
     h.max_keys = cfg.max_keys;
     h.seq = seq;
@@ -859,7 +890,7 @@ struct shp_engine {
     SnapHeader h;
     if (!buf || len < sizeof h) return fail(SHP_ERR_ARG, "snapshot too short");
     memcpy(&h, buf, sizeof h);
-    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 2) return fail(SHP_ERR_ARG, "not a snapshot (or of another version)");
+    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 3) return fail(SHP_ERR_ARG, "not a snapshot (or of another version)");
     if (h.path != fast || h.max_keys != cfg.max_keys || h.program_hash != fnv1a(program))
       return fail(SHP_ERR_ARG, "snapshot is of a different query, path or key capacity");
     if (fast == 0 && (h.pad < 0 || h.pad >= LANE_TIERS)) return fail(SHP_ERR_ARG, "snapshot capacity tier unknown");
@@ -875,6 +906,20 @@ struct shp_engine {
       Yn.build(cfg.max_keys, h.pad);
       if (sizeof h + 8 + (size_t)Yn.bytes != len) return fail(SHP_ERR_ARG, "snapshot layout mismatch");
       if (!set_tier(h.pad, false)) return fail(SHP_ERR_CAPACITY, "no device memory for the snapshot's capacity tier");
+    }
+    if (fast == 2) {  // the blob's pool capacity (the 5th-last section holds its ts column)
+      const char* q0 = (const char*)buf + sizeof h;
+      std::vector<uint64_t> sz;
+      for (int64_t i = 0; i < h.sections && (size_t)(q0 - (const char*)buf) + 8 <= len; i++) {
+        uint64_t b;
+        memcpy(&b, q0, 8);
+        sz.push_back(b);
+        q0 += 8 + b;
+      }
+      if (sz.size() < 5) return fail(SHP_ERR_ARG, "snapshot layout mismatch");
+      const int64_t pc = (int64_t)(sz[sz.size() - 5] / 8);
+      HIP_OK(hipStreamSynchronize(stream));
+      sw.pool_exact(sw.D.cur, pc);
     }
     auto secs = state_sections();
     if ((size_t)h.sections != secs.size() || sizeof h + (size_t)h.payload != len)
@@ -896,7 +941,10 @@ struct shp_engine {
     }
     seq = h.seq;
     clock = h.clock;
-    if (fast == 2) sw.D.maybe_null = h.maybe_null;
+    if (fast == 2) {
+      sw.D.maybe_null = h.maybe_null;
+      sw.D.spill_on = sw.count_spilled() > 0;
+    }
     return SHP_OK;
   }
 
@@ -911,7 +959,7 @@ struct shp_engine {
     SnapHeader h;
     if (!buf || len < sizeof h) throw std::runtime_error("snapshot too short");
     memcpy(&h, buf, sizeof h);
-    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 2 || h.path != fast || h.max_keys != cfg.max_keys ||
+    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 3 || h.path != fast || h.max_keys != cfg.max_keys ||
         h.program_hash != fnv1a(program))
       throw std::runtime_error("not a snapshot of this engine's query, path and key capacity");
     LaneLayout Yb = Y;  // lanes: the layout of the snapshot's capacity tier
@@ -930,6 +978,7 @@ struct shp_engine {
     for (size_t i = 0; i < secs.size(); i++) {
       uint64_t b;
       memcpy(&b, q, 8);
+      if (fast == 2 && i + 5 >= secs.size()) secs[i].bytes = b;  // the pool: the blob's capacity
       if (b != secs[i].bytes || (size_t)(q + 8 + b - (const char*)buf) > len)
         throw std::runtime_error("snapshot layout mismatch");
       sp[i] = q + 8;
@@ -1030,11 +1079,26 @@ struct shp_engine {
         const int64_t* c_seq = (const int64_t*)sp[2];
         const uint8_t* c_lk = (const uint8_t*)sp[4];
         const uint8_t* lc = (const uint8_t*)sp[6];
+        const size_t s0 = sw.D.agg ? 9 : 7;  // spill sections: spilled, sp_n, sp_base, pool ts / seq / v / lk / null
+        const uint8_t* spl = (const uint8_t*)sp[s0];
+        const int32_t* spn = (const int32_t*)sp[s0 + 1];
+        const int64_t* spb = (const int64_t*)sp[s0 + 2];
+        const int64_t* p_ts = (const int64_t*)sp[s0 + 3];
+        const int64_t* p_seq = (const int64_t*)sp[s0 + 4];
+        const uint8_t* p_lk = (const uint8_t*)sp[s0 + 6];
         for (int32_t ow = 0; ow < nown; ow++) {
-          for (int i = 0; i < c_n[ow]; i++) {
-            const int64_t c = (int64_t)ow * SWS_CCAP + i;
-            const int32_t k = inv[(size_t)ow * SW_LK + c_lk[c]];
-            if (k >= 0) open[k].push_back({c_seq[c], c_ts[c]});
+          if (spl[ow] && spn[ow] >= 0) {  // a spilled owner: its open candidates are in the pool
+            for (int64_t i = 0; i < spn[ow]; i++) {
+              const int64_t c = spb[ow] + i;
+              const int32_t k = inv[(size_t)ow * SW_LK + p_lk[c]];
+              if (k >= 0) open[k].push_back({p_seq[c], p_ts[c]});
+            }
+          } else {
+            for (int i = 0; i < c_n[ow]; i++) {
+              const int64_t c = (int64_t)ow * SWS_CCAP + i;
+              const int32_t k = inv[(size_t)ow * SW_LK + c_lk[c]];
+              if (k >= 0) open[k].push_back({c_seq[c], c_ts[c]});
+            }
           }
           for (int l = 0; l < SW_LK; l++) {
             const int32_t k = inv[(size_t)ow * SW_LK + l];
@@ -1466,6 +1530,8 @@ int64_t shp_engine_stat(const shp_engine* e, const char* which) {
   if (w == "lean_pushes") return e->lean_pushes;
   if (w == "lean_fallbacks") return e->lean_fallbacks;
   if (w == "labs_fallbacks") return e->labs_fallbacks;
+  if (w == "spill_reruns") return e->spill_reruns;
+  if (w == "spilled_owners") return e->fast == 2 ? e->sw.count_spilled() : 0;
   return -1;
 }
 

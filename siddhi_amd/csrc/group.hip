@@ -48,7 +48,7 @@ namespace {
 constexpr int GS_THREADS = 256;
 constexpr int GS_TILE = 65536;  // events per split workgroup
 constexpr int GS_MAXG = 16;
-constexpr int GS_MAXCOL = 12;
+constexpr int GS_MAXCOL = 20;
 
 // columns moved by the split: in[c] (4 or 8 bytes per event) -> out[c] grouped by destination
 struct GsCols {
@@ -179,7 +179,8 @@ __global__ __launch_bounds__(GS_THREADS) void k_gs_scatter(const int32_t* __rest
       okey[o] = (int32_t)((uint32_t)key[i] / (uint32_t)G);
       for (int c = 0; c < cols.n; c++) {
         if (cols.sz[c] == 8) ((int64_t*)cols.out[c])[o] = ((const int64_t*)cols.in[c])[i];
-        else ((int32_t*)cols.out[c])[o] = ((const int32_t*)cols.in[c])[i];
+        else if (cols.sz[c] == 4) ((int32_t*)cols.out[c])[o] = ((const int32_t*)cols.in[c])[i];
+        else ((uint8_t*)cols.out[c])[o] = ((const uint8_t*)cols.in[c])[i];  // null bytes
       }
       if (oclk) oclk[o] = max(seed, rmax[i]);
       if (oseq) oseq[o] = seq_base + i;
@@ -237,14 +238,17 @@ struct shp_group {
     DevBuf cnt, off, tot, tsmax, rmax, scan_tmp;
     // send (destination-grouped) columns: ts, key, stream, clock, seq, predicate columns
     DevBuf s_ts, s_key, s_stream, s_clk, s_seq;
-    DevBuf s_col[shp::MAXCOL];
+    DevBuf s_col[shp::MAXCOL], s_null[shp::MAXCOL];
+    DevBuf zero;                    // zero bytes: the null column of a slice without one
     int64_t n_slice = 0;
     int64_t max_ts = INT64_MIN;
+    uint32_t null_mask = 0;         // columns this rank's slice carries a null array for
     std::vector<int64_t> send_cnt;  // per destination
     // three receive slots: batch i + 2 can be exchanged while the engines run batch i
     struct Slot {
       DevBuf r_ts, r_key, r_stream, r_clk, r_seq;
-      DevBuf r_col[shp::MAXCOL];
+      DevBuf r_col[shp::MAXCOL], r_null[shp::MAXCOL];
+      uint32_t null_cols = 0;         // columns whose null bytes this batch exchanges
       std::vector<int64_t> recv_cnt;  // per source
       int64_t n_recv = 0;
       int64_t push_clock = INT64_MIN, next_seq = 0;
@@ -308,11 +312,15 @@ void split_count(shp_group& g, shp_group::Local& l, const shp_batch& b) {
   GH(hipStreamSynchronize(l.s));
   l.send_cnt.assign(tot.begin(), tot.begin() + G);
   l.n_slice = n;
+  l.null_mask = 0;
+  for (int c = 0; c < g.ncol; c++)
+    if (b.nulls && b.nulls[c]) l.null_mask |= 1u << c;
   l.max_ts = mx ? (int64_t)(mx ^ (1ull << 63)) : INT64_MIN;
 }
 
 // step 1b: the scatter into destination-grouped send columns
-void split_scatter(shp_group& g, shp_group::Local& l, const shp_batch& b, int64_t clock_seed, int64_t seq_base) {
+void split_scatter(shp_group& g, shp_group::Local& l, const shp_batch& b, int64_t clock_seed, int64_t seq_base,
+                   uint32_t null_cols) {
   GH(hipSetDevice(l.dev));
   const int G = g.world;
   const int64_t n = b.n;
@@ -335,6 +343,20 @@ void split_scatter(shp_group& g, shp_group::Local& l, const shp_batch& b, int64_
     const int sz = col_bytes(g.ctag[c]);
     if (sz == 1) throw std::runtime_error("group: bool columns are not exchanged");
     add(b.cols[c], l.s_col[c], sz);
+  }
+  // null bytes travel as 1-byte columns for every column some rank's slice has nulls in (the
+  // same set on every rank: the masks are all-gathered); a slice without them sends zeros
+  for (int c = 0; c < g.ncol; c++) {
+    if (!((null_cols >> c) & 1u)) continue;
+    const uint8_t* in = (b.nulls && b.nulls[c]) ? b.nulls[c] : nullptr;
+    if (!in) {
+      if (l.zero.bytes < cap) {
+        l.zero.ensure(cap);
+        GH(hipMemsetAsync(l.zero.p, 0, l.zero.bytes, l.s));
+      }
+      in = (const uint8_t*)l.zero.p;
+    }
+    add(in, l.s_null[c], 1);
   }
   int64_t* oclk = nullptr;
   if (g.need_clock && n > 0) {  // the global clock after each event: running max of ts, seeded
@@ -370,6 +392,8 @@ void ensure_recv(shp_group& g, shp_group::Local::Slot& r, int64_t n) {
   if (g.need_clock) r.r_clk.ensure(cap * 8);
   if (g.need_seq) r.r_seq.ensure(cap * 8);
   for (int c = 0; c < g.ncol; c++) r.r_col[c].ensure(cap * col_bytes(g.ctag[c]));
+  for (int c = 0; c < g.ncol; c++)
+    if ((r.null_cols >> c) & 1u) r.r_null[c].ensure(cap);
 }
 
 // the columns exchanged, as (send buffer, receive buffer, bytes per event)
@@ -380,6 +404,8 @@ std::vector<std::tuple<void*, void*, int>> column_pairs(shp_group& g, shp_group:
   if (g.need_clock) v.emplace_back(src.s_clk.p, dst.r_clk.p, 8);
   if (g.need_seq) v.emplace_back(src.s_seq.p, dst.r_seq.p, 8);
   for (int c = 0; c < g.ncol; c++) v.emplace_back(src.s_col[c].p, dst.r_col[c].p, col_bytes(g.ctag[c]));
+  for (int c = 0; c < g.ncol; c++)
+    if ((dst.null_cols >> c) & 1u) v.emplace_back(src.s_null[c].p, dst.r_null[c].p, 1);
   return v;
 }
 
@@ -398,7 +424,10 @@ int run_local(shp_group& g, shp_group::Local& l, shp_group::Local::Slot& r) {
   b.key = (const int32_t*)r.r_key.p;
   b.stream = (const int32_t*)r.r_stream.p;
   b.cols = colp.data();
-  b.nulls = nullptr;
+  std::vector<const uint8_t*> nullp(std::max(1, g.ncol), nullptr);
+  for (int c = 0; c < g.ncol; c++)
+    if ((r.null_cols >> c) & 1u) nullp[c] = (const uint8_t*)r.r_null[c].p;
+  b.nulls = r.null_cols ? nullp.data() : nullptr;
   b.clock = g.need_clock ? (const int64_t*)r.r_clk.p : nullptr;
   b.seq = g.need_seq ? (const int64_t*)r.r_seq.p : nullptr;
   (void)next_seq;
@@ -430,32 +459,37 @@ int stage_impl(shp_group& g, const shp_batch* slices) {
   }
   // 1a + 2: counts, slice lengths, largest ts of every rank
   for (int i = 0; i < g.nlocal; i++) split_count(g, g.L[i], slices[i]);
-  std::vector<int64_t> all((size_t)G * (G + 2));  // per rank: counts[G], n, maxts
+  constexpr int X = 3;  // per rank: counts[G], n, maxts, null-column mask
+  std::vector<int64_t> all((size_t)G * (G + X));
   if (g.rccl) {
     shp_group::Local& l = g.L[0];
     DevBuf mine, gath;
-    mine.ensure((G + 2) * 8);
-    gath.ensure((size_t)G * (G + 2) * 8);
+    mine.ensure((G + X) * 8);
+    gath.ensure((size_t)G * (G + X) * 8);
     std::vector<int64_t> v(l.send_cnt);
     v.push_back(l.n_slice);
     v.push_back(l.max_ts);
-    GH(hipMemcpyAsync(mine.p, v.data(), (G + 2) * 8, hipMemcpyHostToDevice, l.s));
-    GN(ncclAllGather(mine.p, gath.p, (size_t)(G + 2), ncclInt64, g.comm, l.s));
+    v.push_back((int64_t)l.null_mask);
+    GH(hipMemcpyAsync(mine.p, v.data(), (G + X) * 8, hipMemcpyHostToDevice, l.s));
+    GN(ncclAllGather(mine.p, gath.p, (size_t)(G + X), ncclInt64, g.comm, l.s));
     GH(hipMemcpyAsync(all.data(), gath.p, all.size() * 8, hipMemcpyDeviceToHost, l.s));
     GH(hipStreamSynchronize(l.s));
   } else {
     for (int i = 0; i < g.nlocal; i++) {
       shp_group::Local& l = g.L[i];
-      for (int d = 0; d < G; d++) all[(size_t)l.rank * (G + 2) + d] = l.send_cnt[d];
-      all[(size_t)l.rank * (G + 2) + G] = l.n_slice;
-      all[(size_t)l.rank * (G + 2) + G + 1] = l.max_ts;
+      for (int d = 0; d < G; d++) all[(size_t)l.rank * (G + X) + d] = l.send_cnt[d];
+      all[(size_t)l.rank * (G + X) + G] = l.n_slice;
+      all[(size_t)l.rank * (G + X) + G + 1] = l.max_ts;
+      all[(size_t)l.rank * (G + X) + G + 2] = (int64_t)l.null_mask;
     }
   }
-  auto cnt = [&](int s, int d) { return all[(size_t)s * (G + 2) + d]; };
+  auto cnt = [&](int s, int d) { return all[(size_t)s * (G + X) + d]; };
   std::vector<int64_t> base(G + 1, g.seq), seed(G + 1, g.clock);
+  uint32_t null_cols = 0;
   for (int r = 0; r < G; r++) {
-    base[r + 1] = base[r] + all[(size_t)r * (G + 2) + G];
-    seed[r + 1] = std::max(seed[r], all[(size_t)r * (G + 2) + G + 1]);
+    base[r + 1] = base[r] + all[(size_t)r * (G + X) + G];
+    seed[r + 1] = std::max(seed[r], all[(size_t)r * (G + X) + G + 1]);
+    null_cols |= (uint32_t)all[(size_t)r * (G + X) + G + 2];
   }
   // every rank's receive total from the all-gathered counts (identical on every rank): if any
   // rank would overflow, every rank fails here, before any exchange is posted (a rank that failed
@@ -480,9 +514,11 @@ int stage_impl(shp_group& g, const shp_batch* slices) {
                                           std::to_string(r.n_recv) + " events (> max_batch)");
     r.push_clock = seed[G];
     r.next_seq = base[G];
+    r.null_cols = null_cols;
   }
   // 1b: scatter
-  for (int i = 0; i < g.nlocal; i++) split_scatter(g, g.L[i], slices[i], seed[g.L[i].rank], base[g.L[i].rank]);
+  for (int i = 0; i < g.nlocal; i++)
+    split_scatter(g, g.L[i], slices[i], seed[g.L[i].rank], base[g.L[i].rank], null_cols);
   for (int i = 0; i < g.nlocal; i++) ensure_recv(g, g.L[i].slot[sl], g.L[i].slot[sl].n_recv);
   // 3: exchange
   if (g.rccl) {
@@ -534,6 +570,8 @@ int stage_impl(shp_group& g, const shp_batch* slices) {
     shp_group::Local::Slot& r = l.slot[sl];
     GH(hipSetDevice(l.dev));
     if (!g.has_stream_col) GH(hipMemsetAsync(r.r_stream.p, 0, (size_t)r.n_recv * 4, l.s));
+    for (int c = 0; c < g.ncol; c++)
+      if ((r.null_cols >> c) & 1u) GH(hipMemsetAsync((uint8_t*)r.r_null[c].p + r.n_recv, 0, 1, l.s));
     if (g.need_clock && r.push_clock != INT64_MIN)
       k_gs_fill_tail<<<1, 1, 0, l.s>>>((int64_t*)r.r_ts.p, (int32_t*)r.r_key.p, (int32_t*)r.r_stream.p,
                                        (int64_t*)r.r_clk.p, g.need_seq ? (int64_t*)r.r_seq.p : nullptr, r.n_recv,

@@ -82,6 +82,7 @@ constexpr int SWE_RANGE = 1 << 23;  // ts outside base +- 2^49 ms
 constexpr int SWE_AGGNULL = 1 << 24; // SHP_LAYOUT_AGG: a closing event's aggregated value is null
 constexpr int SWE_P32 = 1 << 25;     // SHP_LAYOUT_PAIRS32: e2 seq - e1 seq >= 2^32
 constexpr int SWE_LEAN = 1 << 26;    // k_sw_lean handed the push to k_sw_solve (not an error)
+constexpr int SWE_SPILL = 1 << 19;   // an owner's carry outgrew SWS_CCAP: it moves to k_sw_spill (re-run)
 constexpr int SWE_BOUND = 1 << 30;   // a match pair names an event outside the push (a broken
                                      // invariant: the expansion skips it and the push fails)
 
@@ -175,6 +176,24 @@ struct SweepDev {
   double* agg_c[2];
   int32_t* inv;          // nown * SW_LK
   unsigned long long* stamps;  // diagnostic build: nown * 8 phase cycle counts (else unused)
+  // spilled owners (sweep_spill.h): solved by k_sw_spill with their open candidates in HBM
+  int32_t spill_on;      // some owner is spilled: the LDS solves skip spilled owners
+  uint8_t* spilled[2];   // nown, double-buffered like the carry
+  int32_t* sp_n[2];      // nown: the owner's carry in the pool (-1: still in the c_* arrays)
+  int64_t* sp_base[2];   // nown: its segment of pool copy c
+  int64_t* p_ts[2];      // the pool, per copy: ts, seq, value, local key, null
+  int64_t* p_seq[2];
+  uint32_t* p_v[2];
+  uint8_t* p_lk[2];
+  uint8_t* p_null[2];
+  uint8_t* ovf;          // nown: k_sw_solve's carry overflowed for this owner in this push
+  int32_t* sp_active;    // owners still spilled after a push (k_sw_spill counts them)
+  int64_t* scr_base;     // nown: the owner's scratch segment for this push
+  uint32_t* s_idx;       // scratch: record positions grouped by key
+  int64_t* s_ts;         // scratch: per-key candidate lists
+  int64_t* s_seq;
+  uint32_t* s_v;
+  uint8_t* s_st;
 };
 
 // Predicate terms lowered for the sweep (host, SweepState::lower): with one 4-byte column, every
@@ -925,6 +944,7 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
   const uint64_t lt = sw_lanemask_lt();
   const int64_t rb = D.off[(int64_t)o * D.nst], re = D.off[(int64_t)(o + 1) * D.nst];
   const int rd = D.cur, wr = D.cur ^ 1;  // double-buffered per-owner state: read rd, write wr
+  if (D.spill_on && D.spilled[rd][o]) return;  // k_sw_spill solves this owner
   if (rb == re) {  // no events for this owner: its state passes through unchanged
     const int n0 = D.c_n[rd][o];
     for (int i = tid; i < n0; i += SWS_THREADS) {
@@ -1333,8 +1353,9 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
           pre++;
         }
       }
-      if (ntot > (uint32_t)SWS_CCAP) {
-        e |= E_LIST;
+      if (ntot > (uint32_t)SWS_CCAP) {  // the owner moves to k_sw_spill (the push re-runs)
+        e |= SWE_SPILL;
+        if (tid == 0) D.ovf[o] = 1;
         ntot = SWS_CCAP;
       }
       nc = (int)ntot;
@@ -1476,12 +1497,17 @@ __global__ void k_sw_init(SweepDev D) {
 }  // namespace shp
 
 #include "sweep_lean.h"
+#include "sweep_bal.h"
+#include "sweep_spill.h"
 
 // ------------------------------------------------------------------ host side
 namespace shp {
 
 struct SweepState {
   SweepDev D{};
+  int64_t pool_cap[2] = {0, 0};  // entries of each pool copy (spilled owners' carries)
+  int64_t scr_cap = 0;           // entries of the spill scratch
+  int64_t* sizes = nullptr;      // k_sw_spill_sizes output (3 x nown)
   int ct = 0;  // compare type of the probe loop (see SwCand)
   int lean_opc = 0;  // > 0: k_sw_lean applies to the query (its f2 comparison class)
   int64_t st_len = 65536;
@@ -1710,6 +1736,19 @@ struct SweepState {
       al(D.lastc[c], (int64_t)nown * SW_LK);
     }
     al(D.tsmax, 2);
+    for (int c = 0; c < 2; c++) {
+      al(D.spilled[c], nown);
+      al(D.sp_n[c], nown);
+      al(D.sp_base[c], nown);
+      if (hipMemsetAsync(D.spilled[c], 0, nown, s) != hipSuccess ||
+          hipMemsetAsync(D.sp_n[c], 0, (size_t)nown * 4, s) != hipSuccess)
+        throw std::runtime_error("sweep: spill state");
+    }
+    al(D.ovf, nown);
+    al(D.sp_active, 1);
+    al(D.scr_base, nown);
+    if (hipMemsetAsync(D.ovf, 0, nown, s) != hipSuccess) throw std::runtime_error("sweep: spill state");
+    D.spill_on = 0;
     D.cur = 0;
     (void)rocprim::exclusive_scan(nullptr, tmp_bytes, D.cnt, D.off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s);
     if (hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)) != hipSuccess)
@@ -1747,14 +1786,18 @@ struct SweepState {
   void commit() { D.cur ^= 1; }
 
   void release() {
-    void* ps[] = {(void*)D.lk8, D.inv, D.cnt, D.off, D.recs, D.tsmax, tmp};
+    void* ps[] = {(void*)D.lk8, D.inv, D.cnt, D.off, D.recs, D.tsmax, tmp, D.ovf, D.sp_active, D.scr_base,
+                  D.s_idx, D.s_ts, D.s_seq, D.s_v, D.s_st, sizes};
     for (void* p : ps)
       if (p) (void)hipFree(p);
     for (int c = 0; c < 2; c++) {
-      void* qs[] = {D.agg_s[c], D.agg_c[c], D.c_n[c], D.c_ts[c], D.c_seq[c], D.c_v[c], D.c_lk[c], D.c_null[c], D.lastc[c]};
+      void* qs[] = {D.agg_s[c], D.agg_c[c], D.c_n[c], D.c_ts[c], D.c_seq[c], D.c_v[c], D.c_lk[c], D.c_null[c], D.lastc[c],
+                    D.spilled[c], D.sp_n[c], D.sp_base[c], D.p_ts[c], D.p_seq[c], D.p_v[c], D.p_lk[c], D.p_null[c]};
       for (void* q : qs)
         if (q) (void)hipFree(q);
     }
+    pool_cap[0] = pool_cap[1] = scr_cap = 0;
+    sizes = nullptr;
     D = SweepDev{};
     tmp = nullptr;
   }
@@ -1788,6 +1831,18 @@ struct SweepState {
   bool lean_push_for(const BatchView& B) const { return lean_opc && !D.agg && !D.maybe_null && !B.nulls[0]; }
 
   void launch_lean(const BatchView& B, const MatchOut& O, int* err, hipStream_t s) {
+    static const int bal = getenv("SHP_SW_BAL") ? atoi(getenv("SHP_SW_BAL")) : 0;  // A/B: k_sw_bal
+    if (bal) {
+#define SB_CASE(c, p) \
+  case c * 8 + p: k_sw_bal<c, p><<<D.nown, SL_THREADS, 0, s>>>(D, B, O, err); break;
+      switch (ct * 8 + lean_opc) {
+        SB_CASE(1, 1) SB_CASE(1, 2) SB_CASE(1, 3) SB_CASE(1, 4) SB_CASE(1, 5) SB_CASE(1, 6)
+        SB_CASE(2, 1) SB_CASE(2, 2) SB_CASE(2, 3) SB_CASE(2, 4) SB_CASE(2, 5) SB_CASE(2, 6)
+        default: break;
+      }
+#undef SB_CASE
+      return;
+    }
 #define SL_CASE(c, p) \
   case c * 8 + p: k_sw_lean<c, p><<<D.nown, SL_THREADS, 0, s>>>(D, B, O, err); break;
     switch (ct * 8 + lean_opc) {
@@ -1813,6 +1868,136 @@ struct SweepState {
       default: break;
     }
     kt.mark(nullptr, s);
+  }
+
+  // ---- spilled owners (sweep_spill.h)
+  void ensure_pool(int c, int64_t n) {
+    if (n <= pool_cap[c]) return;
+    const int64_t cap = std::max<int64_t>(n, pool_cap[c] * 2);
+    int64_t *ts = nullptr, *seq = nullptr;
+    uint32_t* v = nullptr;
+    uint8_t *lk = nullptr, *nl = nullptr;
+    al(ts, cap);
+    al(seq, cap);
+    al(v, cap);
+    al(lk, cap);
+    al(nl, cap);
+    // keep what the copy holds (a committed copy may be grown too: restore)
+    if (pool_cap[c] > 0) {
+      const size_t m = (size_t)pool_cap[c];
+      if (hipMemcpy(ts, D.p_ts[c], m * 8, hipMemcpyDeviceToDevice) != hipSuccess ||
+          hipMemcpy(seq, D.p_seq[c], m * 8, hipMemcpyDeviceToDevice) != hipSuccess ||
+          hipMemcpy(v, D.p_v[c], m * 4, hipMemcpyDeviceToDevice) != hipSuccess ||
+          hipMemcpy(lk, D.p_lk[c], m, hipMemcpyDeviceToDevice) != hipSuccess ||
+          hipMemcpy(nl, D.p_null[c], m, hipMemcpyDeviceToDevice) != hipSuccess)
+        throw std::runtime_error("sweep: spill pool copy");
+    }
+    for (void* q : {(void*)D.p_ts[c], (void*)D.p_seq[c], (void*)D.p_v[c], (void*)D.p_lk[c], (void*)D.p_null[c]})
+      if (q) (void)hipFree(q);
+    D.p_ts[c] = ts;
+    D.p_seq[c] = seq;
+    D.p_v[c] = v;
+    D.p_lk[c] = lk;
+    D.p_null[c] = nl;
+    pool_cap[c] = cap;
+  }
+  void ensure_scratch(int64_t n) {
+    if (n <= scr_cap) return;
+    const int64_t cap = std::max<int64_t>(n, scr_cap * 2);
+    for (void* q : {(void*)D.s_idx, (void*)D.s_ts, (void*)D.s_seq, (void*)D.s_v, (void*)D.s_st})
+      if (q) (void)hipFree(q);
+    D.s_idx = nullptr;
+    D.s_ts = D.s_seq = nullptr;
+    D.s_v = nullptr;
+    D.s_st = nullptr;
+    al(D.s_idx, cap);
+    al(D.s_ts, cap);
+    al(D.s_seq, cap);
+    al(D.s_v, cap);
+    al(D.s_st, cap);
+    scr_cap = cap;
+  }
+  // restore: pool copy c with exactly n entries (contents follow from the snapshot)
+  void pool_exact(int c, int64_t n) {
+    if (n == pool_cap[c]) return;
+    for (void* q : {(void*)D.p_ts[c], (void*)D.p_seq[c], (void*)D.p_v[c], (void*)D.p_lk[c], (void*)D.p_null[c]})
+      if (q) (void)hipFree(q);
+    D.p_ts[c] = D.p_seq[c] = nullptr;
+    D.p_v[c] = nullptr;
+    D.p_lk[c] = D.p_null[c] = nullptr;
+    pool_cap[c] = 0;
+    if (n > 0) {
+      al(D.p_ts[c], n);
+      al(D.p_seq[c], n);
+      al(D.p_v[c], n);
+      al(D.p_lk[c], n);
+      al(D.p_null[c], n);
+      pool_cap[c] = n;
+    }
+  }
+  // owners spilled in the committed state (host read-back)
+  int64_t count_spilled() const {
+    std::vector<uint8_t> f((size_t)D.nown);
+    if (hipMemcpy(f.data(), D.spilled[D.cur], f.size(), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    int64_t n = 0;
+    for (uint8_t x : f) n += x ? 1 : 0;
+    return n;
+  }
+  // the push's overflowing owners become spilled in the committed state (the push then re-runs)
+  void mark_spilled(hipStream_t s) {
+    k_sw_mark_spilled<<<(unsigned)((D.nown + 255) / 256), 256, 0, s>>>(D);
+    D.spill_on = 1;
+  }
+  // k_sw_spill over the spilled owners of this push: size their scratch and pool segments on the
+  // host (one small read-back), then solve them
+  void spill(const BatchView& B, const MatchOut& O, int* err, hipStream_t s, KTimer& kt) {
+    if (!D.spill_on) return;
+    const int rd = D.cur, wr = D.cur ^ 1;
+    if (!sizes) al(sizes, (int64_t)D.nown * 3);
+    k_sw_spill_sizes<<<(unsigned)((D.nown + 255) / 256), 256, 0, s>>>(D, sizes);
+    std::vector<int64_t> h((size_t)D.nown * 3);
+    if (hipMemcpyAsync(h.data(), sizes, h.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      throw std::runtime_error("sweep: spill sizes");
+    std::vector<int64_t> scr((size_t)D.nown, 0), pb((size_t)D.nown, 0);
+    int64_t tot = 0;
+    for (int32_t o = 0; o < D.nown; o++) {
+      if (!h[3 * o]) continue;
+      scr[o] = pb[o] = tot;
+      tot += h[3 * o + 1] + h[3 * o + 2];  // records + carried: bounds the carry out too
+    }
+    ensure_scratch(tot + 1);
+    ensure_pool(wr, tot + 1);
+    if (hipMemcpyAsync(D.scr_base, scr.data(), scr.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(D.sp_base[wr], pb.data(), pb.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(D.sp_active, 0, 4, s) != hipSuccess)
+      throw std::runtime_error("sweep: spill sizes");
+    (void)rd;
+    kt.mark("sw_spill", s);
+    switch (D.f2.n * 3 + ct) {
+#define SP_CASE(b, c) \
+  case b * 3 + c: k_sw_spill<b, c><<<D.nown, SP_THREADS, 0, s>>>(D, B, O, err); break;
+      SP_CASE(0, 0) SP_CASE(0, 1) SP_CASE(0, 2) SP_CASE(1, 0) SP_CASE(1, 1) SP_CASE(1, 2)
+      SP_CASE(2, 0) SP_CASE(2, 1) SP_CASE(2, 2)
+#undef SP_CASE
+      default: break;
+    }
+    kt.mark(nullptr, s);
+  }
+  // after a committed push: are owners still spilled?  When none is, the spill state is cleared
+  // in both copies and the LDS solves stop checking it
+  void spill_settle(hipStream_t s) {
+    if (!D.spill_on) return;
+    int32_t act = 0;
+    if (hipMemcpyAsync(&act, D.sp_active, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      throw std::runtime_error("sweep: spill state");
+    if (act) return;
+    for (int c = 0; c < 2; c++)
+      if (hipMemsetAsync(D.spilled[c], 0, D.nown, s) != hipSuccess ||
+          hipMemsetAsync(D.sp_n[c], 0, (size_t)D.nown * 4, s) != hipSuccess)
+        throw std::runtime_error("sweep: spill state");
+    D.spill_on = 0;
   }
 
   void expand(const BatchView& B, const int32_t* key, const MatchOut& O, int* err, hipStream_t s, KTimer& kt,

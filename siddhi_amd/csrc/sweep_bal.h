@@ -1,102 +1,59 @@
-// siddhi-hip: k_sw_lean, the sweep solve for the common 2-state shape (included by sweep.h).
+// siddhi-hip: k_sw_bal, the balanced form of k_sw_lean (included by sweep.h after sweep_lean.h).
 //
-// Same semantics and output as k_sw_solve (StreamPreStateProcessor
-// .processAndReturn / expireEvents :326-403): per key, candidate i (e1's filter, evaluated by the
-// scatter) closes at the first later event j of the key with ts_j - ts_i <= W and f2(i, j), and
-// expires at the first later event beyond W; matches per key in (j, i) order.
-//
-// It covers the shape the headline configs use -- one f2 term `e2.v OP e1.v` or `e2.v OP const`
-// over a float or int column compared in its own type, no nulls, pair layouts -- and keeps every
-// quantity of the per-chunk work 32-bit.  Anything outside that (a push whose timestamps leave
-// base +- 2^30 ms, a key whose timestamps decrease, a carry beyond SL_CCAP, a closing event with
-// more than 255 far candidates) raises SWE_LEAN: the engine then re-runs the solve of the same
-// push with k_sw_solve, which is exact for all of them.  The two kernels share the per-owner
-// state in HBM (carry in key order, absolute ts), so either can continue from the other.
-//
-// Structure per chunk of SL_CHUNK records of the owner (512 threads, 3 block barriers):
-//   rank    stable ranks by local key (wave ballots, per-wave counters)          | barrier A
-//   scan    wave 0: key run offsets (carried first), write cursors, and the split
-//           of the sorted positions into 8 wave ranges aligned to key runs         | barrier B
-//   place   records and carried candidates at their sorted positions             | barrier C
-//   then every wave works alone on its range (whole key runs, so nothing crosses waves):
-//   probe   each candidate tests the next SW_P1 events of its key; unresolved ones go to the
-//           wave's worklist (SW_P2 events per round).  A closer records its distance in a
-//           32-bit word of the closing event: bits 0..23 = distance 1..24, bits 24..31 = count
-//           of farther ones.
-//   scan    per lane a contiguous block of positions: closes and still-open candidates, one
-//           wave scan, one LDS atomic for the wave's carry slots; open candidates are compacted
-//           (key order) as the next carry.  The last wave through reserves the chunk's output
-//           with one global atomic (per-wave global atomics were measured 2.7x slower: 400k
-//           same-address atomics per launch serialise).
-//   emit    between barriers A and B of the next chunk (the chunk's positions are intact until
-//           the next place step): a candidate's rank among its closer's candidates is the
-//           popcount of the nearer distance bits, so each match is written straight to its slot.
+// Same semantics, shape and hand-back rules as k_sw_lean (SURVEY.md Appendix A.7;
+// StreamPreStateProcessor.processAndReturn / expireEvents :326-403): per key, candidate i closes at
+// the first later event j of its key with ts_j - ts_i <= W and f2(i, j), expires at the first later
+// event beyond W; matches per key in (j, i) order.  What changes is how a chunk's work is split
+// over the 8 waves.  k_sw_lean gives each wave whole key runs, so with the ~20 keys an owner holds
+// at C2 a wave gets 2 or 3 runs and every barrier waits for the most loaded one.  Here every wave
+// takes exactly E / 8 sorted positions, wherever the key runs fall:
+//   rank    stable ranks by local key (wave ballots, per-wave counters)            | barrier A
+//   emit    the previous chunk's matches (its positions are intact until the place step)
+//   scan    one wave: key run offsets (carried first) and per-wave write cursors    | barrier B
+//   place   records and carried candidates at their sorted positions              | barrier C
+//   probe   each wave's E / 8 positions: a candidate tests the next SW_P1 events of its key, then
+//           the wave's worklist; a probe may read, and a closer may count into, positions of
+//           another wave (LDS atomics on the closing position's distance bits)     | barrier D
+//   offsets per lane a contiguous block of the wave's positions: closes and still-open
+//           candidates, a wave scan, the wave totals                              | barrier E
+//           then block offsets: each closing position's output offset (chunk-relative), and the
+//           open candidates compacted in position order -- which is key order -- as the next
+//           carry; one thread reserves the chunk's output with one global atomic.
+// The carry therefore stays in key order without a per-key gather, and the final write-back is a
+// straight copy.
 #pragma once
 
 namespace shp {
 
-constexpr int SL_THREADS = 512;
-constexpr int SL_WAVES = SL_THREADS / 64;
-constexpr int SL_R = 4;                       // records per thread per chunk
-constexpr int SL_CHUNK = SL_THREADS * SL_R;   // 2048
-constexpr int SL_CCAP = 384;                  // carried candidates per owner (<= SWS_CCAP)
-constexpr int SL_EMAX = SL_CHUNK + SL_CCAP;
-constexpr int SL_PAD = 16;                    // sentinel positions past E (probe reads)
-constexpr int SL_WL = 120;                    // worklist entries per wave (drained from SL_WLD on)
-constexpr int SL_WLD = 56;
-constexpr int SL_NEAR = 24;                   // closer distances kept as bits
-static_assert(SL_CCAP <= SWS_CCAP, "lean carry must fit the HBM carry arrays");
-
-struct SwLeanSmem {
+struct SwBalSmem {
   int2 tv[SL_EMAX + SL_PAD];         // (ts - chunk base, value) by sorted position; later x = output offset
-  uint32_t ref[SL_EMAX];             // batch index, or carry slot (carried)
+  uint32_t ref[SL_EMAX];             // batch index (e1's filter in bit 31), or carry slot (carried)
   uint32_t cl[SL_EMAX];              // closers of this position: distance bits | far count << 24
   uint32_t meta[SL_EMAX + SL_PAD];   // local key | key run end << 8 | first event of the run << 20
-                                     // (carried: position < first event; e1's filter: ref bit 31)
   int16_t m[SL_EMAX];                // >= 0 closing position, -1 expired, -2 open, -3 not a candidate
   uint16_t wc[SL_WAVES][256];        // per-wave rank counters, then write cursors
-  uint32_t binoff[257];              // key run starts (then, at the end, key-order carry offsets)
+  uint32_t binoff[257];              // key run starts
   uint16_t fe[256];                  // first event position of a key's run (after its carried)
-  uint32_t ncar[256];                // carried candidates of a key in the current carry buffer
+  uint16_t cst[256], cen[256];       // carry prefix at a key's run start / after its run end
   uint16_t ckf[2][256];              // index of a key's first entry in carry buffer 0/1
+  uint32_t ncar[256];                // carried candidates of a key in the current carry buffer
   uint8_t lastc[256];                // the key's latest event opened a candidate (SweepDev::lastc)
+  uint8_t run[256];                  // the key has a run in the chunk being finished
   int64_t cts[2][SL_CCAP];           // carry: ts - batch base (exact)
   int64_t cseq[2][SL_CCAP];
   uint32_t cv[2][SL_CCAP];
   uint8_t clk[2][SL_CCAP];
   uint32_t wl[SL_WAVES][SL_WL];      // worklists: position | next probe position << 16
-  int32_t ps[SL_WAVES + 1];          // wave ranges of sorted positions
+  uint32_t wt[SL_WAVES];             // per wave: closes << 16 | opens
   int32_t cn[2];                     // entries in carry buffer 0/1
-  uint32_t wtot[SL_WAVES];
-  uint32_t wt[SL_WAVES], wb[SL_WAVES];  // matches per wave in the chunk, and their offsets
-  unsigned long long gbase;           // the chunk's output range (one global atomic per chunk)
-  int32_t done;                       // waves through the chunk's reservation step
-  int32_t scanner[2];                 // the wave that runs the scan step of even / odd chunks
+  unsigned long long gbase;          // the chunk's output range (one global atomic per chunk)
   int32_t flag;
 };
 
-template <int CT, int OPC, int P>
-__device__ __forceinline__ int sl_probe(const int2* tv, int qb, int end, int32_t a_ts, int32_t W,
-                                        typename SwTy<CT>::T b) {
-  int2 x[P];
-#pragma unroll
-  for (int d = 0; d < P; d++) x[d] = tv[qb + d];
-  int res = -4;
-#pragma unroll
-  for (int d = 0; d < P; d++) {
-    const bool hit = sw_cmp_op<OPC>(0, sw_val<CT>((uint32_t)x[d].y, 0.0, 0.0, false), b);
-    const int r = qb + d >= end ? -2 : (x[d].x - a_ts > W ? -1 : (hit ? qb + d : -4));
-    res = res == -4 ? r : res;
-  }
-  return res;
-}
-
-__device__ __forceinline__ uint32_t sl_closes(uint32_t c) { return (uint32_t)__popc(c & 0xFFFFFFu) + (c >> 24); }
-
 template <int CT, int OPC>
-__global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView B, MatchOut O, int* err) {
+__global__ __launch_bounds__(SL_THREADS, 4) void k_sw_bal(SweepDev D, BatchView B, MatchOut O, int* err) {
   using T = typename SwTy<CT>::T;
-  __shared__ SwLeanSmem S;
+  __shared__ SwBalSmem S;
   const int o = blockIdx.x;
   const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
   const uint64_t lt = sw_lanemask_lt();
@@ -121,19 +78,17 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     return;
   }
   const int nc0 = D.c_n[rd][o];
-  // the scatter saw a ts beyond base +- 2^30 (batch-relative ts are 32-bit here), or the carry
-  // is larger than the lean kernel holds
-  if (D.tsmax[1] != 0 || nc0 > SL_CCAP) {
+  if (D.tsmax[1] != 0 || nc0 > SL_CCAP) {  // a ts beyond base +- 2^30, or a carry larger than held here
     if (tid == 0) atomicOr(err, SWE_LEAN);
     return;
   }
   const int64_t base = B.ts[0];
-  const int32_t W = (int32_t)D.within;  // <= SW_TS_SPAN (SweepState::shape_ok)
+  const int32_t W = (int32_t)D.within;
   const SwTerm t2 = D.f2.t[0];
   const bool bconst = t2.bk == 0;
   const T bc = (T)t2.bc;
   const int lkbits = D.lk_bits;
-  const int nb = lkbits >= 8 ? SW_LK : (1 << lkbits);  // local keys 0..nb-1
+  const int nb = lkbits >= 8 ? SW_LK : (1 << lkbits);
   int e = 0;
   for (int i = tid; i < 256; i += SL_THREADS) {
     S.ncar[i] = 0;
@@ -143,13 +98,11 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   for (int i = tid; i < SL_WAVES * 256; i += SL_THREADS) (&S.wc[0][0])[i] = 0;
   if (tid == 0) {
     S.flag = 0;
-    S.done = 0;
-    S.scanner[0] = S.scanner[1] = 0;
     S.cn[0] = nc0;
     S.cn[1] = 0;
   }
   __syncthreads();
-  // carry from the previous push (key order): counts and first index per key
+  // carry from the previous push (key order, as both solves write it): counts and first index per key
   for (int x = tid; x < nc0; x += SL_THREADS) {
     const int64_t c = (int64_t)o * SWS_CCAP + x;
     const uint32_t lk = D.c_lk[rd][c];
@@ -168,11 +121,10 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     if (rb + jj < re) pf[s] = D.recs[rb + jj];
   }
   uint64_t tbk = D.recs[rb].kt;
-  // 6. emit (a chunk's matches are written between barriers A and B of the next chunk, once the
-  //    last wave through the chunk has reserved its output range with one global atomic):
-  //    slot = offset(q) + (closes(q) - 1 - later), later = closers of q nearer than p
+  // emit a finished chunk's matches (this wave's positions of it): slot = offset(q) + (closes(q)
+  // - 1 - later), later = closers of q nearer than p
   auto emit = [&](int PS, int PE, int pc) {
-    const unsigned long long gb = S.gbase + S.wb[w];
+    const unsigned long long gb = S.gbase;
     for (int g = PS; g < PE; g += 64) {
       const int p = g + (int)lane;
       if (p >= PE) continue;
@@ -204,27 +156,12 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       }
     }
   };
-  int pPS = 0, pPE = 0, pcur = 0;  // this wave's range of the previous chunk, and its carry buffer
-#ifdef SHP_SW_STAMPS  // diagnostic build: wave cycles per phase (barrier waits count in the phase before)
-  unsigned long long stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t stp = clock64();
-#define SL_STAMP(k)                 \
-  do {                              \
-    const uint64_t t_ = clock64();  \
-    stc[k] += t_ - stp;             \
-    stp = t_;                       \
-  } while (0)
-#else
-#define SL_STAMP(k) \
-  do {              \
-  } while (0)
-#endif
+  int pPS = 0, pPE = 0, pcur = 0;
   __syncthreads();
-  int ci = 0;  // chunk counter (the scanner of a chunk is chosen by the one before)
-  for (int64_t cb = rb; cb < re; cb += SL_CHUNK, ci++) {
+  for (int64_t cb = rb; cb < re; cb += SL_CHUNK) {
     const int nchunk = (int)min((int64_t)SL_CHUNK, re - cb);
     const int nx = cur ^ 1;
-    const int32_t tb32 = (int32_t)(uint32_t)tbk;  // chunk base, batch-relative (|.| < 2^30)
+    const int32_t tb32 = (int32_t)(uint32_t)tbk;
     // 1. rank by local key (stable: wave-major, then slot, then lane = arrival order)
     uint32_t rk[SL_R], bin[SL_R];
 #pragma unroll
@@ -242,20 +179,12 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       }
     }
     __syncthreads();  // A
-    SL_STAMP(0);
-    // flags raised by the previous chunk are read here, where no thread writes S.flag (all
-    // threads take the same branch)
     if (S.flag) break;
     if (cb != rb) emit(pPS, pPE, pcur);  // the previous chunk's matches
-    SL_STAMP(1);
     const int E = S.cn[cur] + nchunk;
-    // 2. key run offsets and the wave split (one wave: the one with the least to emit, the
-    //    previous chunk's scanner picked it from that chunk's split)
-    if ((int)w == S.scanner[ci & 1]) {
+    // 2. key run offsets and write cursors (wave 0); the previous chunk's per-key carry counts
+    if (w == 0) {
       uint32_t run = 0;
-      int32_t psv[SL_WAVES];
-#pragma unroll
-      for (int k = 0; k < SL_WAVES; k++) psv[k] = -1;
       for (int b0 = 0; b0 < nb; b0 += 64) {
         const int b = b0 + (int)lane;
         const bool v = b < nb;
@@ -265,7 +194,17 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
           c[ww] = v ? S.wc[ww][b] : 0u;
           t += c[ww];
         }
-        const uint32_t nk = v ? S.ncar[b] : 0u;
+        uint32_t nk = 0;
+        if (v) {
+          if (cb != rb) {  // the carry the previous chunk left: [cst, cen) of keys that had a run
+            const bool had = S.run[b] != 0;
+            nk = had ? (uint32_t)(S.cen[b] - S.cst[b]) : 0u;
+            S.ckf[cur][b] = had ? S.cst[b] : (uint16_t)0;
+            S.ncar[b] = nk;
+          } else {
+            nk = S.ncar[b];
+          }
+        }
         t += nk;
         uint32_t x = t;
 #pragma unroll
@@ -277,6 +216,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         if (v) {
           S.binoff[b] = pre;
           S.fe[b] = (uint16_t)(pre + nk);
+          S.run[b] = t ? 1 : 0;
           uint32_t g = pre + nk;
 #pragma unroll
           for (int ww = 0; ww < SL_WAVES; ww++) {
@@ -284,42 +224,11 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
             g += c[ww];
           }
         }
-        // wave k starts at the first key run that starts at or after k * E / 8
-#pragma unroll
-        for (int k = 1; k < SL_WAVES; k++) {
-          const uint64_t mk = __ballot(v && (int64_t)pre * SL_WAVES >= (int64_t)k * E);
-          if (mk && psv[k] < 0) psv[k] = __builtin_amdgcn_readlane((int)pre, __ffsll((unsigned long long)mk) - 1);
-        }
         run += __shfl(x, 63, 64);
       }
-      if (lane == 0) {
-        S.binoff[nb] = run;  // = E
-        S.ps[0] = 0;
-        S.ps[SL_WAVES] = E;
-      }
-      if (lane > 0 && lane < (uint32_t)SL_WAVES) {
-        int32_t pv = -1;
-#pragma unroll
-        for (int k = 1; k < SL_WAVES; k++) pv = (uint32_t)k == lane ? psv[k] : pv;
-        S.ps[lane] = pv < 0 ? E : pv;
-      }
-      if (lane == 0) {  // the next chunk's scanner: the wave with the smallest range of this chunk
-        int best = 0, bl = 1 << 30, prev = 0;
-#pragma unroll
-        for (int k = 0; k < SL_WAVES; k++) {
-          const int nxt = k + 1 < SL_WAVES ? (psv[k + 1] < 0 ? E : psv[k + 1]) : E;
-          const int len = nxt - prev;
-          if (len < bl) {
-            bl = len;
-            best = k;
-          }
-          prev = nxt;
-        }
-        S.scanner[(ci + 1) & 1] = best;
-      }
+      if (lane == 0) S.binoff[nb] = run;  // = E
     }
     __syncthreads();  // B
-    SL_STAMP(2);
     // 3. place records and carried candidates at their sorted positions
 #pragma unroll
     for (int s = 0; s < SL_R; s++) {
@@ -337,7 +246,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         const uint32_t lk = S.clk[cur][x];
         const uint32_t p = S.binoff[lk] + (uint32_t)x - S.ckf[cur][lk];
         const int64_t r = S.cts[cur][x] - (int64_t)tb32;
-        if (r > SW_TS_SPAN) S.flag = 1;  // later than the chunk's span: the exact kernel
+        if (r > SW_TS_SPAN) S.flag = 1;
         const int32_t crel = r < (int64_t)SW_TS_FLOOR ? SW_TS_FLOOR : (int32_t)r;
         S.tv[p] = make_int2(crel, (int32_t)S.cv[cur][x]);
         S.meta[p] = lk | (S.binoff[lk + 1] << 8) | ((uint32_t)S.fe[lk] << 20);
@@ -348,7 +257,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       S.tv[E + tid] = make_int2(0, 0);
       S.meta[E + tid] = SW_LKF_NONE;
     }
-    if (tid == 0) S.cn[nx] = 0;
+    for (int p = tid; p < E; p += SL_THREADS) S.cl[p] = 0;
     {  // prefetch the next chunk while this one is solved
       const int64_t nbk = cb + SL_CHUNK;
 #pragma unroll
@@ -359,11 +268,9 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       if (nbk < re) tbk = D.recs[nbk].kt;
     }
     __syncthreads();  // C
-    SL_STAMP(3);
-    // ---- from here each wave works alone on its key runs [PS, PE)
-    const int PS = S.ps[w], PE = S.ps[w + 1];
+    // ---- balanced: wave w takes sorted positions [PS, PE), E / 8 of them, across key runs
+    const int PS = (int)(((int64_t)E * w) >> 3), PE = (int)(((int64_t)E * (w + 1)) >> 3);
     for (int b = (int)lane; b < nb; b += 64) S.wc[w][b] = 0;  // this wave's counters, next chunk
-    for (int p = PS + (int)lane; p < PE; p += 64) S.cl[p] = 0;
     auto record = [&](int p, int res) {
       S.m[p] = (int16_t)res;
       if (res >= 0) {
@@ -377,7 +284,6 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       }
     };
     uint32_t* wl = S.wl[w];
-    // 4. probe: round 1 per position, unresolved candidates to the worklist, drained 8 events a round
     auto drain = [&](uint32_t nwl) -> uint32_t {
       uint32_t nn = 0;
       for (uint32_t b0 = 0; b0 < nwl; b0 += 64) {
@@ -403,14 +309,13 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       }
       return nn;
     };
+    // 4. probe
     uint32_t nwl = 0;
     for (int g = PS; g < PE; g += 64) {
       const int p = g + (int)lane;
       int res = -3;
       uint32_t qn = 0;
       if (p < PE) {
-        // all of a position's facts in independent loads: its meta word (key, run end, first
-        // event), its (ts, value), its ref (e1's filter in bit 31) and the previous position's
         const uint32_t mt = S.meta[p];
         const int2 a = S.tv[p];
         const bool f1 = (S.ref[p] >> 31) != 0;
@@ -418,11 +323,10 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         const int tprev = p > 0 ? S.tv[p - 1].x : 0;
         const uint32_t lk = mt & 0xFFu;
         const int end = (int)((mt >> 8) & 0xFFFu), fe = (int)(mt >> 20);
-        const bool first = (mprev & 0xFFu) != lk;  // the key run starts here
-        if (first) S.ncar[lk] = 0;  // recounted by the carry step below
+        const bool first = (mprev & 0xFFu) != lk;
         if (p == end - 1 && p >= fe) S.lastc[lk] = f1 ? 1 : 0;
         if (!first && tprev > a.x) S.flag = 1;  // ts decrease within the key: exact kernel
-        if (p < fe || f1) {  // carried, or e1's filter
+        if (p < fe || f1) {
           const T bv = bconst ? bc : sw_val<CT>((uint32_t)a.y, 0.0, 0.0, false);
           const int q0 = max(p + 1, fe);
           res = sl_probe<CT, OPC, SW_P1>(S.tv, q0, end, a.x, W, bv);
@@ -438,9 +342,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       if (nwl >= SL_WLD) nwl = drain(nwl);
     }
     while (nwl > 0) nwl = drain(nwl);
-    SL_STAMP(4);
-    // 5. closes and open candidates per position (contiguous block per lane), output range and
-    //    carry slots; open candidates compacted in key order; tv.x becomes the output offset
+    __syncthreads();  // D: every closer has been counted
+    // 5. closes and open candidates per position (contiguous block per lane)
     const int nw = PE - PS;
     const int K = (nw + 63) >> 6;
     const int lb = PS + (int)lane * K, le = min(lb + K, PE);
@@ -456,36 +359,34 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       const uint32_t y = __shfl_up(incl, d, 64);
       if (lane >= (uint32_t)d) incl += y;
     }
-    const uint32_t tot = __shfl(incl, 63, 64);
-    const uint32_t ctot = tot >> 16, otot = tot & 0xFFFFu;
-    int cbase = 0;
-    if (lane == 0) {
-      cbase = otot ? atomicAdd(&S.cn[nx], (int)otot) : 0;
-      S.wt[w] = ctot;
-      // the last wave through reserves the chunk's output (LDS keeps each wave's operations in
-      // order, so it sees every other wave's count)
-      if (atomicAdd(&S.done, 1) == SL_WAVES - 1) {
-        uint32_t t = 0;
-        for (int ww = 0; ww < SL_WAVES; ww++) {
-          S.wb[ww] = t;
-          t += S.wt[ww];
-        }
-        const unsigned long long g0 = t ? atomicAdd(O.count, (unsigned long long)t) : 0ull;
-        if (g0 + t > (unsigned long long)O.cap) e |= E_OUT;
-        S.gbase = g0;
-        S.done = 0;
-      }
+    if (lane == 63) S.wt[w] = incl;
+    __syncthreads();  // E
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < SL_WAVES; ww++) {
+      const uint32_t t = S.wt[ww];
+      wbase += (uint32_t)ww < w ? t : 0u;
+      tot += t;
     }
-    cbase = __shfl(cbase, 0, 64);
-    if (cbase + (int)otot > SL_CCAP) S.flag = 1;
+    const uint32_t ctot = tot >> 16, otot = tot & 0xFFFFu;
+    if (otot > (uint32_t)SL_CCAP) S.flag = 1;
+    if (tid == 0) {
+      const unsigned long long g0 = ctot ? atomicAdd(O.count, (unsigned long long)ctot) : 0ull;
+      if (g0 + ctot > (unsigned long long)O.cap) e |= E_OUT;
+      S.gbase = g0;
+      S.cn[nx] = (int32_t)min(otot, (uint32_t)SL_CCAP);
+    }
     {
-      uint32_t co = (incl - pk) >> 16, oo = (incl - pk) & 0xFFFFu;
+      const uint32_t ex = wbase + incl - pk;
+      uint32_t co = ex >> 16, oo = ex & 0xFFFFu;
       for (int q = lb; q < le; q++) {
         const uint32_t c = sl_closes(S.cl[q]);
+        const uint32_t f = S.meta[q];
+        const uint32_t lk = f & 0xFFu;
+        if (q == 0 || (S.meta[q - 1] & 0xFFu) != lk) S.cst[lk] = (uint16_t)oo;  // the key's run starts here
         if (S.m[q] == -2) {
-          const int x = cbase + (int)oo;
+          const int x = (int)oo;
           if (x < SL_CCAP) {
-            const uint32_t f = S.meta[q];
             const uint32_t r = S.ref[q] & 0x7FFFFFFFu;
             if (q < (int)(f >> 20)) {  // carried
               S.cts[nx][x] = S.cts[cur][r];
@@ -497,30 +398,19 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
               S.cv[nx][x] = (uint32_t)a.y;
               S.cseq[nx][x] = bseq(B, r);
             }
-            S.clk[nx][x] = (uint8_t)(f & 0xFFu);
+            S.clk[nx][x] = (uint8_t)lk;
           }
           oo++;
         }
+        if (q + 1 == (int)((f >> 8) & 0xFFFu)) S.cen[lk] = (uint16_t)oo;  // the key's run ends here
         S.tv[q].x = (int32_t)co;
         co += c;
-      }
-    }
-    {  // per-key first index and count of the new carry entries
-      const int xe = min(cbase + (int)otot, SL_CCAP);
-      for (int x = cbase + (int)lane; x < xe; x += 64) {
-        const uint32_t lk = S.clk[nx][x];
-        if (x == cbase || S.clk[nx][x - 1] != lk) S.ckf[nx][lk] = (uint16_t)x;
-      }
-      for (int x = cbase + (int)lane; x < xe; x += 64) {
-        const uint32_t lk = S.clk[nx][x];
-        if (x + 1 == xe || S.clk[nx][x + 1] != lk) S.ncar[lk] = (uint32_t)(x + 1 - S.ckf[nx][lk]);
       }
     }
     pPS = PS;
     pPE = PE;
     pcur = cur;
     cur = nx;
-    SL_STAMP(5);
   }
   __syncthreads();
   if (S.flag) {
@@ -528,34 +418,14 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     return;
   }
   emit(pPS, pPE, pcur);  // the last chunk's matches
-#ifdef SHP_SW_STAMPS
-  SL_STAMP(1);
-  {
-    __shared__ unsigned long long sts[8];
-    if (tid < 8) sts[tid] = 0;
-    __syncthreads();
-    if (lane == 0)
-      for (int k = 0; k < 8; k++) atomicAdd(&sts[k], stc[k]);
-    __syncthreads();
-    if (tid < 8 && D.stamps) D.stamps[(int64_t)o * 8 + tid] = sts[tid];
-  }
-#endif
-  // write back the carry in key order (k_sw_solve's layout) and the per-key flags (copy wr)
-  {
-    uint32_t total;
-    const uint32_t v = tid < (uint32_t)nb ? S.ncar[tid] : 0u;
-    const uint32_t pre = sw_block_scan_n<SL_WAVES>(v, S.wtot, total);
-    if (tid < (uint32_t)nb) S.binoff[tid] = pre;
-  }
-  __syncthreads();
+  // write back the carry: already in key order (position order)
   const int ncf = S.cn[cur];
   for (int x = tid; x < ncf; x += SL_THREADS) {
-    const uint32_t lk = S.clk[cur][x];
-    const int64_t c = (int64_t)o * SWS_CCAP + S.binoff[lk] + (uint32_t)x - S.ckf[cur][lk];
+    const int64_t c = (int64_t)o * SWS_CCAP + x;
     D.c_ts[wr][c] = base + S.cts[cur][x];
     D.c_seq[wr][c] = S.cseq[cur][x];
     D.c_v[wr][c] = S.cv[cur][x];
-    D.c_lk[wr][c] = (uint8_t)lk;
+    D.c_lk[wr][c] = S.clk[cur][x];
     D.c_null[wr][c] = 0;
   }
   for (int i = tid; i < SW_LK; i += SL_THREADS) D.lastc[wr][(int64_t)o * SW_LK + i] = S.lastc[i];

@@ -405,13 +405,21 @@ class HipGroup:
             raise ShpError(rc, lib().shp_group_last_error(self.h).decode())
 
     def _batches(self, slices):
+        """slices: per local rank (ts, key, stream-or-None, [cols]) or (..., [cols], [nulls-or-None])."""
         arr = (ShpBatch * self.nlocal)()
         keep = []
-        for i, (ts, key, stream, cols) in enumerate(slices):
+        for i, sl in enumerate(slices):
+            ts, key, stream, cols = sl[:4]
+            nulls = sl[4] if len(sl) > 4 else None
             colp = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
             keep.append(colp)
+            nulp = None
+            if nulls is not None:
+                nulp = (ctypes.c_void_p * max(1, len(cols)))(*[0 if m is None else m.data_ptr() for m in nulls])
+                keep.append(nulp)
             arr[i] = ShpBatch(ts.numel(), ts.data_ptr(), key.data_ptr(), None if stream is None else stream.data_ptr(),
-                              ctypes.cast(colp, ctypes.c_void_p), None)
+                              ctypes.cast(colp, ctypes.c_void_p),
+                              None if nulp is None else ctypes.cast(nulp, ctypes.c_void_p))
         return arr, keep
 
     def push_device(self, slices):

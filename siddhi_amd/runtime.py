@@ -210,10 +210,8 @@ class SiddhiAppRuntime:
             ts[j] = t
             stream[j] = s
             sname = stream_names[s]
-            if sname not in qr.streams:  # clock-only (playback): no key, no values
-                stream[j] = -1
-                for c in range(len(cols)):
-                    nulls[c][j] = 1
+            if sname not in qr.streams:  # clock-only (playback): no key, no values (the kernels never
+                stream[j] = -1          # read a stream -1 row's values, so its null flags stay 0)
                 continue
             if pk is not None:
                 attr = pk[sname]

@@ -142,3 +142,37 @@ def test_group_member_rccl_one_rank(q, keys):
         want, got = _drop_pos(want), _drop_pos(got)
     assert compare(want, got) is None, compare(want, got)
     assert sum(len(v) for v in want.values()) > 1000
+
+
+def test_group_null_values_travel_with_their_events():
+    """Null values on the sharded path: each rank's slice may carry null bytes for a column (here
+    only the odd ranks' slices do); the group exchanges them with the events, so a null price
+    compares as null (CompareConditionExpressionExecutor: a null operand is false) exactly as in
+    one engine."""
+    import torch
+    from siddhi_amd.native import LAYOUT_FULL, HipGroup
+    cq = program_for(2)
+    keys, world = 600, 3
+    g = small_stream(2, 90_000, keys)
+    rng = np.random.default_rng(4)
+    nul = (rng.random(len(g["ts"])) < 0.2).astype(np.uint8)
+    bounds = [r * len(nul) // world for r in range(world + 1)]
+    for r in range(0, world, 2):  # even ranks' slices carry no null array
+        nul[bounds[r]:bounds[r + 1]] = 0
+    cols = columns_for(cq, g)
+    ora = OracleEngine(cq.program_json(), 0)
+    ora.push(g["ts"], g["key"], g["stream"], cols, [nul])
+    want = per_key(ora.fetch())
+    grp = HipGroup(cq.program_json(), 0, max_keys=keys, max_batch=1 << 17, max_matches=1 << 17,
+                   devices=[0] * world, match_layout=LAYOUT_FULL)
+    sl = []
+    for r in range(world):
+        a, b = bounds[r], bounds[r + 1]
+        t = lambda x: torch.from_numpy(np.ascontiguousarray(x[a:b])).to("cuda:0")  # noqa: E731
+        sl.append((t(g["ts"]), t(g["key"]), None, [t(c) for c in cols], [t(nul)] if r % 2 else None))
+    grp.push_device(sl)
+    got = per_key(grp.fetch())
+    torch.cuda.synchronize()
+    grp.close()
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(v) for v in want.values()) > 5_000
