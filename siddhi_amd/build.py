@@ -16,9 +16,14 @@ LIB = os.path.join(HERE, "libsiddhi_hip.so")
 SRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build_obj")
 HEADERS = ["nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h", "sweep.h", "sweep_lean.h", "sweep_bal.h",
-           "cseq.h", "labs.h"]
-UNITS = ["engine.hip", "synth.hip", "shard.hip", "group.hip", "siddhiql.cpp"]
-DEPS = HEADERS + UNITS
+           "sweep_spill.h", "cseq.h", "labs.h"]
+# (object name, source, extra flags): the kernel families are split over units that build in
+# parallel (sweep_solve.hip once per e1 term count), heaviest first
+UNITS = [("sweep_solve0", "sweep_solve.hip", ["-DSW_NT1=0"]), ("sweep_solve1", "sweep_solve.hip", ["-DSW_NT1=1"]),
+         ("sweep_solve2", "sweep_solve.hip", ["-DSW_NT1=2"]), ("lanes", "lanes.hip", []),
+         ("sweep_lean", "sweep_lean.hip", []), ("engine", "engine.hip", []), ("group", "group.hip", []),
+         ("siddhiql", "siddhiql.cpp", []), ("shard", "shard.hip", []), ("synth", "synth.hip", [])]
+DEPS = HEADERS + sorted({u[1] for u in UNITS})
 
 
 def _hdr_time() -> float:
@@ -50,18 +55,19 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
     os.makedirs(odir, exist_ok=True)
     ht = _hdr_time()
 
-    def obj(u: str) -> str:
-        src = os.path.join(SRC, u)
-        o = os.path.join(odir, u + ".o")
+    def obj(u) -> str:
+        name, file, extra = u
+        src = os.path.join(SRC, file)
+        o = os.path.join(odir, name + ".o")
         if force or not os.path.exists(o) or os.path.getmtime(o) < max(ht, os.path.getmtime(src)):
-            cmd = [hipcc] + flags + ["-c", "-o", o + ".tmp", src]
+            cmd = [hipcc] + flags + extra + ["-c", "-o", o + ".tmp", src]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             subprocess.check_call(cmd)
             os.replace(o + ".tmp", o)
         return o
 
-    with ThreadPoolExecutor(max_workers=len(UNITS)) as ex:
+    with ThreadPoolExecutor(max_workers=min(len(UNITS), os.cpu_count() or 8, 16)) as ex:
         objs = list(ex.map(obj, UNITS))
     cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-lrccl"]
     if verbose:

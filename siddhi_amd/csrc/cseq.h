@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void k_cseq(CseqDev C, BatchView B, MatchOut O
   if (e) atomicOr(err, e);
 }
 
-__global__ void k_cseq_init(CseqDev C) {
+static __global__ void k_cseq_init(CseqDev C) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int c = 0; c < 2; c++) {
     if (i < C.nk) {

@@ -138,75 +138,6 @@ __global__ void k_clamp_clock(int64_t* rmax, int64_t n, int64_t clock0) {
     if (rmax[i] < clock0) rmax[i] = clock0;
 }
 
-// SHP_LANES_WPE: waves per EU requested from the compiler for the lane kernels (diagnostic A/B:
-// fewer VGPRs and more waves to hide the lanes' dependent memory latency, against more spills)
-#ifdef SHP_LANES_WPE
-#define SHP_LANES_ATTR __attribute__((amdgpu_waves_per_eu(SHP_LANES_WPE, SHP_LANES_WPE)))
-#else
-#define SHP_LANES_ATTR
-#endif
-
-template <int T>
-__global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes(const DevProg* __restrict__ Pp, LaneLayout Y, char* arena,
-                                                  BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
-                                                  const uint32_t* __restrict__ kbeg,
-                                                  const uint32_t* __restrict__ kcnt, int32_t nlanes, int* err) {
-  int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-#ifdef SHP_LANES_PLDS  // A/B: the program in LDS (the lanes' field reads at LDS latency)
-  __shared__ DevProg sP;
-  for (int i = threadIdx.x; i < (int)(sizeof(DevProg) / 4); i += blockDim.x)
-    ((uint32_t*)&sP)[i] = ((const uint32_t*)Pp)[i];
-  __syncthreads();
-  if (k >= nlanes) return;
-  const DevProg& P = sP;
-#else
-  if (k >= nlanes) return;
-  const DevProg& P = *Pp;
-#endif
-  LaneT<1, T> ln(P, Y, arena, k, k, B, O);
-  if (!B.partitioned && !ln.template at<uint8_t>(Y.o_kinit, 0)) {
-    ln.clock = B.init_clock;
-    ln.emit_pos = B.seq0;
-    ln.init_partition();
-  }
-  int64_t lo = 0;
-  uint32_t b = kbeg[k], e = b + kcnt[k];
-  for (uint32_t p = b; p < e && !ln.err; p++) {
-    int64_t g = perm[p];
-    ln.maybe_gc();
-    ln.timers(lo, g);
-    ln.on_event(g);
-    lo = g + 1;
-  }
-  if (!ln.err) {
-    ln.maybe_gc();
-    ln.timers(lo, B.n - 1);
-  }
-  ln.flush_ret();
-  if (ln.err) {
-    ln.template at<int32_t>(Y.o_err, 0) |= ln.err;
-    atomicOr(err, ln.err);
-  }
-}
-
-// copy one lane's state between two arena layouts (element i of lane l at field[i * L + l])
-__device__ inline void lane_copy(const LaneLayout& Yd, char* dst, int64_t ld, const LaneLayout& Ys, const char* src,
-                                 int64_t ls) {
-  for (int f = 0; f < Ys.nf; f++) {
-    const int sz = Ys.f_sz[f];
-    for (int i = 0; i < Ys.f_elems[f]; i++) {
-      char* d = dst + Yd.f_off[f] + ((int64_t)i * Yd.L + ld) * sz;
-      const char* s = src + Ys.f_off[f] + ((int64_t)i * Ys.L + ls) * sz;
-      switch (sz) {
-        case 8: *(uint64_t*)d = *(const uint64_t*)s; break;
-        case 4: *(uint32_t*)d = *(const uint32_t*)s; break;
-        case 2: *(uint16_t*)d = *(const uint16_t*)s; break;
-        default: *d = *s; break;
-      }
-    }
-  }
-}
-
 // Capacity growth: the committed arena of layout Ys (tier t) into layout Yd (tier >= t), every
 // lane.  Fields keep their order and element sizes across tiers; element indices that embed a
 // capacity are re-indexed: list items ((which * MAXP + p) * LCAP + i) and the timer rings
@@ -240,46 +171,14 @@ __global__ __launch_bounds__(256) void k_lane_migrate(LaneLayout Yd, char* dst, 
   }
 }
 
-// Few keys: the lanes' state lives in LDS for the batch (copied in and out of the HBM arena),
-// so the per-event chain of dependent state accesses runs at LDS latency instead of HBM
-// latency.  Same Lane code, one lane per thread, blockDim lanes per workgroup.
-__global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes_lds(const DevProg* __restrict__ Pp, LaneLayout Y,
-                                const char* arena, char* arena_out, LaneLayout Yl,
-                                BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
-                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt, int32_t nlanes,
-                                int* err) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int32_t t = threadIdx.x;
-  const int32_t k = blockIdx.x * blockDim.x + t;
-  if (k >= nlanes) return;
-  lane_copy(Yl, lds, t, Y, (char*)arena, k);
-  const DevProg& P = *Pp;
-  LaneT<3> ln(P, Yl, lds, t, k, B, O);
-  if (!B.partitioned && !ln.at<uint8_t>(Yl.o_kinit, 0)) {
-    ln.clock = B.init_clock;
-    ln.emit_pos = B.seq0;
-    ln.init_partition();
-  }
-  int64_t lo = 0;
-  uint32_t b = kbeg[k], e = b + kcnt[k];
-  for (uint32_t p = b; p < e && !ln.err; p++) {
-    int64_t g = perm[p];
-    ln.maybe_gc();
-    ln.timers(lo, g);
-    ln.on_event(g);
-    lo = g + 1;
-  }
-  if (!ln.err) {
-    ln.maybe_gc();
-    ln.timers(lo, B.n - 1);
-  }
-  ln.flush_ret();
-  if (ln.err) {
-    ln.at<int32_t>(Yl.o_err, 0) |= ln.err;
-    atomicOr(err, ln.err);
-  }
-  lane_copy(Y, arena_out, k, Yl, lds, t);
-}
+// the general lanes' kernels (k_nfa_lanes<tier>, k_nfa_lanes_lds) live in lanes.hip, a unit of
+// their own (the library's units build in parallel)
+void lanes_launch(int tier, unsigned grid, hipStream_t s, const DevProg* P, const LaneLayout& Y, char* arena,
+                  const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg,
+                  const uint32_t* kcnt, int32_t nlanes, int* err);
+void lanes_launch_lds(unsigned grid, unsigned block, hipStream_t s, const DevProg* P, const LaneLayout& Y,
+                      const char* arena, char* arena_out, const LaneLayout& Yl, const BatchView& B, const MatchOut& O,
+                      const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt, int32_t nlanes, int* err);
 
 // ---------------------------------------------------------------- engine
 constexpr int32_t SWEEP_MIN_KEYS = 256;
@@ -640,14 +539,12 @@ struct shp_engine {
         int L = cfg.max_keys;
         kt.mark("nfa_lanes", stream);
         if (lds_lanes > 0 && tier == 0) {  // reads the committed arena, writes arena2
-          k_nfa_lanes_lds<<<(L + lds_lanes - 1) / lds_lanes, lds_lanes, (size_t)Yl.bytes, stream>>>(
-              dprog, Y, arena, arena2, Yl, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+          lanes_launch_lds((unsigned)((L + lds_lanes - 1) / lds_lanes), (unsigned)lds_lanes, stream, dprog, Y, arena,
+                           arena2, Yl, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
         } else {
           HIP_OK(hipMemcpyAsync(arena2, arena, Y.bytes, hipMemcpyDeviceToDevice, stream));
           const unsigned gl = (unsigned)((L + 63) / 64);
-          if (tier == 0) k_nfa_lanes<0><<<gl, 64, 0, stream>>>(dprog, Y, arena2, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
-          else if (tier == 1) k_nfa_lanes<1><<<gl, 64, 0, stream>>>(dprog, Y, arena2, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
-          else k_nfa_lanes<2><<<gl, 64, 0, stream>>>(dprog, Y, arena2, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
+          lanes_launch(tier, gl, stream, dprog, Y, arena2, B, O, d_perm, d_kbeg, d_kcnt, L, d_err);
         }
         kt.mark(nullptr, stream);
       }
@@ -991,7 +888,7 @@ struct shp_engine {
     jnum(o, h.seq);
     o += ",\"clock\":";
     jnum(o, h.clock);
-    if (fast == 0) {  // general lanes: the capacity tier of the pools and lists (LaneCaps)
+    if (fast == 0 || fast == 4) {  // lanes: the tier of the pools and lists (LaneCaps); labs: of the rings
       o += ",\"tier\":";
       jnum(o, h.pad);
     }

@@ -67,13 +67,13 @@ struct KTimer {
   }
 };
 
-__global__ void k_fast_gather(const DevProg* __restrict__ Pp, BatchView B, FastDev F, const uint32_t* __restrict__ perm,
+static __global__ void k_fast_gather(const DevProg* __restrict__ Pp, BatchView B, FastDev F, const uint32_t* __restrict__ perm,
                               const uint32_t* __restrict__ skey, int64_t n, int* err) {
   int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; p < n; p += (int64_t)gridDim.x * blockDim.x) fast_gather_item(*Pp, B, F, perm, skey, p, err);
 }
 
-__global__ void k_fast_search(const DevProg* __restrict__ Pp, BatchView B, FastDev F, const uint32_t* __restrict__ perm,
+static __global__ void k_fast_search(const DevProg* __restrict__ Pp, BatchView B, FastDev F, const uint32_t* __restrict__ perm,
                               const uint32_t* __restrict__ skey, const uint32_t* __restrict__ kbeg,
                               const uint32_t* __restrict__ kcnt, int64_t n, int fstream) {
   int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -83,13 +83,13 @@ __global__ void k_fast_search(const DevProg* __restrict__ Pp, BatchView B, FastD
   for (int64_t c = p; c < (int64_t)F.nk * FCC; c += stride) fast_search_carry_item(B, F, perm, kbeg, kcnt, c, fstream);
 }
 
-__global__ void k_fast_seq(FastDev F, BatchView B, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ kbeg,
+static __global__ void k_fast_seq(FastDev F, BatchView B, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ kbeg,
                            const uint32_t* __restrict__ kcnt, int fstream) {
   int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < F.nk) fast_seq_item(F, B, perm, kbeg, kcnt, k, fstream);
 }
 
-__global__ void k_fast_emit(FastDev F, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
+static __global__ void k_fast_emit(FastDev F, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
                             const uint32_t* __restrict__ skey, const uint32_t* __restrict__ kbeg, int64_t n,
                             const unsigned long long* total, int* err) {
   int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -101,13 +101,13 @@ __global__ void k_fast_emit(FastDev F, BatchView B, MatchOut O, const uint32_t* 
   for (; q < n; q += (int64_t)gridDim.x * blockDim.x) fast_emit_item(F, B, O, perm, skey, kbeg, q);
 }
 
-__global__ void k_fast_carry(FastDev F, BatchView B, const uint32_t* __restrict__ perm,
+static __global__ void k_fast_carry(FastDev F, BatchView B, const uint32_t* __restrict__ perm,
                              const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt, int* err) {
   int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < F.nk) fast_carry_item(F, B, perm, kbeg, kcnt, k, err);
 }
 
-__global__ void k_fast_init(FastDev F) {
+static __global__ void k_fast_init(FastDev F) {
   int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= F.nk) return;
   F.c_n[k] = 0;
@@ -117,7 +117,7 @@ __global__ void k_fast_init(FastDev F) {
   F.first_open[k] = 0xffffffffu;
 }
 
-__global__ void k_fast_total(const uint32_t* nclose, const uint32_t* moff, int64_t n, unsigned long long* total) {
+static __global__ void k_fast_total(const uint32_t* nclose, const uint32_t* moff, int64_t n, unsigned long long* total) {
   *total = n > 0 ? (unsigned long long)moff[n - 1] + nclose[n - 1] : 0ull;
 }
 

@@ -24,8 +24,8 @@
 // modelled, as on the general lanes (parity-unpinned).  A key whose timestamps
 // decrease fails the push with SHP_ERR_UNSUPPORTED (the general lanes, force_general = 1, replay
 // such streams exactly).  The waiting pairs of a key form a ring of wcap entries: 16 in LDS at
-// first, growing to 256 and 4096 in HBM (capacity tiers, as the general lanes have) when a push
-// overflows it; the push then re-runs from the committed state.
+// first, growing x16 per tier in HBM (256, 4096, 65536, ... capacity tiers, as the general lanes
+// have) when a push overflows it; the push then re-runs from the committed state.
 //
 // Kernels: the batch is partitioned by key with the engine's stable radix sort; k_labs runs one
 // thread per key over its events in arrival order (pend in registers, waits in LDS), twice: a
@@ -46,8 +46,11 @@
 namespace shp {
 
 constexpr int LA_WCAP = 8;                       // waiting pairs per key held in LDS (tier 0)
-constexpr int LA_TIERS = 3;
-constexpr int32_t LA_CAPS[LA_TIERS] = {8, 256, 4096};
+// the reference's per-key timer queue is unbounded (Scheduler.java: a LinkedBlockingQueue): the
+// rings grow x16 per tier while device memory lasts (set_tier fails, and the push with it, only
+// when the next tier's rings do not fit)
+constexpr int LA_TIERS = 6;
+constexpr int32_t LA_CAPS[LA_TIERS] = {8, 256, 4096, 65536, 1 << 20, 1 << 24};
 constexpr int LA_SB = 16;                        // events of a key staged in LDS per refill
 
 struct __attribute__((aligned(16))) LaEv {  // one event: packed (32 B, one sector), key order, LDS staging
@@ -119,7 +122,7 @@ struct LabsDev {
 // event g in arrival order (coalesced reads): ts, clock, batch index, the value of its stream's
 // column, stream, null -- one 32-byte record, so the key-order gather reads one sector per event
 // (the five columns gathered separately cost five: 9.0 ms per 100M events)
-__global__ void k_labs_pack(LabsDev D, BatchView B, int64_t n) {
+static __global__ void k_labs_pack(LabsDev D, BatchView B, int64_t n) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x) {
     const int st = B.stream ? B.stream[g] : 0;
     const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
@@ -135,7 +138,7 @@ __global__ void k_labs_pack(LabsDev D, BatchView B, int64_t n) {
   }
 }
 // sorted position i <- the packed event perm[i]
-__global__ void k_labs_gather(LabsDev D, const uint32_t* __restrict__ perm, int64_t n) {
+static __global__ void k_labs_gather(LabsDev D, const uint32_t* __restrict__ perm, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     D.s_ev[i] = D.p_ev[perm[i]];
 }
@@ -435,7 +438,7 @@ __device__ __forceinline__ bool la_kill(const LaPredD& p, const LaKill& K, doubl
 
 // one pass: records into the key's region of D.rec, the key's count into D.cm, the state into
 // copy wr; k_labs_out then writes the push's records contiguously
-__global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
+static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
                                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                                int* err) {
   __shared__ LaWait A[64];  // waiting pairs, completion order
@@ -825,7 +828,7 @@ __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uin
 
 // k_labs_w's records of each key (its region of D.rec) to the push's output at the key's offset,
 // with the fire event found as k_labs_pos does
-__global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ kbeg,
+static __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ kbeg,
                                                   const uint32_t* __restrict__ kcnt, int* err) {
   const int k = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   if (k >= D.nk) return;
@@ -870,7 +873,7 @@ __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B, MatchO
 
 // the event that fired each timer record of the push: the first batch index in [pos, aux] whose
 // running clock reaches the record's due time (the playback clock is non-decreasing)
-__global__ void k_labs_pos(LabsDev D, BatchView B, MatchOut O) {
+static __global__ void k_labs_pos(LabsDev D, BatchView B, MatchOut O) {
   const int64_t m = min((int64_t)O.count[0], O.cap);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t a = O.pos[i], b = D.aux[i];
@@ -885,7 +888,7 @@ __global__ void k_labs_pos(LabsDev D, BatchView B, MatchOut O) {
 }
 
 // a key's waiting pairs into a ring of another capacity (tier change), head reset to 0
-__global__ void k_labs_migrate(LabsDev Dn, LabsDev Do) {
+static __global__ void k_labs_migrate(LabsDev Dn, LabsDev Do) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= Do.nk) return;
   const int c = Do.cur;
@@ -896,7 +899,7 @@ __global__ void k_labs_migrate(LabsDev Dn, LabsDev Do) {
   Dn.pend[c][k] = s;
 }
 
-__global__ void k_labs_init(LabsDev D) {
+static __global__ void k_labs_init(LabsDev D) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < D.nk) {
     LaPend s{};

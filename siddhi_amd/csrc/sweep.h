@@ -26,9 +26,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <rocprim/rocprim.hpp>
 #include <cmath>
 #include <cstring>
+#include <rocprim/rocprim.hpp>
 #include <utility>
 #include <stdexcept>
 #include <vector>
@@ -371,7 +371,7 @@ __device__ __forceinline__ uint32_t sw_block_scan(uint32_t v, uint32_t* wtot, ui
 }
 
 // ------------------------------------------------------------------ pass 1: count
-__global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B, const int32_t* __restrict__ key,
+static __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B, const int32_t* __restrict__ key,
                                                          int* err) {
   __shared__ uint32_t h[SW_MAXOWN];
   const int st = blockIdx.x;
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B
 }
 
 // ------------------------------------------------------------------ pass 2: stable scatter by owner
-__global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchView B, const int32_t* __restrict__ key,
+static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchView B, const int32_t* __restrict__ key,
                                                            int* err) {
   // dynamic LDS: per-wave counts (then write cursors) [SWP_WAVES][nown], running owner offsets
   // [nown], and (lk_lds) the key -> local key table
@@ -1443,7 +1443,7 @@ __global__ __launch_bounds__(SWS_THREADS, 4) void k_sw_solve(SweepDev D, BatchVi
 // expansion read stale pair words as batch indices g and loaded B.ts[g] / key[g] far out of
 // bounds.  Now a handed-back push is not expanded (the exact re-run expands its own output), and
 // any pair whose index falls outside the push sets SWE_BOUND instead of being dereferenced.
-__global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchOut O, int p32, int* err) {
+static __global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchOut O, int p32, int* err) {
   // a push k_sw_lean handed back has reserved slots it never wrote: the exact re-run expands
   if (*err & SWE_LEAN) return;
   int bad = 0;
@@ -1488,7 +1488,7 @@ __global__ void k_sw_expand(BatchView B, const int32_t* __restrict__ key, MatchO
   if (bad) atomicOr(err, bad);
 }
 
-__global__ void k_sw_init(SweepDev D) {
+static __global__ void k_sw_init(SweepDev D) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < D.nown) D.c_n[0][i] = D.c_n[1][i] = 0;
   if (i < (int64_t)D.nown * SW_LK) D.lastc[0][i] = D.lastc[1][i] = 0;
@@ -1502,6 +1502,15 @@ __global__ void k_sw_init(SweepDev D) {
 
 // ------------------------------------------------------------------ host side
 namespace shp {
+
+// The solve kernels' template instantiations live in units of their own (sweep_solve.hip, built
+// once per NT1, and sweep_lean.hip), so the library's units build in parallel.
+void sw_launch_solve(int nt1, int nt2, int ct, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                     const MatchOut& O, int* err);
+void sw_launch_lean(bool bal, int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                    const MatchOut& O, int* err);
+void sw_launch_spill(int nt2, int ct, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                     const MatchOut& O, int* err);
 
 struct SweepState {
   SweepDev D{};
@@ -1832,41 +1841,14 @@ struct SweepState {
 
   void launch_lean(const BatchView& B, const MatchOut& O, int* err, hipStream_t s) {
     static const int bal = getenv("SHP_SW_BAL") ? atoi(getenv("SHP_SW_BAL")) : 0;  // A/B: k_sw_bal
-    if (bal) {
-#define SB_CASE(c, p) \
-  case c * 8 + p: k_sw_bal<c, p><<<D.nown, SL_THREADS, 0, s>>>(D, B, O, err); break;
-      switch (ct * 8 + lean_opc) {
-        SB_CASE(1, 1) SB_CASE(1, 2) SB_CASE(1, 3) SB_CASE(1, 4) SB_CASE(1, 5) SB_CASE(1, 6)
-        SB_CASE(2, 1) SB_CASE(2, 2) SB_CASE(2, 3) SB_CASE(2, 4) SB_CASE(2, 5) SB_CASE(2, 6)
-        default: break;
-      }
-#undef SB_CASE
-      return;
-    }
-#define SL_CASE(c, p) \
-  case c * 8 + p: k_sw_lean<c, p><<<D.nown, SL_THREADS, 0, s>>>(D, B, O, err); break;
-    switch (ct * 8 + lean_opc) {
-      SL_CASE(1, 1) SL_CASE(1, 2) SL_CASE(1, 3) SL_CASE(1, 4) SL_CASE(1, 5) SL_CASE(1, 6)
-      SL_CASE(2, 1) SL_CASE(2, 2) SL_CASE(2, 3) SL_CASE(2, 4) SL_CASE(2, 5) SL_CASE(2, 6)
-      default: break;
-    }
-#undef SL_CASE
+    sw_launch_lean(bal != 0, ct, lean_opc, (unsigned)D.nown, s, D, B, O, err);
   }
 
   // the exact solve (k_sw_solve) over the partition the scatter left; also the re-run of a push
   // k_sw_lean handed back with SWE_LEAN (the per-owner state it read is unchanged)
   void solve(const BatchView& B, const MatchOut& O, int* err, hipStream_t s, KTimer& kt) {
     kt.mark("sw_solve", s);
-    switch ((D.f1.n * 3 + D.f2.n) * 3 + ct) {
-#define SW_CASE(a, b, c) \
-  case (a * 3 + b) * 3 + c: k_sw_solve<a, b, c><<<D.nown, SWS_THREADS, 0, s>>>(D, B, O, err); break;
-#define SW_CASES(a, b) SW_CASE(a, b, 0) SW_CASE(a, b, 1) SW_CASE(a, b, 2)
-      SW_CASES(0, 0) SW_CASES(0, 1) SW_CASES(0, 2) SW_CASES(1, 0) SW_CASES(1, 1) SW_CASES(1, 2)
-      SW_CASES(2, 0) SW_CASES(2, 1) SW_CASES(2, 2)
-#undef SW_CASES
-#undef SW_CASE
-      default: break;
-    }
+    sw_launch_solve(D.f1.n, D.f2.n, ct, (unsigned)D.nown, s, D, B, O, err);
     kt.mark(nullptr, s);
   }
 
@@ -1974,14 +1956,7 @@ struct SweepState {
       throw std::runtime_error("sweep: spill sizes");
     (void)rd;
     kt.mark("sw_spill", s);
-    switch (D.f2.n * 3 + ct) {
-#define SP_CASE(b, c) \
-  case b * 3 + c: k_sw_spill<b, c><<<D.nown, SP_THREADS, 0, s>>>(D, B, O, err); break;
-      SP_CASE(0, 0) SP_CASE(0, 1) SP_CASE(0, 2) SP_CASE(1, 0) SP_CASE(1, 1) SP_CASE(1, 2)
-      SP_CASE(2, 0) SP_CASE(2, 1) SP_CASE(2, 2)
-#undef SP_CASE
-      default: break;
-    }
+    sw_launch_spill(D.f2.n, ct, (unsigned)D.nown, s, D, B, O, err);
     kt.mark(nullptr, s);
   }
   // after a committed push: are owners still spilled?  When none is, the spill state is cleared

@@ -1,0 +1,54 @@
+// siddhi-hip: the instantiations of k_sw_lean / k_sw_bal (the headline shape's solves) and
+// k_sw_spill (spilled owners), and the dispatcher of k_sw_solve's units (sweep_solve.hip), in a
+// unit of their own so the library's units build in parallel.
+#include "sweep.h"
+
+namespace shp {
+
+void sw_launch_solve_nt1_0(int, int, unsigned, hipStream_t, const SweepDev&, const BatchView&, const MatchOut&, int*);
+void sw_launch_solve_nt1_1(int, int, unsigned, hipStream_t, const SweepDev&, const BatchView&, const MatchOut&, int*);
+void sw_launch_solve_nt1_2(int, int, unsigned, hipStream_t, const SweepDev&, const BatchView&, const MatchOut&, int*);
+
+void sw_launch_solve(int nt1, int nt2, int ct, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                     const MatchOut& O, int* err) {
+  if (nt1 == 0) sw_launch_solve_nt1_0(nt2, ct, grid, s, D, B, O, err);
+  else if (nt1 == 1) sw_launch_solve_nt1_1(nt2, ct, grid, s, D, B, O, err);
+  else if (nt1 == 2) sw_launch_solve_nt1_2(nt2, ct, grid, s, D, B, O, err);
+}
+
+void sw_launch_lean(bool bal, int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                    const MatchOut& O, int* err) {
+  if (bal) {
+#define SB_CASE(c, p) \
+  case c * 8 + p: k_sw_bal<c, p><<<grid, SL_THREADS, 0, s>>>(D, B, O, err); break;
+    switch (ct * 8 + opc) {
+      SB_CASE(1, 1) SB_CASE(1, 2) SB_CASE(1, 3) SB_CASE(1, 4) SB_CASE(1, 5) SB_CASE(1, 6)
+      SB_CASE(2, 1) SB_CASE(2, 2) SB_CASE(2, 3) SB_CASE(2, 4) SB_CASE(2, 5) SB_CASE(2, 6)
+      default: break;
+    }
+#undef SB_CASE
+    return;
+  }
+#define SL_CASE(c, p) \
+  case c * 8 + p: k_sw_lean<c, p><<<grid, SL_THREADS, 0, s>>>(D, B, O, err); break;
+  switch (ct * 8 + opc) {
+    SL_CASE(1, 1) SL_CASE(1, 2) SL_CASE(1, 3) SL_CASE(1, 4) SL_CASE(1, 5) SL_CASE(1, 6)
+    SL_CASE(2, 1) SL_CASE(2, 2) SL_CASE(2, 3) SL_CASE(2, 4) SL_CASE(2, 5) SL_CASE(2, 6)
+    default: break;
+  }
+#undef SL_CASE
+}
+
+void sw_launch_spill(int nt2, int ct, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                     const MatchOut& O, int* err) {
+  switch (nt2 * 3 + ct) {
+#define SP_CASE(b, c) \
+  case b * 3 + c: k_sw_spill<b, c><<<grid, SP_THREADS, 0, s>>>(D, B, O, err); break;
+    SP_CASE(0, 0) SP_CASE(0, 1) SP_CASE(0, 2) SP_CASE(1, 0) SP_CASE(1, 1) SP_CASE(1, 2)
+    SP_CASE(2, 0) SP_CASE(2, 1) SP_CASE(2, 2)
+#undef SP_CASE
+    default: break;
+  }
+}
+
+}  // namespace shp

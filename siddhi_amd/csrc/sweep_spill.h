@@ -293,7 +293,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_sw_spill(SweepDev D, BatchView B
 
 // the owners whose carry overflowed in a push become spilled in the committed state (their carry
 // stays in the LDS solves' arrays: sp_n = -1), for the re-run of that push
-__global__ void k_sw_mark_spilled(SweepDev D) {
+static __global__ void k_sw_mark_spilled(SweepDev D) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= D.nown) return;
   if (D.ovf[o]) {
@@ -304,7 +304,7 @@ __global__ void k_sw_mark_spilled(SweepDev D) {
 }
 
 // per owner: first record offset, record count, carry-in count (host sizing of the spill scratch)
-__global__ void k_sw_spill_sizes(SweepDev D, int64_t* out) {
+static __global__ void k_sw_spill_sizes(SweepDev D, int64_t* out) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= D.nown) return;
   const int rd = D.cur;

@@ -361,3 +361,25 @@ def test_labs_hands_back_keys_with_many_waiting_pairs():
     assert compare(want, got) is None, compare(want, got)
     assert sum(len(x) for x in want.values()) > 5000
     assert eng.stat("labs_fallbacks") > 0
+
+
+@pytest.mark.gpu
+def test_labs_more_than_4096_waiting_pairs():
+    """`for 20 sec`: a pair completes every ~2 ms on one key and none is killed, so ~10k pairs
+    wait on the absent state at once -- past the 4096 ring -- and the rings grow to the 65536 tier
+    (the reference's timer queue is unbounded).  Exact against the oracle."""
+    from siddhi_amd import synth
+    from siddhi_amd.query.compiler import compile_app
+    app = synth.QUERIES[4].replace("for 5 sec within 10 sec", "for 20 sec within 30 sec")
+    cq = compile_app(app)[1][0]
+    n = 60_000
+    rng = np.random.default_rng(9)
+    g = {"ts": np.arange(n, dtype=np.int64) + 10_000, "key": np.zeros(n, np.int32),
+         "stream": rng.integers(0, 2, n).astype(np.int32),
+         "price": (50 + rng.integers(0, 1000, n) / 100.0).astype(np.float32)}
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g, 30_000))
+    eng = _hip(cq, 1, 30_000)
+    got = per_key(run(eng, cq, g, 30_000))
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 10_000
+    assert eng.describe(eng.snapshot())["engine"]["tier"] >= 3
