@@ -222,6 +222,12 @@ int shp_group_stage(shp_group* g, const shp_batch* slices);
 int shp_group_run(shp_group* g, int64_t* matches);
 /* The local ranks' matches of the last push in host memory, global key ids, per-key emission order. */
 int shp_group_fetch_matches(shp_group* g, shp_matches* out);
+/* Every rank's matches of the last push gathered to rank `root` (a collective call: every rank of
+ * a one-process-per-GPU group calls it).  The records move in HBM (RCCL send / recv to the root,
+ * or device copies within one process); global key ids, ranks in order, per-key emission order.
+ * The root's out holds host pointers (valid until the next gather); other ranks get m = 0.
+ * "the matches are ncclGather'ed to rank 0". */
+int shp_group_gather_matches(shp_group* g, int32_t root, shp_matches* out);
 int shp_group_local_engines(const shp_group* g);
 shp_engine* shp_group_engine(shp_group* g, int32_t i);  /* local rank i's engine (timings, snapshots) */
 const char* shp_group_last_error(const shp_group* g);

@@ -20,7 +20,8 @@ HEADERS = ["nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "js
 # (object name, source, extra flags): the kernel families are split over units that build in
 # parallel (sweep_solve.hip once per e1 term count), heaviest first
 UNITS = [("sweep_solve0", "sweep_solve.hip", ["-DSW_NT1=0"]), ("sweep_solve1", "sweep_solve.hip", ["-DSW_NT1=1"]),
-         ("sweep_solve2", "sweep_solve.hip", ["-DSW_NT1=2"]), ("lanes", "lanes.hip", []),
+         ("sweep_solve2", "sweep_solve.hip", ["-DSW_NT1=2"])] + \
+        [(f"lanes{t}", "lanes.hip", [f"-DSHP_LANE_TIER={t}"]) for t in range(5)] + [
          ("sweep_lean", "sweep_lean.hip", []), ("engine", "engine.hip", []), ("group", "group.hip", []),
          ("siddhiql", "siddhiql.cpp", []), ("shard", "shard.hip", []), ("synth", "synth.hip", [])]
 DEPS = HEADERS + sorted({u[1] for u in UNITS})

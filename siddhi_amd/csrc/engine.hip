@@ -173,9 +173,28 @@ __global__ __launch_bounds__(256) void k_lane_migrate(LaneLayout Yd, char* dst, 
 
 // the general lanes' kernels (k_nfa_lanes<tier>, k_nfa_lanes_lds) live in lanes.hip, a unit of
 // their own (the library's units build in parallel)
-void lanes_launch(int tier, unsigned grid, hipStream_t s, const DevProg* P, const LaneLayout& Y, char* arena,
-                  const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg,
-                  const uint32_t* kcnt, int32_t nlanes, int* err);
+#define LN_DECL(t)                                                                                        \
+  void lanes_launch_t##t(unsigned grid, hipStream_t s, const DevProg* P, const LaneLayout& Y, char* arena,   \
+                         const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg, \
+                         const uint32_t* kcnt, int32_t nlanes, int* err);
+LN_DECL(0)
+LN_DECL(1)
+LN_DECL(2)
+LN_DECL(3)
+LN_DECL(4)
+#undef LN_DECL
+static void lanes_launch(int tier, unsigned grid, hipStream_t s, const DevProg* P, const LaneLayout& Y, char* arena,
+                         const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg,
+                         const uint32_t* kcnt, int32_t nlanes, int* err) {
+  static_assert(LANE_TIERS == 5, "one lanes unit per tier");
+  switch (tier) {
+    case 0: lanes_launch_t0(grid, s, P, Y, arena, B, O, perm, kbeg, kcnt, nlanes, err); break;
+    case 1: lanes_launch_t1(grid, s, P, Y, arena, B, O, perm, kbeg, kcnt, nlanes, err); break;
+    case 2: lanes_launch_t2(grid, s, P, Y, arena, B, O, perm, kbeg, kcnt, nlanes, err); break;
+    case 3: lanes_launch_t3(grid, s, P, Y, arena, B, O, perm, kbeg, kcnt, nlanes, err); break;
+    default: lanes_launch_t4(grid, s, P, Y, arena, B, O, perm, kbeg, kcnt, nlanes, err); break;
+  }
+}
 void lanes_launch_lds(unsigned grid, unsigned block, hipStream_t s, const DevProg* P, const LaneLayout& Y,
                       const char* arena, char* arena_out, const LaneLayout& Yl, const BatchView& B, const MatchOut& O,
                       const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt, int32_t nlanes, int* err);
@@ -1370,6 +1389,23 @@ int shp_push_batch_device(shp_engine* e, const shp_batch* in, shp_matches* out) 
     int rc = e->run(in->n, false, in);  // zero-copy: the kernels read the caller's HBM columns
     if (rc != SHP_OK) return rc;
     e->fill_device(out);
+    return SHP_OK;
+  });
+}
+
+// internal (group.hip's device gather): the last push's records in HBM -- expanded to full records
+// for the pair layouts -- and the number of refs; slot_len has stride MAXS on the device
+extern "C" int shp_engine_device_records(shp_engine* e, shp_matches* out, int64_t* nrefs) {
+  if (!e || !out || !nrefs) return SHP_ERR_ARG;
+  return guarded(e, [&]() {
+    e->ensure_expanded();
+    e->fill_device(out);
+    *nrefs = 0;
+    if (out->layout != SHP_LAYOUT_AGG && out->m > 0) {
+      unsigned long long cnt[2];
+      HIP_OK(hipMemcpy(cnt, e->d_mcount, sizeof(cnt), hipMemcpyDeviceToHost));
+      *nrefs = (int64_t)cnt[1];
+    }
     return SHP_OK;
   });
 }

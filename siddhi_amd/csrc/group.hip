@@ -198,6 +198,40 @@ __global__ void k_gs_fill_tail(int64_t* ts, int32_t* key, int32_t* stream, int64
   if (seq) seq[at] = seqv;
 }
 
+// ---- device gather of the matches (shp_group_gather_matches): each rank's records of the last push
+// move to the root in HBM (RCCL send / recv between processes, peer copies within one process);
+// the per-record work (global key ids, slot stride, ref offsets) runs on the device and the host
+// takes the gathered columns with one copy each
+__global__ void k_gm_nref(const int16_t* __restrict__ slot, int64_t m, int S, int64_t* __restrict__ nref) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = 0;
+    for (int s = 0; s < S; s++) t += slot[i * shp::MAXS + s];
+    nref[i] = t;
+  }
+}
+// global key ids, slot lengths at stride S, and the refs in record order (the engine appends a
+// record's refs wherever its reservation fell): noff = exclusive scan of the records' ref counts
+__global__ void k_gm_pack(const int32_t* __restrict__ key, const int16_t* __restrict__ slot,
+                          const int64_t* __restrict__ off, const int64_t* __restrict__ refs, int64_t m, int S,
+                          int world, int rank, int32_t* __restrict__ okey, int16_t* __restrict__ oslot,
+                          const int64_t* __restrict__ noff, int64_t* __restrict__ orefs) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    okey[i] = (int32_t)((int64_t)key[i] * world + rank);  // rank-local dense id -> global key
+    if (slot) {
+      int64_t o = off[i], d = noff[i];
+      for (int s = 0; s < S; s++) {
+        const int l = slot[i * shp::MAXS + s];
+        oslot[i * S + s] = (int16_t)l;
+        for (int t = 0; t < l; t++) orefs[d++] = refs[o++];
+      }
+    }
+  }
+}
+__global__ void k_gm_rebase(int64_t* __restrict__ off, int64_t m, int64_t base) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+    off[i] += base;
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -216,6 +250,9 @@ struct DevBuf {
 int col_bytes(int8_t tag) { return (tag == shp::T_LONG || tag == shp::T_DOUBLE) ? 8 : (tag == shp::T_BOOL ? 1 : 4); }
 
 }  // namespace
+
+// engine.hip (internal): the last push's records in HBM, pair layouts expanded to full records
+extern "C" int shp_engine_device_records(shp_engine* e, shp_matches* out, int64_t* nrefs);
 
 struct shp_group {
   int world = 1;
@@ -255,6 +292,8 @@ struct shp_group {
       hipEvent_t done = nullptr;      // the exchange into this slot has landed
     } slot[3];
     int64_t last_m = 0;
+    DevBuf p_key, p_slot, p_off, p_refs, p_tmp;  // gather: this rank's records, global key ids, S-stride slots,
+                                                 // refs in record order
   };
   std::atomic<int64_t> staged{0}, ran{0};  // batches exchanged / run (at most three staged ahead)
   std::vector<Local> L;
@@ -267,6 +306,8 @@ struct shp_group {
   std::vector<int8_t> h_type;
   std::vector<int16_t> h_slot;
   std::vector<double> h_agg;
+  // gather: the root's device columns (key, ts, type, pos, ref_off, slot_len, refs, agg)
+  DevBuf g_key, g_ts, g_type, g_pos, g_off, g_slot, g_refs, g_agg;
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -617,6 +658,190 @@ int run_impl(shp_group& g, int64_t* counts) {
   return SHP_OK;
 }
 
+// shp_group_gather_matches: every rank's records of the last push to `root` (a collective call
+// between processes).  Per rank r: m_r records and n_r refs, all-gathered; the root's columns hold
+// rank 0's records, then rank 1's, ...; each rank's keep their engine's per-key order.
+int gather_impl(shp_group& g, int root, shp_matches* out) {
+  const int G = g.world;
+  if (root < 0 || root >= G) return g.fail(SHP_ERR_ARG, "root outside the group");
+  const int S = shp_engine_num_states(g.L[0].eng);
+  std::vector<shp_matches> dm(g.nlocal);
+  std::vector<int64_t> mine(3 * (size_t)g.nlocal);
+  for (int i = 0; i < g.nlocal; i++) {
+    int64_t nr = 0;
+    const int rc = shp_engine_device_records(g.L[i].eng, &dm[i], &nr);
+    if (rc != SHP_OK) return g.fail(rc, "rank " + std::to_string(g.L[i].rank) + ": " + shp_last_error(g.L[i].eng));
+    mine[3 * i] = dm[i].m;
+    mine[3 * i + 1] = nr;
+    mine[3 * i + 2] = dm[i].layout;
+  }
+  std::vector<int64_t> all(3 * (size_t)G);
+  if (g.rccl) {
+    shp_group::Local& l = g.L[0];
+    GH(hipSetDevice(l.dev));
+    DevBuf a, b;
+    a.ensure(3 * 8);
+    b.ensure((size_t)G * 3 * 8);
+    GH(hipMemcpyAsync(a.p, mine.data(), 3 * 8, hipMemcpyHostToDevice, l.s));
+    GN(ncclAllGather(a.p, b.p, 3, ncclInt64, g.comm, l.s));
+    GH(hipMemcpyAsync(all.data(), b.p, all.size() * 8, hipMemcpyDeviceToHost, l.s));
+    GH(hipStreamSynchronize(l.s));
+  } else {
+    all = mine;
+  }
+  const bool agg = all[2] == SHP_LAYOUT_AGG;
+  std::vector<int64_t> mb(G + 1, 0), rb(G + 1, 0);
+  for (int r = 0; r < G; r++) {
+    mb[r + 1] = mb[r] + all[3 * r];
+    rb[r + 1] = rb[r] + all[3 * r + 1];
+  }
+  const int64_t M = mb[G], R = rb[G];
+  // pack: global key ids, slot lengths at stride S, refs in record order with their new offsets
+  for (int i = 0; i < g.nlocal; i++) {
+    shp_group::Local& l = g.L[i];
+    const int64_t m = dm[i].m, nr = mine[3 * i + 1];
+    GH(hipSetDevice(l.dev));
+    const unsigned gb = (unsigned)std::min<int64_t>((m + 255) / 256, 4096);
+    l.p_key.ensure((size_t)std::max<int64_t>(m, 1) * 4);
+    if (!agg) {
+      l.p_slot.ensure((size_t)std::max<int64_t>(m, 1) * S * 2);
+      l.p_off.ensure((size_t)std::max<int64_t>(m, 1) * 8);
+      l.p_refs.ensure((size_t)std::max<int64_t>(nr, 1) * 8);
+      l.rmax.ensure((size_t)std::max<int64_t>(m, 1) * 8);  // scratch: the records' ref counts
+    }
+    if (m > 0 && !agg) {
+      k_gm_nref<<<gb, 256, 0, l.s>>>(dm[i].slot_len, m, S, (int64_t*)l.rmax.p);
+      size_t tb = 0;
+      GH(rocprim::exclusive_scan(nullptr, tb, (const int64_t*)l.rmax.p, (int64_t*)l.p_off.p, (int64_t)0, (size_t)m,
+                                 rocprim::plus<int64_t>(), l.s));
+      l.p_tmp.ensure(tb);
+      GH(rocprim::exclusive_scan(l.p_tmp.p, tb, (const int64_t*)l.rmax.p, (int64_t*)l.p_off.p, (int64_t)0, (size_t)m,
+                                 rocprim::plus<int64_t>(), l.s));
+    }
+    if (m > 0)
+      k_gm_pack<<<gb, 256, 0, l.s>>>(dm[i].key, agg ? nullptr : dm[i].slot_len, dm[i].ref_off, dm[i].refs, m, S, G,
+                                     l.rank, (int32_t*)l.p_key.p, agg ? nullptr : (int16_t*)l.p_slot.p,
+                                     (const int64_t*)l.p_off.p, (int64_t*)l.p_refs.p);
+    GH(hipGetLastError());
+  }
+  // the root's local slot (an in-process group: local index = rank)
+  int ri = -1;
+  for (int i = 0; i < g.nlocal; i++)
+    if (g.L[i].rank == root) ri = i;
+  struct Col {
+    DevBuf* dst;
+    int sz;
+  };
+  std::vector<Col> cols = agg ? std::vector<Col>{{&g.g_key, 4}, {&g.g_agg, 8}}
+                              : std::vector<Col>{{&g.g_key, 4}, {&g.g_ts, 8}, {&g.g_type, 1}, {&g.g_pos, 8},
+                                                 {&g.g_off, 8}, {&g.g_slot, 2 * S}};
+  auto src_of = [&](int i, int c) -> const void* {  // local rank i's device column c (and refs: c = -1)
+    const shp_matches& d = dm[i];
+    if (c < 0) return g.L[i].p_refs.p;
+    if (c == 0) return g.L[i].p_key.p;
+    if (agg) return d.agg;
+    switch (c) {
+      case 1: return d.ts;
+      case 2: return d.type;
+      case 3: return d.pos;
+      case 4: return g.L[i].p_off.p;
+      default: return g.L[i].p_slot.p;
+    }
+  };
+  if (ri >= 0) {
+    GH(hipSetDevice(g.L[ri].dev));
+    for (auto& c : cols) c.dst->ensure((size_t)std::max<int64_t>(M, 1) * c.sz);
+    if (!agg) g.g_refs.ensure((size_t)std::max<int64_t>(R, 1) * 8);
+  }
+  if (g.rccl) {
+    shp_group::Local& l = g.L[0];
+    GH(hipSetDevice(l.dev));
+    GN(ncclGroupStart());
+    for (size_t c = 0; c < cols.size() + (agg ? 0 : 1); c++) {
+      const bool refs = c == cols.size();
+      const int sz = refs ? 8 : cols[c].sz;
+      const int64_t mm = refs ? mine[1] : mine[0];  // this rank's records / refs
+      if (mm > 0) GN(ncclSend(src_of(0, refs ? -1 : (int)c), (size_t)mm * sz, ncclChar, root, g.comm, l.s));
+      if (l.rank == root)
+        for (int r = 0; r < G; r++) {
+          const int64_t n = refs ? all[3 * r + 1] : all[3 * r];
+          const int64_t o = refs ? rb[r] : mb[r];
+          void* dst = refs ? g.g_refs.p : cols[c].dst->p;
+          if (n > 0) GN(ncclRecv((char*)dst + o * sz, (size_t)n * sz, ncclChar, r, g.comm, l.s));
+        }
+    }
+    GN(ncclGroupEnd());
+  } else {
+    shp_group::Local& rl = g.L[ri];
+    for (int i = 0; i < g.nlocal; i++) {
+      GH(hipSetDevice(g.L[i].dev));
+      GH(hipStreamSynchronize(g.L[i].s));
+    }
+    GH(hipSetDevice(rl.dev));
+    for (int i = 0; i < g.nlocal; i++) {
+      const int r = g.L[i].rank;
+      for (size_t c = 0; c < cols.size() + (agg ? 0 : 1); c++) {
+        const bool refs = c == cols.size();
+        const int sz = refs ? 8 : cols[c].sz;
+        const int64_t n = refs ? all[3 * r + 1] : all[3 * r];
+        const int64_t o = refs ? rb[r] : mb[r];
+        void* dst = refs ? g.g_refs.p : cols[c].dst->p;
+        if (n > 0)
+          GH(hipMemcpyPeerAsync((char*)dst + o * sz, rl.dev, src_of(i, refs ? -1 : (int)c), g.L[i].dev, (size_t)n * sz,
+                                rl.s));
+      }
+    }
+  }
+  *out = shp_matches{};
+  out->num_states = S;
+  out->layout = agg ? SHP_LAYOUT_AGG : SHP_LAYOUT_FULL;
+  if (ri < 0) {  // not the root: its records went there
+    out->m = 0;
+    return SHP_OK;
+  }
+  shp_group::Local& rl = g.L[ri];
+  GH(hipSetDevice(rl.dev));
+  if (!agg)  // each source's ref offsets continue after the refs of the ranks before it
+    for (int r = 1; r < G; r++)
+      if (all[3 * r] > 0)
+        k_gm_rebase<<<(unsigned)std::min<int64_t>((all[3 * r] + 255) / 256, 4096), 256, 0, rl.s>>>(
+            (int64_t*)g.g_off.p + mb[r], all[3 * r], rb[r]);
+  GH(hipGetLastError());
+  g.h_key.resize(M);
+  GH(hipMemcpyAsync(g.h_key.data(), g.g_key.p, (size_t)M * 4, hipMemcpyDeviceToHost, rl.s));
+  if (agg) {
+    g.h_agg.resize(M);
+    GH(hipMemcpyAsync(g.h_agg.data(), g.g_agg.p, (size_t)M * 8, hipMemcpyDeviceToHost, rl.s));
+  } else {
+    g.h_ts.resize(M);
+    g.h_type.resize(M);
+    g.h_pos.resize(M);
+    g.h_off.resize(M);
+    g.h_slot.resize((size_t)M * S);
+    g.h_refs.resize(R);
+    GH(hipMemcpyAsync(g.h_ts.data(), g.g_ts.p, (size_t)M * 8, hipMemcpyDeviceToHost, rl.s));
+    GH(hipMemcpyAsync(g.h_type.data(), g.g_type.p, (size_t)M, hipMemcpyDeviceToHost, rl.s));
+    GH(hipMemcpyAsync(g.h_pos.data(), g.g_pos.p, (size_t)M * 8, hipMemcpyDeviceToHost, rl.s));
+    GH(hipMemcpyAsync(g.h_off.data(), g.g_off.p, (size_t)M * 8, hipMemcpyDeviceToHost, rl.s));
+    GH(hipMemcpyAsync(g.h_slot.data(), g.g_slot.p, (size_t)M * S * 2, hipMemcpyDeviceToHost, rl.s));
+    GH(hipMemcpyAsync(g.h_refs.data(), g.g_refs.p, (size_t)R * 8, hipMemcpyDeviceToHost, rl.s));
+  }
+  GH(hipStreamSynchronize(rl.s));
+  out->m = M;
+  out->key = g.h_key.data();
+  if (agg) {
+    out->agg = g.h_agg.data();
+    return SHP_OK;
+  }
+  out->ts = g.h_ts.data();
+  out->type = g.h_type.data();
+  out->pos = g.h_pos.data();
+  out->ref_off = g.h_off.data();
+  out->slot_len = g.h_slot.data();
+  out->refs = g.h_refs.data();
+  return SHP_OK;
+}
+
 int create_impl(shp_group* g, const char* json, const shp_config* cfg, int world, const int32_t* devices, int rank,
                 const void* comm_id) {
   if (world < 1 || world > GS_MAXG) return g->fail(SHP_ERR_ARG, "world must be in [1, 16]");
@@ -807,6 +1032,11 @@ int shp_group_fetch_matches(shp_group* g, shp_matches* out) {
     out->refs = g->h_refs.data();
     return SHP_OK;
   });
+}
+
+int shp_group_gather_matches(shp_group* g, int32_t root, shp_matches* out) {
+  if (!g || !out) return SHP_ERR_ARG;
+  return guarded(g, [&]() { return gather_impl(*g, root, out); });
 }
 
 const char* shp_group_last_error(const shp_group* g) { return g ? g->err.c_str() : "null group"; }

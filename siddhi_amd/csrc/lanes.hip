@@ -76,6 +76,7 @@ __device__ inline void lane_copy(const LaneLayout& Yd, char* dst, int64_t ld, co
   }
 }
 
+#if SHP_LANE_TIER == 0
 // Few keys: the lanes' state lives in LDS for the batch (copied in and out of the HBM arena),
 // so the per-event chain of dependent state accesses runs at LDS latency instead of HBM
 // latency.  Same Lane code, one lane per thread, blockDim lanes per workgroup.
@@ -118,18 +119,24 @@ __global__ __launch_bounds__(64) SHP_LANES_ATTR void k_nfa_lanes_lds(const DevPr
 }
 
 
-void lanes_launch(int tier, unsigned grid, hipStream_t s, const DevProg* P, const LaneLayout& Y, char* arena,
-                  const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg,
-                  const uint32_t* kcnt, int32_t nlanes, int* err) {
-  switch (tier) {
-    case 0: k_nfa_lanes<0><<<grid, 64, 0, s>>>(P, Y, arena, B, O, perm, kbeg, kcnt, nlanes, err); break;
-    case 1: k_nfa_lanes<1><<<grid, 64, 0, s>>>(P, Y, arena, B, O, perm, kbeg, kcnt, nlanes, err); break;
-    default: k_nfa_lanes<2><<<grid, 64, 0, s>>>(P, Y, arena, B, O, perm, kbeg, kcnt, nlanes, err); break;
-  }
+#endif  // SHP_LANE_TIER == 0
+
+#ifndef SHP_LANE_TIER
+#error "lanes.hip is built once per capacity tier (-DSHP_LANE_TIER=0..4)"
+#endif
+// this unit's tier; tier 0's unit also holds the LDS-resident form
+#define LN_FN_(t) lanes_launch_t##t
+#define LN_FN(t) LN_FN_(t)
+void LN_FN(SHP_LANE_TIER)(unsigned grid, hipStream_t s, const DevProg* P, const LaneLayout& Y, char* arena,
+                          const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg,
+                          const uint32_t* kcnt, int32_t nlanes, int* err) {
+  k_nfa_lanes<SHP_LANE_TIER><<<grid, 64, 0, s>>>(P, Y, arena, B, O, perm, kbeg, kcnt, nlanes, err);
 }
 
+#if SHP_LANE_TIER == 0
 void lanes_launch_lds(unsigned grid, unsigned block, hipStream_t s, const DevProg* P, const LaneLayout& Y,
                       const char* arena, char* arena_out, const LaneLayout& Yl, const BatchView& B, const MatchOut& O,
                       const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt, int32_t nlanes, int* err) {
   k_nfa_lanes_lds<<<grid, block, (size_t)Yl.bytes, s>>>(P, Y, arena, arena_out, Yl, B, O, perm, kbeg, kcnt, nlanes, err);
 }
+#endif

@@ -21,10 +21,12 @@
 
 namespace shp {
 
-// per-key capacities of tier T (x1, x4, x16)
+// per-key capacities of tier T (x1, x4, x16, x64, x128: pool, list and queue indices are int16, so
+// x128 -- 16384 nodes, 4096 partials per list, 8192 queued timers per key -- is the last tier)
+SHP_HD constexpr int lane_scale(int t) { return t == 0 ? 1 : (t == 1 ? 4 : (t == 2 ? 16 : (t == 3 ? 64 : 128))); }
 template <int T>
 struct LaneCaps {
-  static constexpr int SCALE = T == 0 ? 1 : (T == 1 ? 4 : 16);
+  static constexpr int SCALE = lane_scale(T);
   static constexpr int NSE = 64 * SCALE;   // StateEvent pool per key
   static constexpr int NN = 128 * SCALE;   // StreamEvent node pool per key
   static constexpr int LCAP = 32 * SCALE;  // capacity of each pending / new-and-every list
@@ -34,7 +36,7 @@ struct LaneCaps {
   static constexpr int GC_SE_RESERVE = 24 * SCALE;
   static constexpr int GC_ND_RESERVE = 48 * SCALE;
 };
-constexpr int LANE_TIERS = 3;
+constexpr int LANE_TIERS = 5;
 
 enum LaneErr : int32_t { E_SE = 1, E_ND = 2, E_LIST = 4, E_Q = 8, E_OUT = 16, E_REF = 32 };
 enum PFlag : uint8_t { F_CHANGED = 1, F_INIT = 2, F_STARTED = 4, F_SUCCESS = 8, F_SSRESET = 16, F_INACTIVE = 32 };
@@ -54,10 +56,10 @@ struct LaneLayout {
   void build(int64_t lanes, int t = 0) {
     L = lanes;
     tier = t;
-    nse = t == 0 ? LaneCaps<0>::NSE : (t == 1 ? LaneCaps<1>::NSE : LaneCaps<2>::NSE);
-    nn = t == 0 ? LaneCaps<0>::NN : (t == 1 ? LaneCaps<1>::NN : LaneCaps<2>::NN);
-    lcap = t == 0 ? LaneCaps<0>::LCAP : (t == 1 ? LaneCaps<1>::LCAP : LaneCaps<2>::LCAP);
-    qcap = t == 0 ? LaneCaps<0>::QCAP : (t == 1 ? LaneCaps<1>::QCAP : LaneCaps<2>::QCAP);
+    nse = 64 * lane_scale(t);  // LaneCaps<t>
+    nn = 128 * lane_scale(t);
+    lcap = 32 * lane_scale(t);
+    qcap = 64 * lane_scale(t);
     const int NSE = nse, NN = nn, LCAP = lcap, QCAP = qcap;
     int64_t o = 0;
     nf = 0;

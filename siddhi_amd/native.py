@@ -29,7 +29,7 @@ SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_
            "shp_host_unregister", "shp_snapshot", "shp_restore", "shp_snapshot_describe", "shp_shard_workspace_bytes",
            "shp_shard_partition", "shp_shard_unpack", "shp_shard_partition_soa", "shp_comm_id",
            "shp_group_create", "shp_group_create_rank", "shp_group_push", "shp_group_stage", "shp_group_run",
-           "shp_group_fetch_matches",
+           "shp_group_fetch_matches", "shp_group_gather_matches",
            "shp_group_local_engines", "shp_group_engine", "shp_group_last_error", "shp_group_destroy",
            "shp_dict_create", "shp_dict_intern", "shp_dict_size", "shp_dict_string", "shp_dict_destroy",
            "shp_compile_siddhiql", "shp_siddhiql_queries", "shp_compile_last_error", "shp_engine_create_siddhiql"]
@@ -121,6 +121,7 @@ def lib():
         L.shp_group_stage.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.shp_group_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.shp_group_fetch_matches.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpMatches)]
+        L.shp_group_gather_matches.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ShpMatches)]
         L.shp_group_local_engines.argtypes = [ctypes.c_void_p]
         L.shp_group_engine.restype = ctypes.c_void_p
         L.shp_group_engine.argtypes = [ctypes.c_void_p, ctypes.c_int32]
@@ -444,6 +445,12 @@ class HipGroup:
     def fetch(self):
         mt = ShpMatches()
         self._check(lib().shp_group_fetch_matches(self.h, ctypes.byref(mt)))
+        return matches_to_numpy(mt)
+
+    def gather(self, root=0):
+        """shp_group_gather_matches: every rank's matches of the last push at `root` (collective)."""
+        mt = ShpMatches()
+        self._check(lib().shp_group_gather_matches(self.h, int(root), ctypes.byref(mt)))
         return matches_to_numpy(mt)
 
     def engine_ms(self, i, which="total"):

@@ -106,7 +106,9 @@ int hc_push(void* hp, int64_t n, const int64_t* ts, const int32_t* key, const in
   int err = 0;
   if (h->Y.tier == 0) err = run_lanes<0>(h, B, O, kbeg, kcnt, perm, n);
   else if (h->Y.tier == 1) err = run_lanes<1>(h, B, O, kbeg, kcnt, perm, n);
-  else err = run_lanes<2>(h, B, O, kbeg, kcnt, perm, n);
+  else if (h->Y.tier == 2) err = run_lanes<2>(h, B, O, kbeg, kcnt, perm, n);
+  else if (h->Y.tier == 3) err = run_lanes<3>(h, B, O, kbeg, kcnt, perm, n);
+  else err = run_lanes<4>(h, B, O, kbeg, kcnt, perm, n);
   if (n) h->clock = rmax[n - 1];
   if (!clock_only) h->seq += n;
   int64_t m = (int64_t)cnt[0];

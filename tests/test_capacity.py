@@ -138,3 +138,19 @@ def test_tier0_workload_stays_at_tier0():
         _push_all(e, ts, key, v, 1 << 14)
     assert compare(per_key(ora.fetch()), per_key(eng.fetch())) is None
     assert _tier(eng) == 0
+
+
+def test_pending_lists_grow_past_x16():
+    """2500 open partials on each of 3 keys: past tier 2 (512 per list) and tier 3 (2048), held at
+    tier 4 (x128: 4096 per list); the reference's lists are unbounded LinkedLists."""
+    cq = _cq(NEVER_CLOSES)
+    keys, opens = 3, 2500
+    ts, key, v = _pending_stream(keys, opens, 12)
+    eng = _lanes(cq, keys, max_batch=1 << 14)
+    ora = OracleEngine(cq.program_json(), 0)
+    for e in (ora, eng):
+        _push_all(e, ts, key, v, 4_001)
+    a, b = per_key(ora.fetch()), per_key(eng.fetch())
+    assert compare(a, b) is None, compare(a, b)
+    assert sum(len(x) for x in a.values()) == keys * opens
+    assert _tier(eng) == 4

@@ -176,3 +176,43 @@ def test_group_null_values_travel_with_their_events():
     grp.close()
     assert compare(want, got) is None, compare(want, got)
     assert sum(len(v) for v in want.values()) > 5_000
+
+
+@pytest.mark.parametrize("world,cfg,root", [(2, 2, 0), (3, 2, 1), (3, 4, 2), (2, 5, 1)], ids=["c2w2", "c2w3", "c4w3", "c5w2"])
+def test_group_gather_to_root_matches_oracle(world, cfg, root):
+    """shp_group_gather_matches: every rank's records move to the root in HBM (device copies here,
+    RCCL send / recv between processes), with global key ids, S-stride slots and the refs in record
+    order; per key they equal the oracle's (C4: timer matches compared without pos, as above)."""
+    import torch
+    from siddhi_amd.native import LAYOUT_AGG, LAYOUT_FULL, HipGroup
+    cq = program_for(cfg)
+    keys = {2: 600, 4: 200, 5: 1000}[cfg]
+    g = small_stream(cfg, 90_000, keys)
+    layout = LAYOUT_AGG if cfg == 5 else LAYOUT_FULL
+    grp = HipGroup(cq.program_json(), 0, max_keys=keys, max_batch=1 << 17, max_matches=1 << 17,
+                   devices=[0] * world, match_layout=layout)
+    cols = columns_for(cq, g)
+    parts = []
+    bounds = np.linspace(0, len(g["ts"]), 4).astype(np.int64)
+    for p in range(3):
+        grp.push_device(_slices(g, cols, bounds[p], bounds[p + 1], world, len(cq.program["streams"]) > 1))
+        parts.append(grp.gather(root))
+        torch.cuda.synchronize()
+    grp.close()
+    got = _concat(parts)
+    ora = run(OracleEngine(cq.program_json(), 0), cq, g)
+    if cfg == 5:
+        from test_gpu_parity import _expected_agg
+        want = _expected_agg(ora, cols[0], "avg")
+        rows = {}
+        for k, v in zip(got["key"], got["agg"]):
+            rows.setdefault(int(k), []).append(float(v))
+        assert set(rows) == set(want)
+        for k in want:
+            np.testing.assert_allclose(rows[k], want[k], rtol=1e-9, atol=0)
+        return
+    want, have = per_key(ora), per_key(got)
+    if cfg == 4:
+        want, have = _drop_pos(want), _drop_pos(have)
+    assert compare(want, have) is None, compare(want, have)
+    assert sum(len(v) for v in want.values()) > 500
