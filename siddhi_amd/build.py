@@ -22,7 +22,7 @@ HEADERS = ["nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "js
 UNITS = [("sweep_solve0", "sweep_solve.hip", ["-DSW_NT1=0"]), ("sweep_solve1", "sweep_solve.hip", ["-DSW_NT1=1"]),
          ("sweep_solve2", "sweep_solve.hip", ["-DSW_NT1=2"])] + \
         [(f"lanes{t}", "lanes.hip", [f"-DSHP_LANE_TIER={t}"]) for t in range(5)] + [
-         ("sweep_lean", "sweep_lean.hip", []), ("engine", "engine.hip", []), ("group", "group.hip", []),
+         ("sweep_lean", "sweep_lean.hip", []), ("sweep_lean_agg", "sweep_lean.hip", ["-DSW_LEAN_AGG"]), ("engine", "engine.hip", []), ("group", "group.hip", []),
          ("siddhiql", "siddhiql.cpp", []), ("shard", "shard.hip", []), ("synth", "synth.hip", [])]
 DEPS = HEADERS + sorted({u[1] for u in UNITS})
 

@@ -1509,6 +1509,8 @@ void sw_launch_solve(int nt1, int nt2, int ct, unsigned grid, hipStream_t s, con
                      const MatchOut& O, int* err);
 void sw_launch_lean(bool bal, int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                     const MatchOut& O, int* err);
+void sw_launch_lean_agg(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                        const MatchOut& O, int* err);
 void sw_launch_spill(int nt2, int ct, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                      const MatchOut& O, int* err);
 
@@ -1836,12 +1838,14 @@ struct SweepState {
   }
 
   // does this push run k_sw_lean (so SWE_LEAN may come back and ask for solve())?
-  bool lean_push() const { return lean_opc && !D.agg && !D.maybe_null; }
-  bool lean_push_for(const BatchView& B) const { return lean_opc && !D.agg && !D.maybe_null && !B.nulls[0]; }
+  // (SHP_LAYOUT_AGG: avg / sum / count fold in k_sw_lean; min / max on k_sw_solve)
+  bool lean_push() const { return lean_opc && D.agg <= 3 && !D.maybe_null; }
+  bool lean_push_for(const BatchView& B) const { return lean_push() && !B.nulls[0]; }
 
   void launch_lean(const BatchView& B, const MatchOut& O, int* err, hipStream_t s) {
     static const int bal = getenv("SHP_SW_BAL") ? atoi(getenv("SHP_SW_BAL")) : 0;  // A/B: k_sw_bal
-    sw_launch_lean(bal != 0, ct, lean_opc, (unsigned)D.nown, s, D, B, O, err);
+    if (D.agg) sw_launch_lean_agg(ct, lean_opc, (unsigned)D.nown, s, D, B, O, err);
+    else sw_launch_lean(bal != 0, ct, lean_opc, (unsigned)D.nown, s, D, B, O, err);
   }
 
   // the exact solve (k_sw_solve) over the partition the scatter left; also the re-run of a push

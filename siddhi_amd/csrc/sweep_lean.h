@@ -60,8 +60,8 @@ struct SwLeanSmem {
   uint32_t ncar[256];                // carried candidates of a key in the current carry buffer
   uint16_t ckf[2][256];              // index of a key's first entry in carry buffer 0/1
   uint8_t lastc[256];                // the key's latest event opened a candidate (SweepDev::lastc)
-  int64_t cts[2][SL_CCAP];           // carry: ts - batch base (exact)
-  int64_t cseq[2][SL_CCAP];
+  int32_t cts[2][SL_CCAP];           // carry: ts - batch base (exact; a carry beyond +-2^31 ms: SWE_LEAN)
+  int32_t cseq[2][SL_CCAP];          // carry: seq - the push's first seq (exact; beyond +-2^31: SWE_LEAN)
   uint32_t cv[2][SL_CCAP];
   uint8_t clk[2][SL_CCAP];
   uint32_t wl[SL_WAVES][SL_WL];      // worklists: position | next probe position << 16
@@ -93,10 +93,14 @@ __device__ __forceinline__ int sl_probe(const int2* tv, int qb, int end, int32_t
 
 __device__ __forceinline__ uint32_t sl_closes(uint32_t c) { return (uint32_t)__popc(c & 0xFFFFFFu) + (c >> 24); }
 
-template <int CT, int OPC>
+// AGG: SHP_LAYOUT_AGG with avg / sum / count (D.agg 1..3) -- the selector's running aggregate per
+// match (QuerySelector.processInBatchNoGroupBy, AvgAttributeAggregatorExecutor: `value += x;
+// count++`) in place of the pairs; min / max stay on k_sw_solve
+template <int CT, int OPC, bool AGG = false>
 __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView B, MatchOut O, int* err) {
   using T = typename SwTy<CT>::T;
   __shared__ SwLeanSmem S;
+  __shared__ double ag[AGG ? 2 * 256 : 1];  // AGG: per local key (running sum, count) before the chunk emitted next
   const int o = blockIdx.x;
   const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
   const uint64_t lt = sw_lanemask_lt();
@@ -116,6 +120,10 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     for (int i = tid; i < SW_LK; i += SL_THREADS) {
       const int64_t k = (int64_t)o * SW_LK + i;
       D.lastc[wr][k] = D.lastc[rd][k];
+      if constexpr (AGG) {
+        D.agg_s[wr][k] = D.agg_s[rd][k];
+        D.agg_c[wr][k] = D.agg_c[rd][k];
+      }
     }
     if (tid == 0) D.c_n[wr][o] = n0;
     return;
@@ -128,6 +136,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     return;
   }
   const int64_t base = B.ts[0];
+  const int64_t sbase = bseq(B, 0);  // carried seqs are kept relative to it
   const int32_t W = (int32_t)D.within;  // <= SW_TS_SPAN (SweepState::shape_ok)
   const SwTerm t2 = D.f2.t[0];
   const bool bconst = t2.bk == 0;
@@ -141,6 +150,11 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     S.lastc[i] = i < SW_LK ? D.lastc[rd][(int64_t)o * SW_LK + i] : 0;
   }
   for (int i = tid; i < SL_WAVES * 256; i += SL_THREADS) (&S.wc[0][0])[i] = 0;
+  if constexpr (AGG)
+    for (int i = tid; i < SW_LK; i += SL_THREADS) {
+      ag[i] = D.agg_s[rd][(int64_t)o * SW_LK + i];
+      ag[256 + i] = D.agg_c[rd][(int64_t)o * SW_LK + i];
+    }
   if (tid == 0) {
     S.flag = 0;
     S.done = 0;
@@ -153,9 +167,11 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   for (int x = tid; x < nc0; x += SL_THREADS) {
     const int64_t c = (int64_t)o * SWS_CCAP + x;
     const uint32_t lk = D.c_lk[rd][c];
-    S.cts[0][x] = D.c_ts[rd][c] - base;
+    const int64_t dts = D.c_ts[rd][c] - base, dsq = D.c_seq[rd][c] - sbase;
+    if (dts != (int64_t)(int32_t)dts || dsq != (int64_t)(int32_t)dsq) S.flag = 1;  // the exact kernel
+    S.cts[0][x] = (int32_t)dts;
     S.cv[0][x] = D.c_v[rd][c];
-    S.cseq[0][x] = D.c_seq[rd][c];
+    S.cseq[0][x] = (int32_t)dsq;
     S.clk[0][x] = (uint8_t)lk;
     atomicAdd(&S.ncar[lk], 1u);
     if (x == 0 || D.c_lk[rd][c - 1] != lk) S.ckf[0][lk] = (uint16_t)x;
@@ -188,7 +204,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         for (int p2 = p + 1; p2 < q - SL_NEAR; p2++) later += S.m[p2] == q ? 1u : 0u;
       }
       const uint32_t r = S.ref[p] & 0x7FFFFFFFu, rq = S.ref[q] & 0x7FFFFFFFu;
-      const int64_t si = p < (int)(S.meta[p] >> 20) ? S.cseq[pc][r] : bseq(B, r);
+      const int64_t si = p < (int)(S.meta[p] >> 20) ? sbase + S.cseq[pc][r] : bseq(B, r);
       const int64_t sq = bseq(B, rq);
       const uint64_t slot = gb + (uint32_t)S.tv[q].x + (sl_closes(c) - 1u - later);
       if (slot < (uint64_t)O.cap) {
@@ -202,6 +218,68 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
           *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
         }
       }
+    }
+  };
+  // AGG emission of the chunk a wave finished (between barriers A and B of the next chunk, like the
+  // pairs): per closing position q in key order, the key's (sum, count) before q by a segmented
+  // wave scan (segments = key runs, seeded with the key's state), then q's c matches: the r-th adds
+  // q's value once more, (S + (r+1) v) / (N + r + 1) for avg -- k_sw_solve's arithmetic.
+  auto emit_agg = [&](int PS, int PE) {
+    const unsigned long long gb = S.gbase + S.wb[w];
+    double cs = 0, cn = 0;       // the running state at the end of the previous 64-block
+    uint32_t clk = 0xFFFFFFFFu;  // ... and its key
+    for (int g0 = PS; g0 < PE; g0 += 64) {
+      const int q = g0 + (int)lane;
+      const bool v = q < PE;
+      const uint32_t lk = v ? (S.meta[q] & 0xFFu) : 0xFFFFu;
+      const uint32_t c = v ? sl_closes(S.cl[q]) : 0u;
+      const uint32_t vb = v ? (uint32_t)S.tv[q].y : 0u;
+      const double x = CT == 1 ? (double)__uint_as_float(vb) : (double)(int32_t)vb;
+      const uint32_t lkp = __shfl_up(lk, 1, 64);
+      const bool head = lane == 0 || lk != lkp;
+      double s0 = 0, n0 = 0;
+      if (head && v) {
+        if (lane == 0 && lk == clk) {
+          s0 = cs;
+          n0 = cn;
+        } else {
+          s0 = ag[lk];
+          n0 = ag[256 + lk];
+        }
+      }
+      double is = (head ? s0 : 0.0) + (double)c * x, in = (head ? n0 : 0.0) + (double)c;
+      int f = head ? 1 : 0;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const double ys = __shfl_up(is, d, 64), yn = __shfl_up(in, d, 64);
+        const int yf = __shfl_up(f, d, 64);
+        if (lane >= (uint32_t)d && !f) {
+          is += ys;
+          in += yn;
+        }
+        if (lane >= (uint32_t)d) f |= yf;
+      }
+      const double ps = __shfl_up(is, 1, 64), pn = __shfl_up(in, 1, 64);
+      const double es = head ? s0 : ps, en = head ? n0 : pn;  // the key's state before q
+      if (c) {
+        const int32_t kid = D.inv[(int64_t)o * SW_LK + lk];
+        const uint64_t s0l = gb + (uint32_t)S.tv[q].x;
+        for (uint32_t r = 0; r < c; r++) {
+          const double sr = es + (double)(r + 1) * x, nr = en + (double)(r + 1);
+          const uint64_t slot = s0l + r;
+          if (slot < (uint64_t)O.cap) {
+            O.key[slot] = kid;
+            O.agg[slot] = D.agg == 1 ? sr / nr : (D.agg == 2 ? sr : nr);
+          }
+        }
+      }
+      if (v && (q + 1 >= PE || (S.meta[q + 1] & 0xFFu) != lk)) {  // the run's end: the key's new state
+        ag[lk] = is;
+        ag[256 + lk] = in;
+      }
+      cs = __shfl(is, 63, 64);
+      cn = __shfl(in, 63, 64);
+      clk = __shfl(lk, 63, 64);
     }
   };
   int pPS = 0, pPE = 0, pcur = 0;  // this wave's range of the previous chunk, and its carry buffer
@@ -246,7 +324,10 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     // flags raised by the previous chunk are read here, where no thread writes S.flag (all
     // threads take the same branch)
     if (S.flag) break;
-    if (cb != rb) emit(pPS, pPE, pcur);  // the previous chunk's matches
+    if (cb != rb) {  // the previous chunk's matches
+      if constexpr (AGG) emit_agg(pPS, pPE);
+      else emit(pPS, pPE, pcur);
+    }
     SL_STAMP(1);
     const int E = S.cn[cur] + nchunk;
     // 2. key run offsets and the wave split (one wave: the one with the least to emit, the
@@ -493,9 +574,11 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
               S.cseq[nx][x] = S.cseq[cur][r];
             } else {
               const int2 a = S.tv[q];
-              S.cts[nx][x] = (int64_t)tb32 + a.x;
+              S.cts[nx][x] = tb32 + a.x;  // |.| < 2^30 (the scatter's wide flag)
               S.cv[nx][x] = (uint32_t)a.y;
-              S.cseq[nx][x] = bseq(B, r);
+              const int64_t dsq = bseq(B, r) - sbase;
+              if (dsq != (int64_t)(int32_t)dsq) S.flag = 1;
+              S.cseq[nx][x] = (int32_t)dsq;
             }
             S.clk[nx][x] = (uint8_t)(f & 0xFFu);
           }
@@ -527,7 +610,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     if (tid == 0) atomicOr(err, SWE_LEAN);
     return;
   }
-  emit(pPS, pPE, pcur);  // the last chunk's matches
+  if constexpr (AGG) emit_agg(pPS, pPE);  // the last chunk's matches
+  else emit(pPS, pPE, pcur);
 #ifdef SHP_SW_STAMPS
   SL_STAMP(1);
   {
@@ -553,12 +637,17 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     const uint32_t lk = S.clk[cur][x];
     const int64_t c = (int64_t)o * SWS_CCAP + S.binoff[lk] + (uint32_t)x - S.ckf[cur][lk];
     D.c_ts[wr][c] = base + S.cts[cur][x];
-    D.c_seq[wr][c] = S.cseq[cur][x];
+    D.c_seq[wr][c] = sbase + S.cseq[cur][x];
     D.c_v[wr][c] = S.cv[cur][x];
     D.c_lk[wr][c] = (uint8_t)lk;
     D.c_null[wr][c] = 0;
   }
   for (int i = tid; i < SW_LK; i += SL_THREADS) D.lastc[wr][(int64_t)o * SW_LK + i] = S.lastc[i];
+  if constexpr (AGG)  // every wave's last emission is behind the block scan's barriers above
+    for (int i = tid; i < SW_LK; i += SL_THREADS) {
+      D.agg_s[wr][(int64_t)o * SW_LK + i] = ag[i];
+      D.agg_c[wr][(int64_t)o * SW_LK + i] = ag[256 + i];
+    }
   if (tid == 0) D.c_n[wr][o] = ncf;
   if (e) atomicOr(err, e);
 }

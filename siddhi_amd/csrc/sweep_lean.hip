@@ -5,6 +5,20 @@
 
 namespace shp {
 
+#ifdef SW_LEAN_AGG  // the SHP_LAYOUT_AGG instantiations, a unit of their own (build.py)
+void sw_launch_lean_agg(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                        const MatchOut& O, int* err) {
+#define SA_CASE(c, p) \
+  case c * 8 + p: k_sw_lean<c, p, true><<<grid, SL_THREADS, 0, s>>>(D, B, O, err); break;
+  switch (ct * 8 + opc) {
+    SA_CASE(1, 1) SA_CASE(1, 2) SA_CASE(1, 3) SA_CASE(1, 4) SA_CASE(1, 5) SA_CASE(1, 6)
+    SA_CASE(2, 1) SA_CASE(2, 2) SA_CASE(2, 3) SA_CASE(2, 4) SA_CASE(2, 5) SA_CASE(2, 6)
+    default: break;
+  }
+#undef SA_CASE
+}
+#else
+
 void sw_launch_solve_nt1_0(int, int, unsigned, hipStream_t, const SweepDev&, const BatchView&, const MatchOut&, int*);
 void sw_launch_solve_nt1_1(int, int, unsigned, hipStream_t, const SweepDev&, const BatchView&, const MatchOut&, int*);
 void sw_launch_solve_nt1_2(int, int, unsigned, hipStream_t, const SweepDev&, const BatchView&, const MatchOut&, int*);
@@ -50,5 +64,7 @@ void sw_launch_spill(int nt2, int ct, unsigned grid, hipStream_t s, const SweepD
     default: break;
   }
 }
+
+#endif  // SW_LEAN_AGG
 
 }  // namespace shp

@@ -97,7 +97,7 @@ def test_spilled_owner_snapshot_restore():
     ts, key, v = _falling_stream(200, 30_000, 3, hot=(11,), fall=5000)
     cut = 3000 + 4000  # inside the falling run: the open list is in the pool
     eng = _eng(cq, 200, 1 << 15, max_matches=1 << 18)
-    _push_all(eng, ts[:cut], key[:cut], v[:cut], 2_500)
+    first = _push_all(eng, ts[:cut], key[:cut], v[:cut], 2_500)
     assert eng.stat("spilled_owners") >= 1
     blob = eng.snapshot()
     d = eng.describe(blob)
@@ -106,7 +106,6 @@ def test_spilled_owner_snapshot_restore():
     fresh = _eng(cq, 200, 1 << 15, max_matches=1 << 18)
     fresh.restore(blob)
     want = _push_all(OracleEngine(cq.program_json(), 0), ts, key, v, 2_500)
-    first = per_key(eng.fetch())
     rest = _push_all(fresh, ts[cut:], key[cut:], v[cut:], 2_500)
     got = {}
     for part in (first, rest):
