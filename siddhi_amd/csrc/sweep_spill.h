@@ -113,7 +113,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_sw_spill(SweepDev D, BatchView B
   }
   __syncthreads();
   // 2. replay, one thread per local key
-  uint32_t nopen = 0;
+  uint32_t nopen = 0, nlist = 0;  // this key's open candidates, and its list's length
   int64_t lbase = 0;
   if (tid < (uint32_t)SW_LK) {
     const uint32_t k = tid;
@@ -243,6 +243,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_sw_spill(SweepDev D, BatchView B
     }
     D.lastc[wr][(int64_t)o * SW_LK + k] = lastc;
     for (uint32_t p = 0; p < nl; p++) nopen += (L_st[p] & 1u) ? 1u : 0u;
+    nlist = nl;
   }
   // 3. the carry out, key order: a block scan of the open counts
   uint32_t x = nopen;
@@ -266,7 +267,8 @@ __global__ __launch_bounds__(SP_THREADS) void k_sw_spill(SweepDev D, BatchView B
     const int64_t* L_seq = D.s_seq + lbase;
     const uint32_t* L_v = D.s_v + lbase;
     const uint8_t* L_st = D.s_st + lbase;
-    const uint32_t nl = ncar[tid] + nrec[tid];
+    // the list as the replay left it: entries past nlist were never written (scratch garbage)
+    const uint32_t nl = nlist;
     int64_t c = back ? (int64_t)o * SWS_CCAP + pre : D.sp_base[wr][o] + pre;
     int64_t* o_ts = back ? D.c_ts[wr] : D.p_ts[wr];
     int64_t* o_seq = back ? D.c_seq[wr] : D.p_seq[wr];

@@ -101,8 +101,8 @@ def test_spilled_owner_snapshot_restore():
     assert eng.stat("spilled_owners") >= 1
     blob = eng.snapshot()
     d = eng.describe(blob)
-    e1 = d["keys"]["11"]["e1"]
-    opens = len(e1["PendingStateEventList"]) + len(e1["NewAndEveryStateEventList"])
+    e2 = d["keys"]["11"]["e2"]  # e1-filled partials wait at e2's pre-processor
+    opens = len(e2["PendingStateEventList"]) + len(e2["NewAndEveryStateEventList"])
     fresh = _eng(cq, 200, 1 << 15, max_matches=1 << 18)
     fresh.restore(blob)
     want = _push_all(OracleEngine(cq.program_json(), 0), ts, key, v, 2_500)
