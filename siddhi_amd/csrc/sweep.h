@@ -1497,7 +1497,6 @@ static __global__ void k_sw_init(SweepDev D) {
 }  // namespace shp
 
 #include "sweep_lean.h"
-#include "sweep_bal.h"
 #include "sweep_spill.h"
 
 // ------------------------------------------------------------------ host side
@@ -1507,7 +1506,7 @@ namespace shp {
 // once per NT1, and sweep_lean.hip), so the library's units build in parallel.
 void sw_launch_solve(int nt1, int nt2, int ct, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                      const MatchOut& O, int* err);
-void sw_launch_lean(bool bal, int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+void sw_launch_lean(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                     const MatchOut& O, int* err);
 void sw_launch_lean_agg(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                         const MatchOut& O, int* err);
@@ -1843,9 +1842,8 @@ struct SweepState {
   bool lean_push_for(const BatchView& B) const { return lean_push() && !B.nulls[0]; }
 
   void launch_lean(const BatchView& B, const MatchOut& O, int* err, hipStream_t s) {
-    static const int bal = getenv("SHP_SW_BAL") ? atoi(getenv("SHP_SW_BAL")) : 0;  // A/B: k_sw_bal
     if (D.agg) sw_launch_lean_agg(ct, lean_opc, (unsigned)D.nown, s, D, B, O, err);
-    else sw_launch_lean(bal != 0, ct, lean_opc, (unsigned)D.nown, s, D, B, O, err);
+    else sw_launch_lean(ct, lean_opc, (unsigned)D.nown, s, D, B, O, err);
   }
 
   // the exact solve (k_sw_solve) over the partition the scatter left; also the re-run of a push

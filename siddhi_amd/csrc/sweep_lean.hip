@@ -1,4 +1,4 @@
-// siddhi-hip: the instantiations of k_sw_lean / k_sw_bal (the headline shape's solves) and
+// siddhi-hip: the instantiations of k_sw_lean (the headline shape's solve) and
 // k_sw_spill (spilled owners), and the dispatcher of k_sw_solve's units (sweep_solve.hip), in a
 // unit of their own so the library's units build in parallel.
 #include "sweep.h"
@@ -30,19 +30,8 @@ void sw_launch_solve(int nt1, int nt2, int ct, unsigned grid, hipStream_t s, con
   else if (nt1 == 2) sw_launch_solve_nt1_2(nt2, ct, grid, s, D, B, O, err);
 }
 
-void sw_launch_lean(bool bal, int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+void sw_launch_lean(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                     const MatchOut& O, int* err) {
-  if (bal) {
-#define SB_CASE(c, p) \
-  case c * 8 + p: k_sw_bal<c, p><<<grid, SL_THREADS, 0, s>>>(D, B, O, err); break;
-    switch (ct * 8 + opc) {
-      SB_CASE(1, 1) SB_CASE(1, 2) SB_CASE(1, 3) SB_CASE(1, 4) SB_CASE(1, 5) SB_CASE(1, 6)
-      SB_CASE(2, 1) SB_CASE(2, 2) SB_CASE(2, 3) SB_CASE(2, 4) SB_CASE(2, 5) SB_CASE(2, 6)
-      default: break;
-    }
-#undef SB_CASE
-    return;
-  }
 #define SL_CASE(c, p) \
   case c * 8 + p: k_sw_lean<c, p><<<grid, SL_THREADS, 0, s>>>(D, B, O, err); break;
   switch (ct * 8 + opc) {

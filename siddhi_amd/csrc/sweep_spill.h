@@ -2,7 +2,7 @@
 //
 // The reference keeps every pending partial of a state in an unbounded LinkedList
 // (StreamPreStateProcessor.java:437-438): one key whose price falls for a whole `within` window at
-// 1 event/ms holds ~1000 open e1 candidates.  The LDS solves (k_sw_lean / k_sw_bal / k_sw_solve)
+// 1 event/ms holds ~1000 open e1 candidates.  The LDS solves (k_sw_lean / k_sw_solve)
 // carry at most SWS_CCAP = 512 open candidates per owner.  An owner whose carry would outgrow that
 // is "spilled": from then on it is solved by this kernel, with its open candidates in HBM, until
 // its carry falls back to SWS_CCAP / 2 (hysteresis), when it returns to the LDS solves.
