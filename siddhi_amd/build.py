@@ -43,22 +43,30 @@ def _stale(lib: str = LIB) -> bool:
 STAMPS_LIB = os.path.join(HERE, "libsiddhi_hip_stamps.so")
 
 
-def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
-    """stamps=True builds the diagnostic variant (in-kernel phase stamps, tools/sweep_probe.py)."""
+def build(force: bool = False, verbose: bool = False, stamps: bool = False, src: str = None, out: str = None,
+          extra=None) -> str:
+    """stamps=True builds the diagnostic variant (in-kernel phase stamps, tools/sweep_probe.py).
+    src / out / extra: an A/B variant -- sources from another tree (tools/build_variant.sh), the
+    library name under siddhi_amd/, extra compiler flags (objects in their own directory)."""
     lib = STAMPS_LIB if stamps else LIB
+    if out:
+        lib = os.path.join(HERE, out)
+        force = True
     if not force and not _stale(lib):
         return lib
+    csrc = os.path.join(src, "siddhi_amd", "csrc") if src else SRC
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"]
     if stamps:
         flags.append("-DSHP_SW_STAMPS")
-    odir = OBJ + ("_stamps" if stamps else "")
+    flags += list(extra or [])
+    odir = OBJ + ("_stamps" if stamps else "") + ("_" + os.path.splitext(out)[0] if out else "")
     os.makedirs(odir, exist_ok=True)
     ht = _hdr_time()
 
     def obj(u) -> str:
         name, file, extra = u
-        src = os.path.join(SRC, file)
+        src = os.path.join(csrc, file)
         o = os.path.join(odir, name + ".o")
         if force or not os.path.exists(o) or os.path.getmtime(o) < max(ht, os.path.getmtime(src)):
             cmd = [hipcc] + flags + extra + ["-c", "-o", o + ".tmp", src]
@@ -79,4 +87,11 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, stamps="--stamps" in sys.argv))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--src", help="tree holding siddhi_amd/csrc (an A/B variant)")
+    ap.add_argument("--out", help="variant library name under siddhi_amd/")
+    a, extra = ap.parse_known_args()
+    print(build(force=a.force, verbose=True, stamps=a.stamps, src=a.src, out=a.out, extra=extra))

@@ -45,7 +45,7 @@
 
 namespace {
 
-constexpr int GS_THREADS = 256;
+constexpr int GS_THREADS = 512;  // split workgroup: 8 waves
 constexpr int GS_TILE = 65536;  // events per split workgroup
 constexpr int GS_MAXG = 16;
 constexpr int GS_MAXCOL = 20;
@@ -115,9 +115,10 @@ __global__ __launch_bounds__(1024) void k_gs_scan(const uint32_t* cnt, uint32_t*
 }
 
 // stable split: per tile, rounds of 64 * SUB events per wave ranked by destination with wave
-// ballots; per-wave running cursors.  Columns are written at their destination-grouped slot.
-// Derived columns: key -> key / G; gclk -> max(seed, running max of ts) (the global clock);
-// gseq -> seq_base + index.
+// ballots; per-wave running cursors.  Columns are written at their destination-grouped slot, one
+// column at a time with the round's SUB loads of a lane issued before its SUB stores (a load ->
+// store chain per element leaves one load in flight per lane).  Derived columns: key -> key / G;
+// gclk -> max(seed, running max of ts) (the global clock); gseq -> seq_base + index.
 template <int SUB>
 __global__ __launch_bounds__(GS_THREADS) void k_gs_scatter(const int32_t* __restrict__ key,
                                                            const int32_t* __restrict__ stream,
@@ -138,12 +139,16 @@ __global__ __launch_bounds__(GS_THREADS) void k_gs_scatter(const int32_t* __rest
   for (int64_t r0 = lo; r0 < hi; r0 += ROUND) {
     if (threadIdx.x < NW * GS_MAXG) (&wc[0][0])[threadIdx.x] = 0;
     __syncthreads();
-    uint32_t dst[SUB], rk[SUB];
+    uint32_t dst[SUB], rk[SUB], kq[SUB];
 #pragma unroll
     for (int s = 0; s < SUB; s++) {
       const int64_t i = r0 + (int64_t)w * (64 * SUB) + s * 64 + lane;
       dst[s] = GS_MAXG;
-      if (i < hi && !(stream && stream[i] < 0)) dst[s] = (uint32_t)key[i] % (uint32_t)G;
+      kq[s] = 0;
+      if (i < hi && !(stream && stream[i] < 0)) {
+        kq[s] = (uint32_t)key[i];
+        dst[s] = kq[s] % (uint32_t)G;
+      }
     }
 #pragma unroll
     for (int s = 0; s < SUB; s++) {
@@ -159,32 +164,64 @@ __global__ __launch_bounds__(GS_THREADS) void k_gs_scatter(const int32_t* __rest
       if (valid && (peers & lt) == 0) wc[w][dst[s]] = before + (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {  // wave cursors: destinations x waves, in order
-      for (int d = 0; d < G; d++) {
-        uint32_t g = run[d];
-        for (int ww = 0; ww < NW; ww++) {
-          const uint32_t c = wc[ww][d];
-          wc[ww][d] = g;
-          g += c;
-        }
-        run[d] = g;
+    if (threadIdx.x < (unsigned)G) {  // wave cursors of destination d: its run, then the waves in order
+      const int d = (int)threadIdx.x;
+      uint32_t g = run[d];
+#pragma unroll
+      for (int ww = 0; ww < NW; ww++) {
+        const uint32_t c = wc[ww][d];
+        wc[ww][d] = g;
+        g += c;
       }
+      run[d] = g;
     }
     __syncthreads();
+    uint32_t o[SUB];
 #pragma unroll
-    for (int s = 0; s < SUB; s++) {
-      if (dst[s] >= GS_MAXG) continue;
-      const int64_t i = r0 + (int64_t)w * (64 * SUB) + s * 64 + lane;
-      const uint32_t o = wc[w][dst[s]] + rk[s];
-      okey[o] = (int32_t)((uint32_t)key[i] / (uint32_t)G);
-      for (int c = 0; c < cols.n; c++) {
-        if (cols.sz[c] == 8) ((int64_t*)cols.out[c])[o] = ((const int64_t*)cols.in[c])[i];
-        else if (cols.sz[c] == 4) ((int32_t*)cols.out[c])[o] = ((const int32_t*)cols.in[c])[i];
-        else ((uint8_t*)cols.out[c])[o] = ((const uint8_t*)cols.in[c])[i];  // null bytes
+    for (int s = 0; s < SUB; s++) o[s] = dst[s] < GS_MAXG ? wc[w][dst[s]] + rk[s] : 0u;
+    const int64_t i0 = r0 + (int64_t)w * (64 * SUB) + lane;
+#pragma unroll
+    for (int s = 0; s < SUB; s++)
+      if (dst[s] < GS_MAXG) okey[o[s]] = (int32_t)(kq[s] / (uint32_t)G);
+    for (int c = 0; c < cols.n; c++) {
+      if (cols.sz[c] == 8) {
+        const int64_t* in = (const int64_t*)cols.in[c];
+        int64_t v[SUB];
+#pragma unroll
+        for (int s = 0; s < SUB; s++) v[s] = dst[s] < GS_MAXG ? in[i0 + s * 64] : 0;
+#pragma unroll
+        for (int s = 0; s < SUB; s++)
+          if (dst[s] < GS_MAXG) ((int64_t*)cols.out[c])[o[s]] = v[s];
+      } else if (cols.sz[c] == 4) {
+        const int32_t* in = (const int32_t*)cols.in[c];
+        int32_t v[SUB];
+#pragma unroll
+        for (int s = 0; s < SUB; s++) v[s] = dst[s] < GS_MAXG ? in[i0 + s * 64] : 0;
+#pragma unroll
+        for (int s = 0; s < SUB; s++)
+          if (dst[s] < GS_MAXG) ((int32_t*)cols.out[c])[o[s]] = v[s];
+      } else {  // null bytes
+        const uint8_t* in = (const uint8_t*)cols.in[c];
+        uint8_t v[SUB];
+#pragma unroll
+        for (int s = 0; s < SUB; s++) v[s] = dst[s] < GS_MAXG ? in[i0 + s * 64] : 0;
+#pragma unroll
+        for (int s = 0; s < SUB; s++)
+          if (dst[s] < GS_MAXG) ((uint8_t*)cols.out[c])[o[s]] = v[s];
       }
-      if (oclk) oclk[o] = max(seed, rmax[i]);
-      if (oseq) oseq[o] = seq_base + i;
     }
+    if (oclk) {
+      int64_t v[SUB];
+#pragma unroll
+      for (int s = 0; s < SUB; s++) v[s] = dst[s] < GS_MAXG ? rmax[i0 + s * 64] : 0;
+#pragma unroll
+      for (int s = 0; s < SUB; s++)
+        if (dst[s] < GS_MAXG) oclk[o[s]] = max(seed, v[s]);
+    }
+    if (oseq)
+#pragma unroll
+      for (int s = 0; s < SUB; s++)
+        if (dst[s] < GS_MAXG) oseq[o[s]] = seq_base + i0 + s * 64;
     __syncthreads();
   }
 }
