@@ -15,8 +15,18 @@
 // those processors (oracle/oracle.cpp): tests/test_cseq.py runs both on random streams for every
 // M in 1..8 and every comparison, with NaN and null values, whole and split batches.
 //
-// Kernels: the batch is partitioned by key with the engine's stable radix sort (as for the
-// general lanes); k_cseq runs one thread per key over the key's events in arrival order, with
+// Kernels (round 3, the default): k_cs_pack packs each event into a 16-byte record (ts, value,
+// batch index | null) and rocPRIM's stable radix sort moves the records with their keys, so every
+// later read is coalesced; k_cs2 then runs the automaton data-parallel over the key-sorted records:
+// per event the transition is a function on L in 0..M (a table of M+1 nibbles: f1(x) = 0 -> 0;
+// f1(x) and f2 -> T11; f1(x) alone -> T10), and L before each event is a segmented wave scan of
+// their composition, seeded at each key's run start with the stored L (every prefix is then a
+// constant).  One wave per key-aligned range of ~CS2_P events: a count pass, a scan over the waves,
+// an emit pass writing each wave's records contiguously (per key in emission order).
+//
+// Kernels (round 2, kept as the reference form of the rule): the batch is partitioned by key with the
+// engine's stable radix sort (as for the general lanes); k_cseq runs one thread per key over the key's
+// events in arrival order, with
 // the automaton, the previous value and the last M events' (seq, ts) in registers.  It runs
 // twice: the first pass counts each key's records and refs, an exclusive scan over the keys
 // places them, the second pass writes them (per key contiguous, in emission order) and the
@@ -28,13 +38,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <stdexcept>
+
+#include <rocprim/rocprim.hpp>
 
 #include "nfa_lane.h"
 #include "prog.h"
 #include "sweep.h"
 
 namespace shp {
+
+// one event of the round-3 form: packed in arrival order, sorted with its key
+struct __attribute__((aligned(16))) CsRec {
+  int64_t ts;
+  uint32_t v;
+  uint32_t g;  // batch index | null << 31
+};
 
 struct CseqDev {
   SwPred f1, f2;     // f1: e1 slot = the arriving event; f2: e1 slot = e1[last], e2 slot = the arriving event
@@ -47,7 +67,289 @@ struct CseqDev {
   unsigned long long* tsmax;  // max ts of the push as ts ^ 2^63 (0: no event)
   uint32_t *cm, *cr;  // nk: records and refs per key (pass 1), then their exclusive scans
   uint32_t *om, *orf;
+  // round-3 form: the packed records, sorted with their keys; per wave range starts, counts, offsets
+  uint32_t *pk, *sk;
+  CsRec *pr, *sr;
+  int64_t* ws;
+  uint32_t *wcm, *wcr, *wom, *wor;
 };
+
+// ---- round-3 data-parallel form (see the header)
+constexpr int CS2_P = 1024;  // nominal events per wave range (ranges start at key runs)
+
+// pack: the sort key (key id; `nokey` for clock-only events and keys out of range) and the record,
+// plus the push's max ts
+static __global__ void k_cs_pack(const int64_t* __restrict__ ts, const int32_t* __restrict__ key,
+                                 const int32_t* __restrict__ stream, const uint32_t* __restrict__ vcol,
+                                 const uint8_t* __restrict__ ncol, int64_t n, int partitioned, uint32_t nokey,
+                                 uint32_t* __restrict__ okey, CsRec* __restrict__ orec, unsigned long long* tsmax,
+                                 int* err) {
+  int e = 0;
+  int64_t mx = INT64_MIN;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t k = 0;
+    const int64_t t = ts[i];
+    if (stream[i] < 0) {
+      k = nokey;
+    } else {
+      mx = max(mx, t);
+      if (partitioned) {
+        const int32_t x = key[i];
+        if (x < 0 || (uint32_t)x >= nokey) {
+          e = 1 << 20;
+          k = nokey;
+        } else {
+          k = (uint32_t)x;
+        }
+      }
+    }
+    okey[i] = k;
+    CsRec r;
+    r.ts = t;
+    r.v = vcol ? vcol[i] : 0u;
+    r.g = (uint32_t)i | ((ncol && ncol[i]) ? 0x80000000u : 0u);
+    orec[i] = r;
+  }
+  for (int d = 32; d > 0; d >>= 1) mx = max(mx, (int64_t)__shfl_xor((long long)mx, d, 64));
+  if (__lane_id() == 0 && mx != INT64_MIN) atomicMax(tsmax, (unsigned long long)mx ^ (1ull << 63));
+  if (e) atomicOr(err, e);
+}
+
+// transition tables: entry i (4 bits at 4 i) = L after the event from L = i
+__device__ __forceinline__ uint64_t cs_tab_const(uint32_t c) { return 0x111111111ull * (uint64_t)c; }
+__device__ __forceinline__ uint32_t cs_at(uint64_t f, uint32_t i) { return (uint32_t)(f >> (4 * i)) & 15u; }
+__device__ __forceinline__ uint64_t cs_comp(uint64_t g, uint64_t f) {  // g after f
+  uint64_t h = 0;
+#pragma unroll
+  for (int i = 0; i <= CSEQ_MAXM; i++) h |= (uint64_t)cs_at(g, cs_at(f, i)) << (4 * i);
+  return h;
+}
+// T10: f1(x) without f2: 0 -> 1, L -> L + 1 (0 < L < M), M -> 1; T11: f1(x) and f2: 0 -> 1, M -> 1, else 0
+__device__ __forceinline__ void cs_tables(int M, uint64_t& t10, uint64_t& t11) {
+  t10 = 1ull | (1ull << (4 * M));
+  t11 = 1ull | (1ull << (4 * M));
+  for (int i = 1; i < M; i++) t10 |= (uint64_t)(i + 1) << (4 * i);
+}
+
+// the first key-run start at or after position j of the sorted keys (n if none): a 64-ary search
+// by the whole wave (every lane gets the result)
+__device__ __forceinline__ int64_t cs_run_start(const uint32_t* __restrict__ sk, int64_t n, int64_t j) {
+  if (j <= 0) return 0;
+  if (j >= n) return n;
+  const uint32_t k = sk[j];
+  if (sk[j - 1] != k) return j;
+  const uint32_t lane = __lane_id();
+  // gallop: [lo, hi) with sk[lo] == k and sk[hi] != k (or hi == n)
+  int64_t lo = j, hi = -1, stride = 1;
+  while (hi < 0) {
+    const int64_t p = lo + (int64_t)(lane + 1) * stride;
+    const bool past = p >= n || sk[p] != k;
+    const uint64_t m = __ballot(past);
+    if (m) {
+      const int f = __ffsll((unsigned long long)m) - 1;
+      hi = min(n, lo + (int64_t)(f + 1) * stride);
+      lo = lo + (int64_t)f * stride;
+    } else {
+      lo += 64 * stride;
+      stride *= 64;
+    }
+  }
+  while (hi - lo > 1) {  // refine: 64 probes per round
+    const int64_t st = (hi - lo + 63) / 64;
+    const int64_t p = lo + (int64_t)(lane + 1) * st;
+    const bool past = p >= hi || sk[p] != k;
+    const uint64_t m = __ballot(past);
+    const int f = __ffsll((unsigned long long)m) - 1;  // m != 0: lane 63 probes >= hi
+    const int64_t nh = min(hi, lo + (int64_t)(f + 1) * st);
+    lo = lo + (int64_t)f * st;
+    hi = nh;
+  }
+  return hi;
+}
+
+// per wave: its range start (ws[w], the count pass) -- the count and emit passes share them
+static __global__ void k_cs2_ranges(const uint32_t* __restrict__ sk, int64_t n, int64_t nw, int64_t* ws) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (w > nw) return;
+  const int64_t s = cs_run_start(sk, n, w * (int64_t)CS2_P);
+  if (__lane_id() == 0) ws[w] = s;
+}
+
+template <int NT1, int NT2, bool EMIT>
+__global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O, const uint32_t* __restrict__ sk,
+                                             const CsRec* __restrict__ sv, const int64_t* __restrict__ ws, int64_t nw,
+                                             int* err) {
+  const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (wv >= nw) return;  // whole waves
+  const uint32_t lane = __lane_id();
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int rd = C.cur, wr = C.cur ^ 1;
+  const int M = C.M;
+  const uint32_t nk = (uint32_t)C.nk;
+  const int64_t S = ws[wv], E = ws[wv + 1];
+  const bool vnull = C.vtag == T_NULL, vflt = C.vtag == T_FLOAT;
+  uint64_t t10, t11;
+  cs_tables(M, t10, t11);
+  // carried from the previous 64 events (lane 63's): L after it, its value, its run's start
+  uint32_t cL = 0, cpv = 0;
+  bool cpn = true;
+  int64_t crs = S;
+  uint32_t nm = 0, nr = 0;
+  int64_t mo = 0, ro = 0;  // EMIT: the wave's next record / ref slot
+  if (EMIT) {
+    mo = C.wom[wv];
+    ro = C.wor[wv];
+    if (wv == nw - 1 && lane == 0) {  // the push's totals
+      O.count[0] = (unsigned long long)(mo + C.wcm[wv]);
+      O.count[1] = (unsigned long long)(ro + C.wcr[wv]);
+    }
+  }
+  int e = 0;
+  for (int64_t p0 = S; p0 < E; p0 += 64) {
+    const int64_t j = p0 + lane;
+    const uint32_t k = j < E ? sk[j] : 0xFFFFFFFFu;
+    const bool v = j < E && k < nk;  // clock-only events sort last (nokey) and are skipped
+    const uint32_t kprev = (j > S && j < E) ? sk[j - 1] : 0xFFFFFFFEu;
+    const bool head = v && (j == S || kprev != k);
+    CsRec r{};
+    if (v) r = sv[j];
+    const uint32_t x = r.v;
+    const bool xn = vnull || (r.g >> 31) != 0;
+    uint32_t L0 = 0, spv = 0;
+    bool spn = true;
+    if (head) {  // the key's stored state (the previous push)
+      L0 = C.len[rd][k];
+      spv = C.prev[rd][k];
+      spn = C.pnull[rd][k] != 0;
+    }
+    // the previous event of the key: lane - 1, or (lane 0) the carried one, or (a run start) stored
+    uint32_t pv = __shfl_up(x, 1, 64);
+    bool pn = __shfl_up((int)xn, 1, 64) != 0;
+    if (lane == 0) {
+      pv = cpv;
+      pn = cpn;
+    }
+    if (head) {
+      pv = spv;
+      pn = spn;
+    }
+    double xf, xi, pf, pi;
+    sw_conv(x, vflt, xf, xi);
+    sw_conv(pv, vflt, pf, pi);
+    const bool a = v && sw_pred<NT1>(C.f1, xf, xi, xn, 0.0, 0.0, true);
+    const bool b = v && sw_pred<NT2>(C.f2, pf, pi, pn, xf, xi, xn);
+    const uint64_t F = a ? (b ? t11 : t10) : 0ull;
+    // seeded elements: a run start composes F with its stored L, lane 0 with the carried L
+    const bool seeded = head || lane == 0;
+    const uint32_t Lseed = head ? L0 : cL;
+    uint64_t val = seeded ? cs_tab_const(cs_at(F, Lseed)) : F;
+    int fl = seeded ? 1 : 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {  // segmented inclusive scan of the compositions
+      const uint64_t y = __shfl_up(val, d, 64);
+      const int yf = __shfl_up(fl, d, 64);
+      if (lane >= (uint32_t)d && !fl) val = cs_comp(val, y);
+      if (lane >= (uint32_t)d) fl |= yf;
+    }
+    const uint32_t La = cs_at(val, 0);  // L after this event (every prefix is a constant)
+    uint32_t Lb = __shfl_up(La, 1, 64);  // L before it
+    if (lane == 0) Lb = cL;
+    if (head) Lb = L0;
+    const bool em = v && Lb > 0 && b;
+    const uint32_t rfs = em ? Lb + 1u : 0u;
+    // this event's run start (for the chain refs and the history): the latest head at or before it
+    int64_t rs = head ? j : -1;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t y = __shfl_up(rs, d, 64);
+      if (lane >= (uint32_t)d && rs < 0) rs = y;
+    }
+    if (rs < 0) rs = crs;
+    if (!EMIT) {
+      nm += em ? 1u : 0u;
+      nr += rfs;
+    } else {
+      // offsets: wave exclusive scans of the records and refs
+      uint32_t xm = em ? 1u : 0u, xr = rfs;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t ym = __shfl_up(xm, d, 64), yr = __shfl_up(xr, d, 64);
+        if (lane >= (uint32_t)d) {
+          xm += ym;
+          xr += yr;
+        }
+      }
+      const int64_t mi = mo + xm - (em ? 1 : 0), ri = ro + xr - rfs;
+      if (em) {
+        if (mi >= O.cap || ri + rfs > O.refcap) {
+          e |= E_OUT;
+        } else {
+          const int64_t sg = bseq(B, r.g & 0x7FFFFFFFu);
+          O.key[mi] = B.partitioned ? (int32_t)k : 0;
+          O.ts[mi] = r.ts;  // StateEvent ts = e2's (StreamPostStateProcessor.process :64-83)
+          O.type[mi] = 0;
+          O.pos[mi] = sg;
+          O.ref_off[mi] = ri;
+          O.slot_len[mi * MAXS] = (int16_t)Lb;
+          O.slot_len[mi * MAXS + 1] = 1;
+#pragma unroll
+          for (int s = 0; s < MAXS; s++)
+            if (s >= 2) O.slot_len[mi * MAXS + s] = 0;
+          // e1's chain: the key's Lb events before this one, oldest first; then e2
+          for (uint32_t t = 1; t <= Lb; t++) {
+            const int64_t pp = j - (int64_t)t;
+            int64_t q;
+            if (pp >= rs) q = bseq(B, sv[pp].g & 0x7FFFFFFFu);
+            else q = C.hseq[rd][(int64_t)(M - (int)(rs - pp)) * C.nk + k];  // before the push
+            O.refs[ri + (Lb - t)] = q;
+          }
+          O.refs[ri + Lb] = sg;
+        }
+      }
+      mo += __shfl(xm, 63, 64);
+      ro += __shfl(xr, 63, 64);
+      // the key's state after its run in the push (the run's last event)
+      const uint32_t knext = j + 1 < E ? sk[j + 1] : 0xFFFFFFFDu;
+      if (v && knext != k) {
+        C.len[wr][k] = (uint8_t)La;
+        C.prev[wr][k] = x;
+        C.pnull[wr][k] = xn ? 1 : 0;
+        for (int s2 = 0; s2 < M; s2++) {  // slot M-1 = this event, M-2 the one before, ...
+          const int64_t pp = j - (int64_t)(M - 1 - s2);
+          int64_t hs, ht;
+          if (pp >= rs) {
+            const CsRec q = pp == j ? r : sv[pp];
+            hs = bseq(B, q.g & 0x7FFFFFFFu);
+            ht = q.ts;
+          } else {
+            const int64_t so = (int64_t)(M - (int)(rs - pp)) * C.nk + k;
+            hs = C.hseq[rd][so];
+            ht = C.hts[rd][so];
+          }
+          C.hseq[wr][(int64_t)s2 * C.nk + k] = hs;
+          C.hts[wr][(int64_t)s2 * C.nk + k] = ht;
+        }
+      }
+    }
+    cL = __shfl(La, 63, 64);
+    cpv = __shfl(x, 63, 64);
+    cpn = __shfl((int)xn, 63, 64) != 0;
+    crs = __shfl(rs, 63, 64);
+    (void)lt;
+  }
+  if (!EMIT) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      nm += __shfl_xor(nm, d, 64);
+      nr += __shfl_xor(nr, d, 64);
+    }
+    if (lane == 0) {
+      C.wcm[wv] = nm;
+      C.wcr[wv] = nr;
+    }
+  }
+  if (e) atomicOr(err, e);
+}
 
 template <int NT1, int NT2, bool EMIT>
 __global__ __launch_bounds__(256) void k_cseq(CseqDev C, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
@@ -207,7 +509,32 @@ struct CseqState {
       throw std::runtime_error("hipMalloc failed (count-sequence path)");
   }
 
-  void create(const DevProg& P, const CseqShape& s, int32_t max_keys, hipStream_t st) {
+  int64_t cap = 0;
+  void* tmp = nullptr;  // the record sort's rocPRIM scratch
+  size_t tmp_bytes = 0;
+
+  void create(const DevProg& P, const CseqShape& s, int32_t max_keys, int64_t batch_cap, int key_bits,
+              hipStream_t st) {
+    cap = std::max<int64_t>(batch_cap, 1);
+    al(D.pk, cap);
+    al(D.sk, cap);
+    al(D.pr, cap);
+    al(D.sr, cap);
+    const int64_t nwmax = cap / CS2_P + 2;
+    al(D.ws, nwmax + 1);
+    al(D.wcm, nwmax);
+    al(D.wcr, nwmax);
+    al(D.wom, nwmax);
+    al(D.wor, nwmax);
+    size_t b1 = 0, b2 = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, b1, D.pk, D.sk, D.pr, D.sr, (size_t)cap, 0, key_bits + 1, st);
+    (void)rocprim::exclusive_scan(nullptr, b2, D.wcm, D.wom, 0u, (size_t)nwmax, rocprim::plus<uint32_t>(), st);
+    tmp_bytes = std::max<size_t>(std::max(b1, b2), 16);
+    if (hipMalloc(&tmp, tmp_bytes) != hipSuccess) throw std::runtime_error("hipMalloc failed (count-sequence sort)");
+    create_state(P, s, max_keys, st);
+  }
+
+  void create_state(const DevProg& P, const CseqShape& s, int32_t max_keys, hipStream_t st) {
     D.vtag = P.ncol == 1 ? P.colTag[0] : T_NULL;
     if (!SweepState::lower(s.f1, (int8_t)D.vtag, D.f1) || !SweepState::lower(s.f2, (int8_t)D.vtag, D.f2))
       throw std::runtime_error("count-sequence: predicate not lowerable");
@@ -269,6 +596,58 @@ struct CseqState {
     kt.mark(nullptr, s);
   }
 
+  template <bool EMIT>
+  void pass2(const BatchView& B, const MatchOut& O, int64_t nw, int* err, hipStream_t s) {
+    const unsigned g = (unsigned)((nw * 64 + 255) / 256);
+    switch (D.f1.n * 3 + D.f2.n) {
+#define CS2_CASE(a, b) \
+  case a * 3 + b: k_cs2<a, b, EMIT><<<g, 256, 0, s>>>(D, B, O, D.sk, D.sr, D.ws, nw, err); break;
+      CS2_CASE(0, 0) CS2_CASE(0, 1) CS2_CASE(0, 2) CS2_CASE(1, 0) CS2_CASE(1, 1) CS2_CASE(1, 2)
+      CS2_CASE(2, 0) CS2_CASE(2, 1) CS2_CASE(2, 2)
+#undef CS2_CASE
+      default: break;
+    }
+  }
+
+  // the round-3 form over one push (device columns): pack, sort the records with their keys,
+  // wave ranges, count pass, scan over the waves, the state carried to copy wr, emit pass
+  void run2(const BatchView& B, const int32_t* key, const int32_t* stream, int key_bits, const MatchOut& O, int* err,
+            hipStream_t s, KTimer& kt) {
+    const int64_t n = B.n;
+    (void)hipMemsetAsync(D.tsmax, 0, sizeof(unsigned long long), s);
+    // the state of keys without events in this push passes to copy wr unchanged
+    const int rd = D.cur, wr = D.cur ^ 1;
+    const size_t nk = (size_t)D.nk, hm = (size_t)D.M * nk * 8;
+    (void)hipMemcpyAsync(D.len[wr], D.len[rd], nk, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(D.prev[wr], D.prev[rd], nk * 4, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(D.pnull[wr], D.pnull[rd], nk, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(D.hseq[wr], D.hseq[rd], hm, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(D.hts[wr], D.hts[rd], hm, hipMemcpyDeviceToDevice, s);
+    if (n <= 0) {
+      (void)hipMemsetAsync(O.count, 0, 2 * sizeof(unsigned long long), s);
+      return;
+    }
+    kt.mark("cs_pack", s);
+    const unsigned gp = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    k_cs_pack<<<gp, 256, 0, s>>>(B.ts, key, stream, (const uint32_t*)B.cols[0], B.nulls[0], n, B.partitioned,
+                                 (uint32_t)D.nk, D.pk, D.pr, D.tsmax, err);
+    kt.mark("cs_sort", s);
+    size_t tb = tmp_bytes;
+    (void)rocprim::radix_sort_pairs(tmp, tb, D.pk, D.sk, D.pr, D.sr, (size_t)n, 0, key_bits + 1, s);
+    kt.mark("cs_count", s);
+    const int64_t nw = (n + CS2_P - 1) / CS2_P;
+    k_cs2_ranges<<<(unsigned)(((nw + 1) * 64 + 255) / 256), 256, 0, s>>>(D.sk, n, nw, D.ws);
+    pass2<false>(B, O, nw, err, s);
+    kt.mark("cs_scan", s);
+    tb = tmp_bytes;
+    (void)rocprim::exclusive_scan(tmp, tb, D.wcm, D.wom, 0u, (size_t)nw, rocprim::plus<uint32_t>(), s);
+    tb = tmp_bytes;
+    (void)rocprim::exclusive_scan(tmp, tb, D.wcr, D.wor, 0u, (size_t)nw, rocprim::plus<uint32_t>(), s);
+    kt.mark("cs_emit", s);
+    pass2<true>(B, O, nw, err, s);
+    kt.mark(nullptr, s);
+  }
+
   void commit() { D.cur ^= 1; }
 
   void release() {
@@ -277,10 +656,11 @@ struct CseqState {
       for (void* p : ps)
         if (p) (void)hipFree(p);
     }
-    void* qs[] = {D.tsmax, D.cm, D.cr, D.om, D.orf};
+    void* qs[] = {D.tsmax, D.cm, D.cr, D.om, D.orf, D.pk, D.sk, D.pr, D.sr, D.ws, D.wcm, D.wcr, D.wom, D.wor, tmp};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = CseqDev{};
+    tmp = nullptr;
   }
 };
 

@@ -264,6 +264,7 @@ struct shp_engine {
   int64_t seq = 0;
   int64_t clock = 0;
   int key_bits = 1;
+  const bool cseq_v1 = getenv("SHP_CSEQ_V1") != nullptr;  // A/B: the round-2 count-sequence kernels
   LaneLayout Yl{};     // per-workgroup LDS layout of the lanes (lds_lanes > 0)
   int lds_lanes = 0;
   double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
@@ -429,7 +430,7 @@ struct shp_engine {
     } else if (fast == 1) {
       fs.create(comp.P, comp.fast, cfg.max_keys, cap, mcap, stream);
     } else if (fast == 3) {
-      cs.create(comp.P, comp.cseq, cfg.max_keys, stream);
+      cs.create(comp.P, comp.cseq, cfg.max_keys, cfg.max_batch, key_bits, stream);
     } else if (fast == 4) {
       la.create(comp.P, comp.labs, cfg.max_keys, mcap, cap, stream);
     } else {
@@ -505,6 +506,11 @@ struct shp_engine {
         expanded = true;
       }
       HIP_OK(hipMemcpyAsync(h_tsmax, sw.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+    } else if (fast == 3 && !cseq_v1) {  // count sequence: its own record sort (cseq.h, run2)
+      kt.mark(nullptr, stream);
+      HIP_OK(hipEventRecord(ev1, stream));
+      cs.run2(B, x_key, x_stream, key_bits, O, d_err, stream, kt);
+      HIP_OK(hipMemcpyAsync(h_tsmax, cs.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
     } else {
       int gb = (int)std::min<int64_t>((n + 255) / 256, 2048);
       if (gb < 1) gb = 1;
