@@ -89,7 +89,7 @@ static __global__ void k_cs_pack(const int64_t* __restrict__ ts, const int32_t* 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t k = 0;
     const int64_t t = ts[i];
-    if (stream[i] < 0) {
+    if (stream && stream[i] < 0) {  // (no stream column: every event on the query's stream)
       k = nokey;
     } else {
       mx = max(mx, t);
@@ -292,9 +292,6 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
           O.ref_off[mi] = ri;
           O.slot_len[mi * MAXS] = (int16_t)Lb;
           O.slot_len[mi * MAXS + 1] = 1;
-#pragma unroll
-          for (int s = 0; s < MAXS; s++)
-            if (s >= 2) O.slot_len[mi * MAXS + s] = 0;
           // e1's chain: the key's Lb events before this one, oldest first; then e2
           for (uint32_t t = 1; t <= Lb; t++) {
             const int64_t pp = j - (int64_t)t;
@@ -513,6 +510,20 @@ struct CseqState {
   void* tmp = nullptr;  // the record sort's rocPRIM scratch
   size_t tmp_bytes = 0;
 
+  // the records sorted with their keys (stable); CS_RADIX_BITS > 8: a onesweep config with that many
+  // bits per pass (fewer passes over the 20 key bits of 1M keys)
+  void sort_records(void* t, size_t& tb, int64_t n, int key_bits, hipStream_t s) {
+#if defined(CS_RADIX_BITS) && CS_RADIX_BITS != 8
+    using Cfg = rocprim::radix_sort_config<
+        rocprim::default_config, rocprim::default_config,
+        rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>,
+                                            CS_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+    (void)rocprim::radix_sort_pairs<Cfg>(t, tb, D.pk, D.sk, D.pr, D.sr, (size_t)n, 0, key_bits + 1, s);
+#else
+    (void)rocprim::radix_sort_pairs(t, tb, D.pk, D.sk, D.pr, D.sr, (size_t)n, 0, key_bits + 1, s);
+#endif
+  }
+
   void create(const DevProg& P, const CseqShape& s, int32_t max_keys, int64_t batch_cap, int key_bits,
               hipStream_t st) {
     cap = std::max<int64_t>(batch_cap, 1);
@@ -527,7 +538,7 @@ struct CseqState {
     al(D.wom, nwmax);
     al(D.wor, nwmax);
     size_t b1 = 0, b2 = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, b1, D.pk, D.sk, D.pr, D.sr, (size_t)cap, 0, key_bits + 1, st);
+    sort_records(nullptr, b1, cap, key_bits, st);
     (void)rocprim::exclusive_scan(nullptr, b2, D.wcm, D.wom, 0u, (size_t)nwmax, rocprim::plus<uint32_t>(), st);
     tmp_bytes = std::max<size_t>(std::max(b1, b2), 16);
     if (hipMalloc(&tmp, tmp_bytes) != hipSuccess) throw std::runtime_error("hipMalloc failed (count-sequence sort)");
@@ -633,7 +644,7 @@ struct CseqState {
                                  (uint32_t)D.nk, D.pk, D.pr, D.tsmax, err);
     kt.mark("cs_sort", s);
     size_t tb = tmp_bytes;
-    (void)rocprim::radix_sort_pairs(tmp, tb, D.pk, D.sk, D.pr, D.sr, (size_t)n, 0, key_bits + 1, s);
+    sort_records(tmp, tb, n, key_bits, s);
     kt.mark("cs_count", s);
     const int64_t nw = (n + CS2_P - 1) / CS2_P;
     k_cs2_ranges<<<(unsigned)(((nw + 1) * 64 + 255) / 256), 256, 0, s>>>(D.sk, n, nw, D.ws);

@@ -466,7 +466,7 @@ struct shp_engine {
     const int32_t* x_key = in ? (P.partitioned ? in->key : d_key) : d_key;
     const int32_t* x_stream = in ? in->stream : d_stream;
     if (in && !P.partitioned && fast != 2) HIP_OK(hipMemsetAsync(d_key, 0, n * 4, stream));
-    if (!x_stream && fast != 2) {  // NULL stream column: every event on stream 0
+    if (!x_stream && fast != 2 && !(fast == 3 && !cseq_v1)) {  // NULL stream column: every event on stream 0
       HIP_OK(hipMemsetAsync(d_stream, 0, n * 4, stream));
       x_stream = d_stream;
     }
