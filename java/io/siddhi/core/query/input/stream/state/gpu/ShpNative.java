@@ -107,6 +107,8 @@ final class ShpNative {
     static final MethodHandle GROUP_STAGE = fn("shp_group_stage", JAVA_INT, ADDRESS, ADDRESS);
     static final MethodHandle GROUP_RUN = fn("shp_group_run", JAVA_INT, ADDRESS, ADDRESS);
     static final MethodHandle GROUP_FETCH = fn("shp_group_fetch_matches", JAVA_INT, ADDRESS, ADDRESS);
+    // collective: every rank's matches of the last push to rank `root` (int32), moved in HBM
+    static final MethodHandle GROUP_GATHER = fn("shp_group_gather_matches", JAVA_INT, ADDRESS, JAVA_INT, ADDRESS);
     static final MethodHandle GROUP_LAST_ERROR = fn("shp_group_last_error", ADDRESS, ADDRESS);
     static final MethodHandle GROUP_DESTROY = fnVoid("shp_group_destroy", ADDRESS);
 
