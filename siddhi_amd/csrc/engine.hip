@@ -265,6 +265,7 @@ struct shp_engine {
   int64_t clock = 0;
   int key_bits = 1;
   const bool cseq_v1 = getenv("SHP_CSEQ_V1") != nullptr;  // A/B: the round-2 count-sequence kernels
+  const bool labs_v1 = getenv("SHP_LABS_V1") != nullptr;  // A/B: logical-absent batch by key sort + gather
   LaneLayout Yl{};     // per-workgroup LDS layout of the lanes (lds_lanes > 0)
   int lds_lanes = 0;
   double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
@@ -433,6 +434,7 @@ struct shp_engine {
       cs.create(comp.P, comp.cseq, cfg.max_keys, cfg.max_batch, key_bits, stream);
     } else if (fast == 4) {
       la.create(comp.P, comp.labs, cfg.max_keys, mcap, cap, stream);
+      if (!labs_v1) la.sort_scratch(cap, key_bits, stream);
     } else {
       Y.build(cfg.max_keys);
       // few keys: lanes in LDS, as many per workgroup as fit 64 KB (at most 16)
@@ -525,7 +527,11 @@ struct shp_engine {
       // 2. partition by key (stable)
       HIP_OK(hipMemsetAsync(d_kcnt, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
       const bool bounds = fast != 1;  // key runs from the sorted keys (the scan kernels keep the histogram)
-      if (!bounds) {
+      la.sorted = false;
+      if (fast == 4 && !labs_v1) {  // the logical-absent records sorted with their keys (labs.h)
+        HIP_OK(hipMemsetAsync(d_kbeg, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
+        la.sort_events(B, x_key, d_skey, d_skey2, key_bits, d_err, stream, kt);
+      } else if (!bounds) {
         kt.mark("key_hist", stream);
         k_key_hist<<<gb, 256, cfg.max_keys <= KEY_HIST_LDS ? (size_t)cfg.max_keys * 4 : 0, stream>>>(
             x_key, x_stream, n, d_kcnt, cfg.max_keys, P.partitioned, d_err);
@@ -541,11 +547,13 @@ struct shp_engine {
         k_sort_keys_chk<<<gb, 256, 0, stream>>>(x_key, x_stream, n, d_skey, P.partitioned, (uint32_t)cfg.max_keys,
                                                  d_err);
       }
-      kt.mark("iota", stream);
-      k_iota<<<gb, 256, 0, stream>>>(d_idx, n);
-      tb = tmp_bytes;
-      kt.mark("radix_sort", stream);
-      HIP_OK(rocprim::radix_sort_pairs(d_tmp, tb, d_skey, d_skey2, d_idx, d_perm, (size_t)n, 0, key_bits + 1, stream));
+      if (!la.sorted) {
+        kt.mark("iota", stream);
+        k_iota<<<gb, 256, 0, stream>>>(d_idx, n);
+        tb = tmp_bytes;
+        kt.mark("radix_sort", stream);
+        HIP_OK(rocprim::radix_sort_pairs(d_tmp, tb, d_skey, d_skey2, d_idx, d_perm, (size_t)n, 0, key_bits + 1, stream));
+      }
       if (bounds) {
         kt.mark("key_bounds", stream);
         k_key_bounds<<<(unsigned)((cfg.max_keys + 255) / 256), 256, 0, stream>>>(d_skey2, n, d_kbeg, d_kcnt,

@@ -137,6 +137,41 @@ static __global__ void k_labs_pack(LabsDev D, BatchView B, int64_t n) {
     D.p_ev[g] = x;
   }
 }
+// the same records with their sort keys (round 3): key id, or `nokey` for clock-only events and
+// keys out of range (SWE_KEYS); rocPRIM's radix sort then moves the records with the keys, so the
+// key-order batch costs one sort of 36-byte pairs instead of a key sort plus a random gather
+static __global__ void k_labs_pack2(LabsDev D, BatchView B, const int32_t* __restrict__ key, int64_t n,
+                                    uint32_t nokey, uint32_t* __restrict__ okey, int* err) {
+  int e = 0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x) {
+    const int st = B.stream ? B.stream[g] : 0;
+    const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
+    const int c = role == 0 ? D.col[0] : (role == 1 ? D.col[1] : (role == 2 ? D.col[2] : -1));
+    uint32_t k = 0;
+    if (st < 0) {
+      k = nokey;
+    } else if (B.partitioned) {
+      const int32_t x = key[g];
+      if (x < 0 || (uint32_t)x >= nokey) {
+        e = 1 << 20;
+        k = nokey;
+      } else {
+        k = (uint32_t)x;
+      }
+    }
+    okey[g] = k;
+    LaEv x;
+    x.ts = B.ts[g];
+    x.clk = B.rmax[g];
+    x.g = (uint32_t)g;
+    x.v = c >= 0 ? ((const uint32_t*)B.cols[c])[g] : 0u;
+    x.st = st;
+    x.n = c < 0 || (B.nulls[c] && B.nulls[c][g]) ? 1u : 0u;
+    D.p_ev[g] = x;
+  }
+  if (e) atomicOr(err, e);
+}
+
 // sorted position i <- the packed event perm[i]
 static __global__ void k_labs_gather(LabsDev D, const uint32_t* __restrict__ perm, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -915,6 +950,9 @@ struct LabsState {
   int tier = 0;
   bool wave_ok = false;  // k_labs_w applies: x's and y's filters read only their own event
   bool slow = false;     // this push re-runs on k_labs (k_labs_w raised LA_SLOW)
+  bool sorted = false;   // this push's key-order batch came from sort_events (no pack + gather)
+  void* stmp = nullptr;  // sort_events' rocPRIM scratch
+  size_t stmp_bytes = 0;
 
   static bool lower_term(const LaTermS& t, const LabsShape& sh, const DevProg& P, LaTermD& o) {
     static const int32_t masks[6] = {4, 6, 1, 3, 2, 13};  // gt ge lt le eq ne
@@ -1012,7 +1050,7 @@ struct LabsState {
     const bool few = D.nk <= 8192;  // a wave per key while that fills the CUs
     const unsigned gk = few ? (unsigned)D.nk : (unsigned)((D.nk + 63) / 64);
     kt.mark("labs_gather", s);
-    if (B.n > 0) {
+    if (B.n > 0 && !sorted) {  // (sort_events already left the batch in key order)
       k_labs_pack<<<2048, 256, 0, s>>>(D, B, B.n);
       k_labs_gather<<<4096, 256, 0, s>>>(D, perm, B.n);
     }
@@ -1037,6 +1075,27 @@ struct LabsState {
     kt.mark("labs_pos", s);
     k_labs_pos<<<1024, 256, 0, s>>>(D, B, O);
     kt.mark(nullptr, s);
+  }
+
+  // the push's events in key order with their sort keys (skey_out, for the key runs): k_labs_pack2,
+  // then one stable radix sort of (key, record) pairs
+  void sort_events(const BatchView& B, const int32_t* key, uint32_t* skey_in, uint32_t* skey_out, int key_bits,
+                   int* err, hipStream_t s, KTimer& kt) {
+    kt.mark("labs_pack", s);
+    if (B.n > 0) k_labs_pack2<<<2048, 256, 0, s>>>(D, B, key, B.n, (uint32_t)D.nk, skey_in, err);
+    kt.mark("labs_sort", s);
+    size_t tb = stmp_bytes;
+    if (B.n > 0)
+      (void)rocprim::radix_sort_pairs(stmp, tb, skey_in, skey_out, D.p_ev, D.s_ev, (size_t)B.n, 0, key_bits + 1, s);
+    kt.mark(nullptr, s);
+    sorted = true;
+  }
+  void sort_scratch(int64_t cap, int key_bits, hipStream_t s) {
+    size_t b = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, D.p_ev, D.s_ev,
+                                    (size_t)std::max<int64_t>(cap, 1), 0, key_bits + 1, s);
+    stmp_bytes = std::max<size_t>(b, 16);
+    if (hipMalloc(&stmp, stmp_bytes) != hipSuccess) throw std::runtime_error("hipMalloc failed (logical-absent sort)");
   }
 
   void commit() { D.cur ^= 1; }
@@ -1073,10 +1132,11 @@ struct LabsState {
       if (D.wq[c]) (void)hipFree(D.wq[c]);
     }
     if (D.wtmp) (void)hipFree(D.wtmp);
-    void* qs[] = {D.aux, D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps};
+    void* qs[] = {D.aux, D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = LabsDev{};
+    stmp = nullptr;
   }
 };
 
