@@ -528,9 +528,22 @@ struct shp_engine {
       HIP_OK(hipMemsetAsync(d_kcnt, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
       const bool bounds = fast != 1;  // key runs from the sorted keys (the scan kernels keep the histogram)
       la.sorted = false;
-      if (fast == 4 && !labs_v1) {  // the logical-absent records sorted with their keys (labs.h)
+      bool la_v1 = labs_v1;
+      if (fast == 4 && !la_v1) {  // the logical-absent records sorted with their keys (labs.h)
         HIP_OK(hipMemsetAsync(d_kbeg, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
         la.sort_events(B, x_key, d_skey, d_skey2, key_bits, d_err, stream, kt);
+        int e0 = 0;  // a push beyond the 16-byte records' ranges: the 32-byte form (pack + gather)
+        HIP_OK(hipMemcpyAsync(&e0, d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        if (e0 & LA_WIDE) {
+          const int keep = e0 & ~LA_WIDE;
+          HIP_OK(hipMemcpyAsync(d_err, &keep, sizeof(int), hipMemcpyHostToDevice, stream));
+          HIP_OK(hipStreamSynchronize(stream));
+          la.sorted = false;
+          la_v1 = true;
+        }
+      }
+      if (fast == 4 && !la_v1) {
       } else if (!bounds) {
         kt.mark("key_hist", stream);
         k_key_hist<<<gb, 256, cfg.max_keys <= KEY_HIST_LDS ? (size_t)cfg.max_keys * 4 : 0, stream>>>(

@@ -60,6 +60,16 @@ struct __attribute__((aligned(16))) LaEv {  // one event: packed (32 B, one sect
   uint32_t n;
 };
 constexpr int LA_UNORDERED = 1 << 27;  // a key's timestamps decrease (this path needs them ordered)
+constexpr int LA_WIDE = 1 << 26;       // a push's ts / clock leave base +- 2^31 ms or its batch index 2^27:
+                                        // the push re-runs with the 32-byte records (not an error)
+
+// the sorted form of LaEv (round 3): 16 bytes, so rocPRIM moves 20-byte (key, record) pairs; ts and
+// clock relative to the push's first ts, stream + 1 and the null flag above the index
+struct __attribute__((aligned(16))) LaEv16 {
+  int32_t ts, clk;
+  uint32_t gs;  // batch index (27 bits) | stream + 1 << 27 (4 bits) | null << 31
+  uint32_t v;
+};
 
 struct LaTermD {
   int32_t mask;      // outcomes that make the term true: 1 A<B, 2 A==B, 4 A>B, 8 unordered
@@ -115,9 +125,27 @@ struct LabsDev {
   // contiguously; random gathers from 16 waves were bound by address translation (5 us an event)
   LaEv* p_ev;        // the batch's events in arrival order, packed (k_labs_pack: one sector each)
   LaEv* s_ev;        // ... in key order (k_labs_gather)
+  int32_t ev16;      // this push's key-order batch is LaEv16 records in s_ev's memory (sort_events)
+  int32_t pad2;
   unsigned long long* stamps;  // diagnostic build (SHP_SW_STAMPS): k_labs_w phase cycles per key
   LaRec* rec;        // k_labs_w's records, per key region (la_region)
 };
+
+// key-order event i of the push, whichever record form the push sorted
+// (the 16-byte form's times are relative to the push's first ts, B.ts[0])
+__device__ __forceinline__ LaEv la_ev_at(const LabsDev& D, const BatchView& B, int64_t i) {
+  if (!D.ev16) return D.s_ev[i];
+  const LaEv16 r = reinterpret_cast<const LaEv16*>(D.s_ev)[i];
+  const int64_t base = B.ts[0];
+  LaEv x;
+  x.ts = base + r.ts;
+  x.clk = base + r.clk;
+  x.g = r.gs & 0x7FFFFFFu;
+  x.st = (int32_t)((r.gs >> 27) & 15u) - 1;
+  x.n = r.gs >> 31;
+  x.v = r.v;
+  return x;
+}
 
 // event g in arrival order (coalesced reads): ts, clock, batch index, the value of its stream's
 // column, stream, null -- one 32-byte record, so the key-order gather reads one sector per event
@@ -143,6 +171,7 @@ static __global__ void k_labs_pack(LabsDev D, BatchView B, int64_t n) {
 static __global__ void k_labs_pack2(LabsDev D, BatchView B, const int32_t* __restrict__ key, int64_t n,
                                     uint32_t nokey, uint32_t* __restrict__ okey, int* err) {
   int e = 0;
+  LaEv16* out = reinterpret_cast<LaEv16*>(D.p_ev);
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x) {
     const int st = B.stream ? B.stream[g] : 0;
     const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
@@ -153,21 +182,24 @@ static __global__ void k_labs_pack2(LabsDev D, BatchView B, const int32_t* __res
     } else if (B.partitioned) {
       const int32_t x = key[g];
       if (x < 0 || (uint32_t)x >= nokey) {
-        e = 1 << 20;
+        e |= 1 << 20;
         k = nokey;
       } else {
         k = (uint32_t)x;
       }
     }
     okey[g] = k;
-    LaEv x;
-    x.ts = B.ts[g];
-    x.clk = B.rmax[g];
-    x.g = (uint32_t)g;
+    const int64_t base = B.ts[0];
+    const int64_t dt = B.ts[g] - base, dc = B.rmax[g] - base;
+    if (dt != (int64_t)(int32_t)dt || dc != (int64_t)(int32_t)dc || g >= (1ll << 27) || st < -1 || st > 14)
+      e |= LA_WIDE;
+    LaEv16 x;
+    x.ts = (int32_t)dt;
+    x.clk = (int32_t)dc;
+    const bool nl = c < 0 || (B.nulls[c] && B.nulls[c][g]);
+    x.gs = ((uint32_t)g & 0x7FFFFFFu) | ((uint32_t)(st + 1) & 15u) << 27 | (nl ? 0x80000000u : 0u);
     x.v = c >= 0 ? ((const uint32_t*)B.cols[c])[g] : 0u;
-    x.st = st;
-    x.n = c < 0 || (B.nulls[c] && B.nulls[c][g]) ? 1u : 0u;
-    D.p_ev[g] = x;
+    out[g] = x;
   }
   if (e) atomicOr(err, e);
 }
@@ -385,7 +417,7 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
 #pragma unroll
     for (int q = 0; q < LA_SB; q++) {
       if (j0 + q < cnt) {
-        sb[q] = D.s_ev[(int64_t)beg + j0 + q];
+        sb[q] = la_ev_at(D, B, (int64_t)beg + j0 + q);
       }
     }
     const uint32_t nq = min((uint32_t)LA_SB, cnt - j0);
@@ -563,7 +595,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   int32_t n_st = -1;
   auto fetch = [&](uint32_t j0) {
     if (j0 + (uint32_t)lane < cnt) {
-      const LaEv x = D.s_ev[(int64_t)beg + j0 + lane];
+      const LaEv x = la_ev_at(D, B, (int64_t)beg + j0 + lane);
       n_ts = x.ts;
       n_clk = x.clk;
       n_g = x.g;
@@ -1050,6 +1082,7 @@ struct LabsState {
     const bool few = D.nk <= 8192;  // a wave per key while that fills the CUs
     const unsigned gk = few ? (unsigned)D.nk : (unsigned)((D.nk + 63) / 64);
     kt.mark("labs_gather", s);
+    if (!sorted) D.ev16 = 0;
     if (B.n > 0 && !sorted) {  // (sort_events already left the batch in key order)
       k_labs_pack<<<2048, 256, 0, s>>>(D, B, B.n);
       k_labs_gather<<<4096, 256, 0, s>>>(D, perm, B.n);
@@ -1086,14 +1119,16 @@ struct LabsState {
     kt.mark("labs_sort", s);
     size_t tb = stmp_bytes;
     if (B.n > 0)
-      (void)rocprim::radix_sort_pairs(stmp, tb, skey_in, skey_out, D.p_ev, D.s_ev, (size_t)B.n, 0, key_bits + 1, s);
+      (void)rocprim::radix_sort_pairs(stmp, tb, skey_in, skey_out, reinterpret_cast<LaEv16*>(D.p_ev),
+                                      reinterpret_cast<LaEv16*>(D.s_ev), (size_t)B.n, 0, key_bits + 1, s);
     kt.mark(nullptr, s);
     sorted = true;
+    D.ev16 = 1;
   }
   void sort_scratch(int64_t cap, int key_bits, hipStream_t s) {
     size_t b = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, D.p_ev, D.s_ev,
-                                    (size_t)std::max<int64_t>(cap, 1), 0, key_bits + 1, s);
+    (void)rocprim::radix_sort_pairs(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (LaEv16*)nullptr,
+                                    (LaEv16*)nullptr, (size_t)std::max<int64_t>(cap, 1), 0, key_bits + 1, s);
     stmp_bytes = std::max<size_t>(b, 16);
     if (hipMalloc(&stmp, stmp_bytes) != hipSuccess) throw std::runtime_error("hipMalloc failed (logical-absent sort)");
   }
