@@ -195,7 +195,11 @@ int shp_engine_path(const shp_engine* e);
  * copies within one process), and every rank's engine runs the keys it owns.  Per-key emission
  * order is the reference's (a key lives on one rank; received events keep global order).  The
  * group's cfg.max_keys is the global key count; cfg.max_batch bounds the events one rank may
- * receive per push.  Absent-state timers get the global playback clock (shp_batch.clock);
+ * receive per push.  Absent-state timers get the global playback clock (shp_batch.clock), so a
+ * timer match carries the reference's ts (the due time) and slots; its `pos` (the sequence number
+ * of the event during which it was emitted) is the owning rank's next event, not necessarily the
+ * global next event -- the one documented divergence of a sharded run from one engine (per-key
+ * record order and every other field are the reference's);
  * SHP_LAYOUT_FULL records name events by global sequence number.  Replaces, for the sharded
  * deployment, PartitionStreamReceiver.receive/send (core/partition/PartitionStreamReceiver.java:
  * 82-283) routing each event to its key's state. */

@@ -60,9 +60,12 @@ constexpr int SW_PREF_OWN = 1024;   // owner count the map stops at unless keys 
 constexpr int SW_MIN_OWN = SWS_OWN_MIN;     // owner count the map grows to while owners keep ~2 keys (fill the CUs)
 constexpr int SW_LKTAB = 65536;     // scatter LDS bound: its counters + the key -> local key table
 // partition
-constexpr int SWP_THREADS = 512;  // scatter workgroup
+#ifndef SWP_THREADS_CFG
+#define SWP_THREADS_CFG 512
+#endif
+constexpr int SWP_THREADS = SWP_THREADS_CFG;  // scatter workgroup
 constexpr int SWP_WAVES = SWP_THREADS / 64;
-constexpr int SWP_ROUND = 4096;  // events ranked per round: 8 per lane
+constexpr int SWP_ROUND = SWP_THREADS * 8;  // events ranked per round: 8 per lane
 constexpr int SWP_SEG = SWP_ROUND / SWP_WAVES;
 constexpr int SWP_SUB = SWP_SEG / 64;
 // solve
