@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--same-device", action="store_true",
                     help="N>1 rehearsal on a one-GPU box without torchrun: one process, an in-process group of "
                          "--gpus ranks all on cuda:0 (device copies stand in for RCCL)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_s3_pmc_traffic.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03_s3_pmc_traffic.json"))
     ap.add_argument("--latency-batches", type=int, default=200,
                     help="§8d latency: batches of --latency-events, push + D2H of the match payload (0: skip)")
     ap.add_argument("--latency-events", type=int, default=16_000_000)
