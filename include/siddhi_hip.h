@@ -275,7 +275,9 @@ double shp_last_kernel_ms(const shp_engine* e, const char* which);
  * k_sw_lean handed back to the exact k_sw_solve: a ts decrease within a key, a push spanning
  * more than 2^30 ms, a large carry) | "labs_fallbacks" (logical-absent pushes that k_labs_w, a
  * wave per key, handed to k_labs, a thread per key: a key with more than 64 pairs waiting at
- * once).  -1 for an unknown name. */
+ * once) | "cseq_wide_reruns" (count-sequence pushes whose ts span more than +-2^31 ms of their
+ * first ts, re-run with 16-byte records) | "spill_reruns" | "spilled_owners".  -1 for an unknown
+ * name. */
 int64_t shp_engine_stat(const shp_engine* e, const char* which);
 const char* shp_last_error(const shp_engine* e);
 void shp_engine_destroy(shp_engine* e);

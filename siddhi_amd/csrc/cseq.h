@@ -39,6 +39,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <stdexcept>
 
 #include <rocprim/rocprim.hpp>
@@ -55,6 +56,23 @@ struct __attribute__((aligned(16))) CsRec {
   uint32_t v;
   uint32_t g;  // batch index | null << 31
 };
+// the narrow form (the default): ts relative to the push's first ts (B.ts[0]), 12 bytes, so the
+// sort moves 32 instead of 40 bytes per event and pass; a push whose ts leave +-2^31 ms of that base
+// sets CS_WIDE and re-runs in the 16-byte form
+struct CsRec12 {
+  int32_t tr;
+  uint32_t v;
+  uint32_t g;
+};
+constexpr int CS_WIDE = 1 << 26;
+__device__ __forceinline__ int64_t cs_ts(const CsRec& r, int64_t) { return r.ts; }
+__device__ __forceinline__ int64_t cs_ts(const CsRec12& r, int64_t base) { return base + r.tr; }
+__device__ __forceinline__ void cs_set_ts(CsRec& r, int64_t t, int64_t, bool&) { r.ts = t; }
+__device__ __forceinline__ void cs_set_ts(CsRec12& r, int64_t t, int64_t base, bool& wide) {
+  const int64_t d = t - base;
+  wide |= d != (int64_t)(int32_t)d;
+  r.tr = (int32_t)d;
+}
 
 struct CseqDev {
   SwPred f1, f2;     // f1: e1 slot = the arriving event; f2: e1 slot = e1[last], e2 slot = the arriving event
@@ -75,17 +93,22 @@ struct CseqDev {
 };
 
 // ---- round-3 data-parallel form (see the header)
-constexpr int CS2_P = 1024;  // nominal events per wave range (ranges start at key runs)
+#ifndef CS2_P_CFG
+#define CS2_P_CFG 4096
+#endif
+constexpr int CS2_P = CS2_P_CFG;  // nominal events per wave range (ranges start at key runs)
 
 // pack: the sort key (key id; `nokey` for clock-only events and keys out of range) and the record,
 // plus the push's max ts
-static __global__ void k_cs_pack(const int64_t* __restrict__ ts, const int32_t* __restrict__ key,
-                                 const int32_t* __restrict__ stream, const uint32_t* __restrict__ vcol,
-                                 const uint8_t* __restrict__ ncol, int64_t n, int partitioned, uint32_t nokey,
-                                 uint32_t* __restrict__ okey, CsRec* __restrict__ orec, unsigned long long* tsmax,
-                                 int* err) {
+template <class R>
+__global__ void k_cs_pack(const int64_t* __restrict__ ts, const int32_t* __restrict__ key,
+                          const int32_t* __restrict__ stream, const uint32_t* __restrict__ vcol,
+                          const uint8_t* __restrict__ ncol, int64_t n, int partitioned, uint32_t nokey,
+                          uint32_t* __restrict__ okey, R* __restrict__ orec, unsigned long long* tsmax, int* err) {
   int e = 0;
   int64_t mx = INT64_MIN;
+  const int64_t base = ts[0];
+  bool wide = false;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t k = 0;
     const int64_t t = ts[i];
@@ -104,14 +127,17 @@ static __global__ void k_cs_pack(const int64_t* __restrict__ ts, const int32_t* 
       }
     }
     okey[i] = k;
-    CsRec r;
-    r.ts = t;
+    R r;
+    bool w = false;  // (clock-only events are never read back: their ts may lie anywhere)
+    cs_set_ts(r, t, base, w);
+    wide |= w && k != nokey;
     r.v = vcol ? vcol[i] : 0u;
     r.g = (uint32_t)i | ((ncol && ncol[i]) ? 0x80000000u : 0u);
     orec[i] = r;
   }
   for (int d = 32; d > 0; d >>= 1) mx = max(mx, (int64_t)__shfl_xor((long long)mx, d, 64));
   if (__lane_id() == 0 && mx != INT64_MIN) atomicMax(tsmax, (unsigned long long)mx ^ (1ull << 63));
+  if (wide) e |= CS_WIDE;
   if (e) atomicOr(err, e);
 }
 
@@ -175,9 +201,9 @@ static __global__ void k_cs2_ranges(const uint32_t* __restrict__ sk, int64_t n, 
   if (__lane_id() == 0) ws[w] = s;
 }
 
-template <int NT1, int NT2, bool EMIT>
+template <int NT1, int NT2, bool EMIT, class R>
 __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O, const uint32_t* __restrict__ sk,
-                                             const CsRec* __restrict__ sv, const int64_t* __restrict__ ws, int64_t nw,
+                                             const R* __restrict__ sv, const int64_t* __restrict__ ws, int64_t nw,
                                              int* err) {
   const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (wv >= nw) return;  // whole waves
@@ -188,6 +214,7 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
   const uint32_t nk = (uint32_t)C.nk;
   const int64_t S = ws[wv], E = ws[wv + 1];
   const bool vnull = C.vtag == T_NULL, vflt = C.vtag == T_FLOAT;
+  const int64_t tbase = B.ts[0];  // the narrow records' ts base (k_cs_pack)
   uint64_t t10, t11;
   cs_tables(M, t10, t11);
   // carried from the previous 64 events (lane 63's): L after it, its value, its run's start
@@ -211,7 +238,7 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
     const bool v = j < E && k < nk;  // clock-only events sort last (nokey) and are skipped
     const uint32_t kprev = (j > S && j < E) ? sk[j - 1] : 0xFFFFFFFEu;
     const bool head = v && (j == S || kprev != k);
-    CsRec r{};
+    R r{};
     if (v) r = sv[j];
     const uint32_t x = r.v;
     const bool xn = vnull || (r.g >> 31) != 0;
@@ -286,7 +313,7 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
         } else {
           const int64_t sg = bseq(B, r.g & 0x7FFFFFFFu);
           O.key[mi] = B.partitioned ? (int32_t)k : 0;
-          O.ts[mi] = r.ts;  // StateEvent ts = e2's (StreamPostStateProcessor.process :64-83)
+          O.ts[mi] = cs_ts(r, tbase);  // StateEvent ts = e2's (StreamPostStateProcessor.process :64-83)
           O.type[mi] = 0;
           O.pos[mi] = sg;
           O.ref_off[mi] = ri;
@@ -315,9 +342,9 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
           const int64_t pp = j - (int64_t)(M - 1 - s2);
           int64_t hs, ht;
           if (pp >= rs) {
-            const CsRec q = pp == j ? r : sv[pp];
+            const R q = pp == j ? r : sv[pp];
             hs = bseq(B, q.g & 0x7FFFFFFFu);
-            ht = q.ts;
+            ht = cs_ts(q, tbase);
           } else {
             const int64_t so = (int64_t)(M - (int)(rs - pp)) * C.nk + k;
             hs = C.hseq[rd][so];
@@ -333,6 +360,273 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
     cpn = __shfl((int)xn, 63, 64) != 0;
     crs = __shfl(rs, 63, 64);
     (void)lt;
+  }
+  if (!EMIT) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      nm += __shfl_xor(nm, d, 64);
+      nr += __shfl_xor(nr, d, 64);
+    }
+    if (lane == 0) {
+      C.wcm[wv] = nm;
+      C.wcr[wv] = nr;
+    }
+  }
+  if (e) atomicOr(err, e);
+}
+
+// The lane-sequential form (the default; k_cs2 kept for A/B, SHP_CSEQ_SCAN64): a wave's range is
+// walked in tiles of 64 x CS3_Q sorted positions, each lane a contiguous CS3_Q of them.  A lane
+// composes its events' transitions itself (seeded at a run start with the stored L), so the wave
+// scans once per tile instead of once per 64 events: one segmented scan of the lanes' compositions
+// (lane 0 seeded with the carried L, so every prefix is a constant), one max-scan of the latest run
+// start, and (emit) one scan of the lanes' record / ref counts.  Then each lane re-walks its events
+// with a concrete L: the same rule as k_cs2, event for event.
+#ifndef CS3_QC_CFG
+#define CS3_QC_CFG 4
+#endif
+#ifndef CS3_QE_CFG
+#define CS3_QE_CFG 2
+#endif
+constexpr int CS3_QC = CS3_QC_CFG;  // events per lane per tile, count pass
+constexpr int CS3_QE = CS3_QE_CFG;  // ... emit pass (measured: 4 and 2 fastest, 8 / 16 slower)
+
+template <int NT1, int NT2, bool EMIT, class R, int CS3_Q = EMIT ? CS3_QE : CS3_QC>
+__global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O, const uint32_t* __restrict__ sk,
+                                             const R* __restrict__ sv, const int64_t* __restrict__ ws, int64_t nw,
+                                             int* err) {
+  static_assert(CS3_Q == 1 || CS3_Q == 2 || CS3_Q == 4 || CS3_Q == 8 || CS3_Q == 16,
+                "a lane's events: 4 flag fields of CS3_Q bits in one word");
+  using Cs3W = typename std::conditional<(CS3_Q > 8), uint64_t, uint32_t>::type;
+  const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (wv >= nw) return;  // whole waves
+  const uint32_t lane = __lane_id();
+  const int rd = C.cur, wr = C.cur ^ 1;
+  const int M = C.M;
+  const uint32_t nk = (uint32_t)C.nk;
+  const int64_t S = ws[wv], E = ws[wv + 1];
+  const bool vnull = C.vtag == T_NULL, vflt = C.vtag == T_FLOAT;
+  const int64_t tbase = B.ts[0];  // the narrow records' ts base (k_cs_pack)
+  uint64_t t10, t11;
+  cs_tables(M, t10, t11);
+  uint64_t ident = 0;
+#pragma unroll
+  for (int i = 0; i <= CSEQ_MAXM; i++) ident |= (uint64_t)i << (4 * i);
+  // carried from the previous tile (its last event): L after it, its value and null flag, its run start
+  uint32_t cL = 0, cpv = 0;
+  bool cpn = true;
+  int64_t crs = S;
+  uint32_t nm = 0, nr = 0;
+  int64_t mo = 0, ro = 0;  // EMIT: the wave's next record / ref slot
+  if (EMIT) {
+    mo = C.wom[wv];
+    ro = C.wor[wv];
+    if (wv == nw - 1 && lane == 0) {  // the push's totals
+      O.count[0] = (unsigned long long)(mo + C.wcm[wv]);
+      O.count[1] = (unsigned long long)(ro + C.wcr[wv]);
+    }
+  }
+  int e = 0;
+  for (int64_t p0 = S; p0 < E; p0 += 64 * CS3_Q) {
+    const int64_t j0 = p0 + (int64_t)lane * CS3_Q;
+    uint32_t kq[CS3_Q];
+    R rq[CS3_Q];
+#pragma unroll
+    for (int q = 0; q < CS3_Q; q++) {
+      const int64_t j = j0 + q;
+      kq[q] = j < E ? sk[j] : 0xFFFFFFFFu;
+      rq[q] = j < E ? sv[j] : R{};
+    }
+    const uint32_t kbefore = (j0 > S && j0 < E) ? sk[j0 - 1] : 0xFFFFFFFEu;
+    // the previous event's value for the lane's first event: lane - 1's last, or (lane 0) the carried
+    const bool xnl = vnull || (rq[CS3_Q - 1].g >> 31) != 0;
+    uint32_t px = __shfl_up(rq[CS3_Q - 1].v, 1, 64);
+    bool pxn = __shfl_up((int)xnl, 1, 64) != 0;
+    if (lane == 0) {
+      px = cpv;
+      pxn = cpn;
+    }
+    // walk 1: per event f1 / f2 / head / valid bits (and the stored L at heads); the lane's composition
+    uint32_t hb = 0, ab = 0, bb = 0, vb = 0;
+    uint64_t L0q = 0;
+    uint64_t G = ident;
+    int gs = 0;
+    int64_t lh = -1;  // the lane's latest run start
+#pragma unroll
+    for (int q = 0; q < CS3_Q; q++) {
+      const int64_t j = j0 + q;
+      const uint32_t k = kq[q];
+      const bool v = j < E && k < nk;  // clock-only events sort last (nokey) and are skipped
+      const uint32_t kp = q == 0 ? kbefore : kq[q - 1];
+      const bool head = v && (j == S || kp != k);
+      const uint32_t x = rq[q].v;
+      const bool xn = vnull || (rq[q].g >> 31) != 0;
+      uint32_t L0 = 0;
+      if (head) {  // the key's stored state (the previous push)
+        L0 = C.len[rd][k];
+        px = C.prev[rd][k];
+        pxn = C.pnull[rd][k] != 0;
+        L0q |= (uint64_t)L0 << (4 * q);
+        lh = j;
+      }
+      double xf, xi, pf, pi;
+      sw_conv(x, vflt, xf, xi);
+      sw_conv(px, vflt, pf, pi);
+      const bool a = v && sw_pred<NT1>(C.f1, xf, xi, xn, 0.0, 0.0, true);
+      const bool b = v && sw_pred<NT2>(C.f2, pf, pi, pxn, xf, xi, xn);
+      const uint64_t F = a ? (b ? t11 : t10) : 0ull;
+      hb |= (head ? 1u : 0u) << q;
+      ab |= (a ? 1u : 0u) << q;
+      bb |= (b ? 1u : 0u) << q;
+      vb |= (v ? 1u : 0u) << q;
+      if (head) {
+        G = cs_tab_const(cs_at(F, L0));
+        gs = 1;
+      } else {
+        G = cs_comp(F, G);
+      }
+      px = x;
+      pxn = xn;
+    }
+    // the wave's scans: L into each lane, and the run start in force at its first event
+    uint64_t val = G;
+    int fl = gs;
+    if (lane == 0 && !gs) {
+      val = cs_tab_const(cs_at(G, cL));
+      fl = 1;
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(val, d, 64);
+      const int yf = __shfl_up(fl, d, 64);
+      if (lane >= (uint32_t)d && !fl) val = cs_comp(val, y);
+      if (lane >= (uint32_t)d) fl |= yf;
+    }
+    uint32_t Lin = cs_at(__shfl_up(val, 1, 64), 0);
+    if (lane == 0) Lin = cL;
+    int64_t rsc = lh;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t y = __shfl_up(rsc, d, 64);
+      if (lane >= (uint32_t)d && y > rsc) rsc = y;
+    }
+    int64_t rs_in = __shfl_up(rsc, 1, 64);
+    if (lane == 0 || rs_in < crs) rs_in = crs;
+    // walk 2: the lane's records and refs; per event L before it (a nibble) and the flags
+    // (emits | run start << Q | valid << 2Q | f1(x) << 3Q) for the event-major emit
+    uint32_t L = Lin, lm = 0, lr = 0;
+    Cs3W lbw = 0, fw = 0;
+#pragma unroll
+    for (int q = 0; q < CS3_Q; q++) {
+      const bool head = (hb >> q) & 1u;
+      const uint32_t Lb = head ? (uint32_t)(L0q >> (4 * q)) & 15u : L;
+      const bool a = (ab >> q) & 1u, b = (bb >> q) & 1u, v = (vb >> q) & 1u;
+      L = cs_at(a ? (b ? t11 : t10) : 0ull, Lb);
+      const bool em = v && Lb > 0 && b;
+      lm += em ? 1u : 0u;
+      lr += em ? Lb + 1u : 0u;
+      lbw |= (Cs3W)Lb << (4 * q);
+      fw |= (Cs3W)(em ? 1u : 0u) << q;
+    }
+    fw |= ((Cs3W)hb << CS3_Q) | ((Cs3W)vb << (2 * CS3_Q)) | ((Cs3W)ab << (3 * CS3_Q));
+    const uint32_t Lend = L;
+    const int64_t rs_end = max(rs_in, lh);
+    const uint32_t xlast = rq[CS3_Q - 1].v;
+    if (!EMIT) {
+      nm += lm;
+      nr += lr;
+    } else {
+      uint32_t xm = lm, xr = lr;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t ym = __shfl_up(xm, d, 64), yr = __shfl_up(xr, d, 64);
+        if (lane >= (uint32_t)d) {
+          xm += ym;
+          xr += yr;
+        }
+      }
+      const uint32_t m0 = xm - lm, r0 = xr - lr;        // the lane's first record / ref, from mo / ro
+      const int32_t rs0 = (int32_t)(rs_in - S);          // its run start in force, from S
+      // event-major: in step s lane l takes event p0 + 64 s + l (coalesced loads and stores), which
+      // lane 8 s + l / 8 walked; that lane's words give L before it and its record / ref slots
+#pragma unroll 1
+      for (int st = 0; st < CS3_Q; st++) {
+        const int src = st * (64 / CS3_Q) + (int)(lane / CS3_Q);
+        const int q = (int)(lane % CS3_Q);
+        const Cs3W LbW = __shfl(lbw, src, 64), FW = __shfl(fw, src, 64);
+        const uint32_t M0 = __shfl(m0, src, 64), R0 = __shfl(r0, src, 64);
+        const int32_t RS = __shfl(rs0, src, 64);
+        const int64_t j = p0 + (int64_t)st * 64 + lane;
+        if (!((FW >> (2 * CS3_Q + q)) & 1u)) continue;  // not a valid event (past E, or clock-only)
+        const uint32_t emw = (uint32_t)(FW & ((1u << CS3_Q) - 1u)), hw = (uint32_t)(FW >> CS3_Q) & ((1u << CS3_Q) - 1u);
+        const uint32_t below = (1u << q) - 1u;
+        uint32_t rb = 0;
+#pragma unroll
+        for (int q2 = 0; q2 < CS3_Q; q2++)
+          rb += ((emw >> q2) & 1u) && q2 < q ? (uint32_t)((LbW >> (4 * q2)) & 15u) + 1u : 0u;
+        const int64_t mi = mo + M0 + (uint32_t)__popc(emw & below), ri = ro + R0 + rb;
+        const uint32_t hm = hw & ((2u << q) - 1u);  // run starts at or before this event
+        const int64_t rs = hm ? p0 + (int64_t)src * CS3_Q + (31 - __clz(hm)) : S + RS;
+        const uint32_t Lb = (uint32_t)(LbW >> (4 * q)) & 15u;
+        const bool em = (emw >> q) & 1u, a = (FW >> (3 * CS3_Q + q)) & 1u;
+        const uint32_t La = cs_at(a ? (em ? t11 : t10) : 0ull, Lb);  // (Lb = 0: T11 and T10 agree)
+        const uint32_t k = sk[j];
+        const R rj = sv[j];
+        if (em) {
+          const uint32_t rfs = Lb + 1u;
+          if (mi >= O.cap || ri + rfs > O.refcap) {
+            e |= E_OUT;
+          } else {
+            const int64_t sg = bseq(B, rj.g & 0x7FFFFFFFu);
+            O.key[mi] = B.partitioned ? (int32_t)k : 0;
+            O.ts[mi] = cs_ts(rj, tbase);  // StateEvent ts = e2's (StreamPostStateProcessor.process :64-83)
+            O.type[mi] = 0;
+            O.pos[mi] = sg;
+            O.ref_off[mi] = ri;
+            O.slot_len[mi * MAXS] = (int16_t)Lb;
+            O.slot_len[mi * MAXS + 1] = 1;
+            // e1's chain: the key's Lb events before this one, oldest first; then e2
+            for (uint32_t t = 1; t <= Lb; t++) {
+              const int64_t pp = j - (int64_t)t;
+              int64_t qs;
+              if (pp >= rs) qs = bseq(B, sv[pp].g & 0x7FFFFFFFu);
+              else qs = C.hseq[rd][(int64_t)(M - (int)(rs - pp)) * C.nk + k];  // before the push
+              O.refs[ri + (Lb - t)] = qs;
+            }
+            O.refs[ri + Lb] = sg;
+          }
+        }
+        // the key's state after its run in the push (the run's last event)
+        const uint32_t knext = j + 1 < E ? sk[j + 1] : 0xFFFFFFFDu;
+        if (knext != k) {
+          const bool xn = vnull || (rj.g >> 31) != 0;
+          C.len[wr][k] = (uint8_t)La;
+          C.prev[wr][k] = rj.v;
+          C.pnull[wr][k] = xn ? 1 : 0;
+          for (int s2 = 0; s2 < M; s2++) {  // slot M-1 = this event, M-2 the one before, ...
+            const int64_t pp = j - (int64_t)(M - 1 - s2);
+            int64_t hs, ht;
+            if (pp >= rs) {
+              const R qv = pp == j ? rj : sv[pp];
+              hs = bseq(B, qv.g & 0x7FFFFFFFu);
+              ht = cs_ts(qv, tbase);
+            } else {
+              const int64_t so = (int64_t)(M - (int)(rs - pp)) * C.nk + k;
+              hs = C.hseq[rd][so];
+              ht = C.hts[rd][so];
+            }
+            C.hseq[wr][(int64_t)s2 * C.nk + k] = hs;
+            C.hts[wr][(int64_t)s2 * C.nk + k] = ht;
+          }
+        }
+      }
+      mo += __shfl(xm, 63, 64);
+      ro += __shfl(xr, 63, 64);
+    }
+    cL = __shfl(Lend, 63, 64);
+    cpv = __shfl(xlast, 63, 64);
+    cpn = __shfl((int)xnl, 63, 64) != 0;
+    crs = __shfl(rs_end, 63, 64);
   }
   if (!EMIT) {
 #pragma unroll
@@ -507,20 +801,24 @@ struct CseqState {
   }
 
   int64_t cap = 0;
+  bool scan64 = getenv("SHP_CSEQ_SCAN64") != nullptr;  // A/B: k_cs2 (a wave scan per 64 events)
   void* tmp = nullptr;  // the record sort's rocPRIM scratch
   size_t tmp_bytes = 0;
 
   // the records sorted with their keys (stable); CS_RADIX_BITS > 8: a onesweep config with that many
   // bits per pass (fewer passes over the 20 key bits of 1M keys)
+  template <class R>
   void sort_records(void* t, size_t& tb, int64_t n, int key_bits, hipStream_t s) {
+    R* pr = reinterpret_cast<R*>(D.pr);
+    R* sr = reinterpret_cast<R*>(D.sr);
 #if defined(CS_RADIX_BITS) && CS_RADIX_BITS != 8
     using Cfg = rocprim::radix_sort_config<
         rocprim::default_config, rocprim::default_config,
         rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>,
                                             CS_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
-    (void)rocprim::radix_sort_pairs<Cfg>(t, tb, D.pk, D.sk, D.pr, D.sr, (size_t)n, 0, key_bits + 1, s);
+    (void)rocprim::radix_sort_pairs<Cfg>(t, tb, D.pk, D.sk, pr, sr, (size_t)n, 0, key_bits + 1, s);
 #else
-    (void)rocprim::radix_sort_pairs(t, tb, D.pk, D.sk, D.pr, D.sr, (size_t)n, 0, key_bits + 1, s);
+    (void)rocprim::radix_sort_pairs(t, tb, D.pk, D.sk, pr, sr, (size_t)n, 0, key_bits + 1, s);
 #endif
   }
 
@@ -537,10 +835,11 @@ struct CseqState {
     al(D.wcr, nwmax);
     al(D.wom, nwmax);
     al(D.wor, nwmax);
-    size_t b1 = 0, b2 = 0;
-    sort_records(nullptr, b1, cap, key_bits, st);
+    size_t b1 = 0, b2 = 0, b3 = 0;
+    sort_records<CsRec>(nullptr, b1, cap, key_bits, st);
+    sort_records<CsRec12>(nullptr, b3, cap, key_bits, st);
     (void)rocprim::exclusive_scan(nullptr, b2, D.wcm, D.wom, 0u, (size_t)nwmax, rocprim::plus<uint32_t>(), st);
-    tmp_bytes = std::max<size_t>(std::max(b1, b2), 16);
+    tmp_bytes = std::max<size_t>(std::max(std::max(b1, b2), b3), 16);
     if (hipMalloc(&tmp, tmp_bytes) != hipSuccess) throw std::runtime_error("hipMalloc failed (count-sequence sort)");
     create_state(P, s, max_keys, st);
   }
@@ -607,12 +906,18 @@ struct CseqState {
     kt.mark(nullptr, s);
   }
 
-  template <bool EMIT>
+  template <bool EMIT, class R>
   void pass2(const BatchView& B, const MatchOut& O, int64_t nw, int* err, hipStream_t s) {
     const unsigned g = (unsigned)((nw * 64 + 255) / 256);
+    const R* sr = reinterpret_cast<const R*>(D.sr);
     switch (D.f1.n * 3 + D.f2.n) {
 #define CS2_CASE(a, b) \
-  case a * 3 + b: k_cs2<a, b, EMIT><<<g, 256, 0, s>>>(D, B, O, D.sk, D.sr, D.ws, nw, err); break;
+  case a * 3 + b:                                                                                \
+    if (scan64)                                                                                  \
+      k_cs2<a, b, EMIT, R><<<g, 256, 0, s>>>(D, B, O, D.sk, sr, D.ws, nw, err);                  \
+    else                                                                                         \
+      k_cs3<a, b, EMIT, R><<<g, 256, 0, s>>>(D, B, O, D.sk, sr, D.ws, nw, err);                  \
+    break;
       CS2_CASE(0, 0) CS2_CASE(0, 1) CS2_CASE(0, 2) CS2_CASE(1, 0) CS2_CASE(1, 1) CS2_CASE(1, 2)
       CS2_CASE(2, 0) CS2_CASE(2, 1) CS2_CASE(2, 2)
 #undef CS2_CASE
@@ -622,8 +927,18 @@ struct CseqState {
 
   // the round-3 form over one push (device columns): pack, sort the records with their keys,
   // wave ranges, count pass, scan over the waves, the state carried to copy wr, emit pass
+  // narrow: the 12-byte records (a push beyond their ts range sets CS_WIDE; the engine re-runs it wide)
   void run2(const BatchView& B, const int32_t* key, const int32_t* stream, int key_bits, const MatchOut& O, int* err,
-            hipStream_t s, KTimer& kt) {
+            hipStream_t s, KTimer& kt, bool narrow) {
+    if (narrow)
+      run2t<CsRec12>(B, key, stream, key_bits, O, err, s, kt);
+    else
+      run2t<CsRec>(B, key, stream, key_bits, O, err, s, kt);
+  }
+
+  template <class R>
+  void run2t(const BatchView& B, const int32_t* key, const int32_t* stream, int key_bits, const MatchOut& O, int* err,
+             hipStream_t s, KTimer& kt) {
     const int64_t n = B.n;
     (void)hipMemsetAsync(D.tsmax, 0, sizeof(unsigned long long), s);
     // the state of keys without events in this push passes to copy wr unchanged
@@ -640,22 +955,22 @@ struct CseqState {
     }
     kt.mark("cs_pack", s);
     const unsigned gp = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-    k_cs_pack<<<gp, 256, 0, s>>>(B.ts, key, stream, (const uint32_t*)B.cols[0], B.nulls[0], n, B.partitioned,
-                                 (uint32_t)D.nk, D.pk, D.pr, D.tsmax, err);
+    k_cs_pack<R><<<gp, 256, 0, s>>>(B.ts, key, stream, (const uint32_t*)B.cols[0], B.nulls[0], n, B.partitioned,
+                                    (uint32_t)D.nk, D.pk, reinterpret_cast<R*>(D.pr), D.tsmax, err);
     kt.mark("cs_sort", s);
     size_t tb = tmp_bytes;
-    sort_records(tmp, tb, n, key_bits, s);
+    sort_records<R>(tmp, tb, n, key_bits, s);
     kt.mark("cs_count", s);
     const int64_t nw = (n + CS2_P - 1) / CS2_P;
     k_cs2_ranges<<<(unsigned)(((nw + 1) * 64 + 255) / 256), 256, 0, s>>>(D.sk, n, nw, D.ws);
-    pass2<false>(B, O, nw, err, s);
+    pass2<false, R>(B, O, nw, err, s);
     kt.mark("cs_scan", s);
     tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.wcm, D.wom, 0u, (size_t)nw, rocprim::plus<uint32_t>(), s);
     tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.wcr, D.wor, 0u, (size_t)nw, rocprim::plus<uint32_t>(), s);
     kt.mark("cs_emit", s);
-    pass2<true>(B, O, nw, err, s);
+    pass2<true, R>(B, O, nw, err, s);
     kt.mark(nullptr, s);
   }
 

@@ -265,6 +265,8 @@ struct shp_engine {
   int64_t clock = 0;
   int key_bits = 1;
   const bool cseq_v1 = getenv("SHP_CSEQ_V1") != nullptr;  // A/B: the round-2 count-sequence kernels
+  const bool cseq_wide = getenv("SHP_CSEQ_WIDE") != nullptr;  // A/B: the 16-byte records on every push
+  int64_t cseq_wide_reruns = 0;
   const bool labs_v1 = getenv("SHP_LABS_V1") != nullptr;  // A/B: logical-absent batch by key sort + gather
   LaneLayout Yl{};     // per-workgroup LDS layout of the lanes (lds_lanes > 0)
   int lds_lanes = 0;
@@ -511,7 +513,7 @@ struct shp_engine {
     } else if (fast == 3 && !cseq_v1) {  // count sequence: its own record sort (cseq.h, run2)
       kt.mark(nullptr, stream);
       HIP_OK(hipEventRecord(ev1, stream));
-      cs.run2(B, x_key, x_stream, key_bits, O, d_err, stream, kt);
+      cs.run2(B, x_key, x_stream, key_bits, O, d_err, stream, kt, !cseq_wide);
       HIP_OK(hipMemcpyAsync(h_tsmax, cs.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
     } else {
       int gb = (int)std::min<int64_t>((n + 255) / 256, 2048);
@@ -629,6 +631,19 @@ struct shp_engine {
       sw.solve(B, O, d_err, stream, kt);
       sw.spill(B, O, d_err, stream, kt);
       if (cfg.match_layout == SHP_LAYOUT_FULL) sw.expand(B, x_key, O, d_err, stream, kt);
+      HIP_OK(hipEventRecord(ev2, stream));
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      std::memcpy(&herr, h_status + 2, sizeof(int));
+    }
+    if (fast == 3 && !cseq_v1 && !cseq_wide && (herr & CS_WIDE)) {
+      // the push's ts leave the narrow records' range (+-2^31 ms of its first ts): the 16-byte
+      // form re-runs it from the same committed state
+      cseq_wide_reruns++;
+      HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
+      cs.run2(B, x_key, x_stream, key_bits, O, d_err, stream, kt, false);
+      HIP_OK(hipMemcpyAsync(h_tsmax, cs.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
       HIP_OK(hipEventRecord(ev2, stream));
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
@@ -1489,6 +1504,7 @@ int64_t shp_engine_stat(const shp_engine* e, const char* which) {
   if (w == "pushes") return e->pushes;
   if (w == "lean_pushes") return e->lean_pushes;
   if (w == "lean_fallbacks") return e->lean_fallbacks;
+  if (w == "cseq_wide_reruns") return e->cseq_wide_reruns;
   if (w == "labs_fallbacks") return e->labs_fallbacks;
   if (w == "spill_reruns") return e->spill_reruns;
   if (w == "spilled_owners") return e->fast == 2 ? e->sw.count_spilled() : 0;

@@ -160,3 +160,19 @@ def test_cseq_equals_general_lanes():
     assert a.path == 3 and b.path == 0
     ra, rb = per_key(run(a, cq, g, 77_777)), per_key(run(b, cq, g, 77_777))
     assert compare(ra, rb) is None, compare(ra, rb)
+
+
+@pytest.mark.gpu
+def test_cseq_wide_ts_span_reruns_with_16_byte_records():
+    """A push whose ts span more than 2^31 ms (the 12-byte records' range): the engine re-runs it
+    in the 16-byte form; the matches (ts included) equal the oracle's."""
+    rng = np.random.default_rng(12)
+    ts, key, v = _stream(rng, 60_000, 200)
+    ts[30_000:] += 3 << 31  # a jump of ~200 days inside the first push
+    cq = _cq(_app(5, "<"))
+    want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 40_000)
+    eng = _hip(cq, 200, 1 << 16)
+    got = _push(eng, ts, key, v, 40_000)
+    assert compare(want, got) is None, compare(want, got)
+    assert eng.stat("cseq_wide_reruns") == 1  # the second push (20k events after the jump) is narrow
+    assert sum(len(x) for x in want.values()) > 100
