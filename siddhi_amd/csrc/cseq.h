@@ -88,13 +88,20 @@ struct CseqDev {
   // round-3 form: the packed records, sorted with their keys; per wave range starts, counts, offsets
   uint32_t *pk, *sk;
   CsRec *pr, *sr;
+  unsigned long long* kend;  // nk: epoch << 32 | sorted position of the key's last event in the push (k_cs3)
+  uint32_t epoch;            // this push's (k_cs_state tells a key with events from one without)
   int64_t* ws;
   uint32_t *wcm, *wcr, *wom, *wor;
 };
 
+// history slot s of key k (s = M-1 the key's latest event, M-2 the one before, ...): a key's M
+// slots are contiguous, so the run end that rewrites them writes one span (slot-major arrays,
+// s * nk + k, measured 0.8 ms of C3''s 2.5 ms emit in scattered 8-byte writes)
+__host__ __device__ __forceinline__ int64_t cs_hslot(int s, int64_t k, int M) { return k * M + s; }
+
 // ---- round-3 data-parallel form (see the header)
 #ifndef CS2_P_CFG
-#define CS2_P_CFG 4096
+#define CS2_P_CFG 2048
 #endif
 constexpr int CS2_P = CS2_P_CFG;  // nominal events per wave range (ranges start at key runs)
 
@@ -324,7 +331,7 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
             const int64_t pp = j - (int64_t)t;
             int64_t q;
             if (pp >= rs) q = bseq(B, sv[pp].g & 0x7FFFFFFFu);
-            else q = C.hseq[rd][(int64_t)(M - (int)(rs - pp)) * C.nk + k];  // before the push
+            else q = C.hseq[rd][cs_hslot(M - (int)(rs - pp), k, M)];  // before the push
             O.refs[ri + (Lb - t)] = q;
           }
           O.refs[ri + Lb] = sg;
@@ -346,12 +353,12 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
             hs = bseq(B, q.g & 0x7FFFFFFFu);
             ht = cs_ts(q, tbase);
           } else {
-            const int64_t so = (int64_t)(M - (int)(rs - pp)) * C.nk + k;
+            const int64_t so = cs_hslot(M - (int)(rs - pp), k, M);
             hs = C.hseq[rd][so];
             ht = C.hts[rd][so];
           }
-          C.hseq[wr][(int64_t)s2 * C.nk + k] = hs;
-          C.hts[wr][(int64_t)s2 * C.nk + k] = ht;
+          C.hseq[wr][cs_hslot(s2, k, M)] = hs;
+          C.hts[wr][cs_hslot(s2, k, M)] = ht;
         }
       }
     }
@@ -557,6 +564,10 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
         const uint32_t M0 = __shfl(m0, src, 64), R0 = __shfl(r0, src, 64);
         const int32_t RS = __shfl(rs0, src, 64);
         const int64_t j = p0 + (int64_t)st * 64 + lane;
+        // the next event's key (a run end: it differs): lane + 1's, lane 63 reads it
+        const uint32_t kl = j < E ? sk[j] : 0xFFFFFFFDu;
+        uint32_t knext = __shfl_down(kl, 1, 64);
+        if (lane == 63) knext = j + 1 < E ? sk[j + 1] : 0xFFFFFFFDu;
         if (!((FW >> (2 * CS3_Q + q)) & 1u)) continue;  // not a valid event (past E, or clock-only)
         const uint32_t emw = (uint32_t)(FW & ((1u << CS3_Q) - 1u)), hw = (uint32_t)(FW >> CS3_Q) & ((1u << CS3_Q) - 1u);
         const uint32_t below = (1u << q) - 1u;
@@ -570,7 +581,7 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
         const uint32_t Lb = (uint32_t)(LbW >> (4 * q)) & 15u;
         const bool em = (emw >> q) & 1u, a = (FW >> (3 * CS3_Q + q)) & 1u;
         const uint32_t La = cs_at(a ? (em ? t11 : t10) : 0ull, Lb);  // (Lb = 0: T11 and T10 agree)
-        const uint32_t k = sk[j];
+        const uint32_t k = kl;
         const R rj = sv[j];
         if (em) {
           const uint32_t rfs = Lb + 1u;
@@ -586,38 +597,22 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
             O.slot_len[mi * MAXS] = (int16_t)Lb;
             O.slot_len[mi * MAXS + 1] = 1;
             // e1's chain: the key's Lb events before this one, oldest first; then e2
+#ifndef CS_DIAG_NOREFS  // diagnostics only (wrong output): the emit without its chain refs
             for (uint32_t t = 1; t <= Lb; t++) {
               const int64_t pp = j - (int64_t)t;
               int64_t qs;
               if (pp >= rs) qs = bseq(B, sv[pp].g & 0x7FFFFFFFu);
-              else qs = C.hseq[rd][(int64_t)(M - (int)(rs - pp)) * C.nk + k];  // before the push
+              else qs = C.hseq[rd][cs_hslot(M - (int)(rs - pp), k, M)];  // before the push
               O.refs[ri + (Lb - t)] = qs;
             }
             O.refs[ri + Lb] = sg;
+#endif
           }
         }
         // the key's state after its run in the push (the run's last event)
-        const uint32_t knext = j + 1 < E ? sk[j + 1] : 0xFFFFFFFDu;
-        if (knext != k) {
-          const bool xn = vnull || (rj.g >> 31) != 0;
+        if (knext != k) {  // the run's last event: L after it, and where it is (k_cs_state does the rest)
           C.len[wr][k] = (uint8_t)La;
-          C.prev[wr][k] = rj.v;
-          C.pnull[wr][k] = xn ? 1 : 0;
-          for (int s2 = 0; s2 < M; s2++) {  // slot M-1 = this event, M-2 the one before, ...
-            const int64_t pp = j - (int64_t)(M - 1 - s2);
-            int64_t hs, ht;
-            if (pp >= rs) {
-              const R qv = pp == j ? rj : sv[pp];
-              hs = bseq(B, qv.g & 0x7FFFFFFFu);
-              ht = cs_ts(qv, tbase);
-            } else {
-              const int64_t so = (int64_t)(M - (int)(rs - pp)) * C.nk + k;
-              hs = C.hseq[rd][so];
-              ht = C.hts[rd][so];
-            }
-            C.hseq[wr][(int64_t)s2 * C.nk + k] = hs;
-            C.hts[wr][(int64_t)s2 * C.nk + k] = ht;
-          }
+          C.kend[k] = ((unsigned long long)C.epoch << 32) | (uint32_t)j;
         }
       }
       mo += __shfl(xm, 63, 64);
@@ -640,6 +635,53 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
     }
   }
   if (e) atomicOr(err, e);
+}
+
+// per key, after k_cs3's emit: a key with events in the push takes its previous value and null
+// flag and its last M events' (seq, ts) from the sorted records at its run end (the slots before the
+// run from its stored history); a key without passes its state through.  One thread per key, each
+// key's M slots contiguous: coalesced where the emit's per-run-end writes were not (0.8 ms of 2.5)
+template <class R>
+__global__ __launch_bounds__(256) void k_cs_state(CseqDev C, BatchView B, const uint32_t* __restrict__ sk,
+                                                  const R* __restrict__ sv) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= C.nk) return;
+  const int rd = C.cur, wr = C.cur ^ 1;
+  const int M = C.M;
+  const unsigned long long ke = C.kend[k];
+  if ((uint32_t)(ke >> 32) != C.epoch) {
+    C.len[wr][k] = C.len[rd][k];
+    C.prev[wr][k] = C.prev[rd][k];
+    C.pnull[wr][k] = C.pnull[rd][k];
+    for (int s2 = 0; s2 < M; s2++) {
+      C.hseq[wr][cs_hslot(s2, k, M)] = C.hseq[rd][cs_hslot(s2, k, M)];
+      C.hts[wr][cs_hslot(s2, k, M)] = C.hts[rd][cs_hslot(s2, k, M)];
+    }
+    return;
+  }
+  const int64_t j = (int64_t)(uint32_t)ke;
+  const int64_t tbase = B.ts[0];
+  const R rj = sv[j];
+  C.prev[wr][k] = rj.v;
+  C.pnull[wr][k] = (C.vtag == T_NULL || (rj.g >> 31) != 0) ? 1 : 0;
+  // the run start, as far back as the history reaches
+  int64_t rs = j;
+  while (rs > j - (M - 1) && rs > 0 && sk[rs - 1] == (uint32_t)k) rs--;
+  for (int s2 = 0; s2 < M; s2++) {  // slot M-1 = the last event, M-2 the one before, ...
+    const int64_t pp = j - (int64_t)(M - 1 - s2);
+    int64_t hs, ht;
+    if (pp >= rs) {
+      const R qv = pp == j ? rj : sv[pp];
+      hs = bseq(B, qv.g & 0x7FFFFFFFu);
+      ht = cs_ts(qv, tbase);
+    } else {
+      const int64_t so = cs_hslot(M - (int)(rs - pp), k, M);
+      hs = C.hseq[rd][so];
+      ht = C.hts[rd][so];
+    }
+    C.hseq[wr][cs_hslot(s2, k, M)] = hs;
+    C.hts[wr][cs_hslot(s2, k, M)] = ht;
+  }
 }
 
 template <int NT1, int NT2, bool EMIT>
@@ -668,8 +710,8 @@ __global__ __launch_bounds__(256) void k_cseq(CseqDev C, BatchView B, MatchOut O
     for (int i = 0; i < CSEQ_MAXM; i++) {
       const int s = i - (CSEQ_MAXM - M);  // history slot s of the stored M
       if (s >= 0) {
-        hs[i] = C.hseq[rd][(int64_t)s * C.nk + k];
-        ht[i] = C.hts[rd][(int64_t)s * C.nk + k];
+        hs[i] = C.hseq[rd][cs_hslot(s, k, M)];
+        ht[i] = C.hts[rd][cs_hslot(s, k, M)];
       }
     }
     beg = kbeg[k];
@@ -766,8 +808,8 @@ __global__ __launch_bounds__(256) void k_cseq(CseqDev C, BatchView B, MatchOut O
     for (int i = 0; i < CSEQ_MAXM; i++) {
       const int s = i - (CSEQ_MAXM - M);
       if (s >= 0) {
-        C.hseq[wr][(int64_t)s * C.nk + k] = hs[i];
-        C.hts[wr][(int64_t)s * C.nk + k] = ht[i];
+        C.hseq[wr][cs_hslot(s, k, M)] = hs[i];
+        C.hts[wr][cs_hslot(s, k, M)] = ht[i];
       }
     }
   }
@@ -831,6 +873,9 @@ struct CseqState {
     al(D.sr, cap);
     const int64_t nwmax = cap / CS2_P + 2;
     al(D.ws, nwmax + 1);
+    al(D.kend, std::max<int64_t>(max_keys, 1));
+    (void)hipMemsetAsync(D.kend, 0, sizeof(unsigned long long) * std::max<int64_t>(max_keys, 1), st);
+    D.epoch = 0;
     al(D.wcm, nwmax);
     al(D.wcr, nwmax);
     al(D.wom, nwmax);
@@ -944,11 +989,18 @@ struct CseqState {
     // the state of keys without events in this push passes to copy wr unchanged
     const int rd = D.cur, wr = D.cur ^ 1;
     const size_t nk = (size_t)D.nk, hm = (size_t)D.M * nk * 8;
-    (void)hipMemcpyAsync(D.len[wr], D.len[rd], nk, hipMemcpyDeviceToDevice, s);
-    (void)hipMemcpyAsync(D.prev[wr], D.prev[rd], nk * 4, hipMemcpyDeviceToDevice, s);
-    (void)hipMemcpyAsync(D.pnull[wr], D.pnull[rd], nk, hipMemcpyDeviceToDevice, s);
-    (void)hipMemcpyAsync(D.hseq[wr], D.hseq[rd], hm, hipMemcpyDeviceToDevice, s);
-    (void)hipMemcpyAsync(D.hts[wr], D.hts[rd], hm, hipMemcpyDeviceToDevice, s);
+    if (scan64 || n <= 0) {  // (k_cs3: k_cs_state passes the state of keys without events)
+      (void)hipMemcpyAsync(D.len[wr], D.len[rd], nk, hipMemcpyDeviceToDevice, s);
+      (void)hipMemcpyAsync(D.prev[wr], D.prev[rd], nk * 4, hipMemcpyDeviceToDevice, s);
+      (void)hipMemcpyAsync(D.pnull[wr], D.pnull[rd], nk, hipMemcpyDeviceToDevice, s);
+      (void)hipMemcpyAsync(D.hseq[wr], D.hseq[rd], hm, hipMemcpyDeviceToDevice, s);
+      (void)hipMemcpyAsync(D.hts[wr], D.hts[rd], hm, hipMemcpyDeviceToDevice, s);
+    }
+    D.epoch++;
+    if (D.epoch == 0) {  // (2^32 pushes) no stale run end may carry the new epoch
+      (void)hipMemsetAsync(D.kend, 0, sizeof(unsigned long long) * nk, s);
+      D.epoch = 1;
+    }
     if (n <= 0) {
       (void)hipMemsetAsync(O.count, 0, 2 * sizeof(unsigned long long), s);
       return;
@@ -971,6 +1023,10 @@ struct CseqState {
     (void)rocprim::exclusive_scan(tmp, tb, D.wcr, D.wor, 0u, (size_t)nw, rocprim::plus<uint32_t>(), s);
     kt.mark("cs_emit", s);
     pass2<true, R>(B, O, nw, err, s);
+    if (!scan64) {
+      kt.mark("cs_state", s);
+      k_cs_state<R><<<(unsigned)((D.nk + 255) / 256), 256, 0, s>>>(D, B, D.sk, reinterpret_cast<const R*>(D.sr));
+    }
     kt.mark(nullptr, s);
   }
 
@@ -982,7 +1038,7 @@ struct CseqState {
       for (void* p : ps)
         if (p) (void)hipFree(p);
     }
-    void* qs[] = {D.tsmax, D.cm, D.cr, D.om, D.orf, D.pk, D.sk, D.pr, D.sr, D.ws, D.wcm, D.wcr, D.wom, D.wor, tmp};
+    void* qs[] = {D.tsmax, D.cm, D.cr, D.om, D.orf, D.pk, D.sk, D.pr, D.sr, D.ws, D.wcm, D.wcr, D.wom, D.wor, D.kend, tmp};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = CseqDev{};

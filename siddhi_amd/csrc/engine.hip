@@ -1001,7 +1001,7 @@ struct shp_engine {
       const int64_t* hseq = (const int64_t*)sp[3];
       const int64_t* hts = (const int64_t*)sp[4];
       for (int32_t k = 0; k < cfg.max_keys; k++) {
-        const int64_t last = hseq[(int64_t)(C.M - 1) * cfg.max_keys + k];
+        const int64_t last = hseq[cs_hslot(C.M - 1, k, C.M)];
         if (last < 0) continue;  // no event of this key yet
         o += firstKey ? "\"" : ",\"";
         firstKey = false;
@@ -1010,14 +1010,14 @@ struct shp_engine {
         o += "\":{\"e1\":{\"Count\":";
         jnum(o, L);
         o += ",\"PendingStateEventList\":[{\"ts\":";
-        jnum(o, L ? hts[(int64_t)(C.M - 1) * cfg.max_keys + k] : -1);
+        jnum(o, L ? hts[cs_hslot(C.M - 1, k, C.M)] : -1);
         o += ",\"slots\":[[";
         for (int i = C.M - L; i < C.M; i++) {
           if (i > C.M - L) o += ",";
-          ev(o, hseq[(int64_t)i * cfg.max_keys + k], hts[(int64_t)i * cfg.max_keys + k]);
+          ev(o, hseq[cs_hslot(i, k, C.M)], hts[cs_hslot(i, k, C.M)]);
         }
         o += "],[]]}]},\"LastEvent\":";
-        ev(o, last, hts[(int64_t)(C.M - 1) * cfg.max_keys + k]);
+        ev(o, last, hts[cs_hslot(C.M - 1, k, C.M)]);
         o += "}";
       }
     } else if (fast == 2 || fast == 1) {
