@@ -65,7 +65,10 @@ constexpr int SW_LKTAB = 65536;     // scatter LDS bound: its counters + the key
 #endif
 constexpr int SWP_THREADS = SWP_THREADS_CFG;  // scatter workgroup
 constexpr int SWP_WAVES = SWP_THREADS / 64;
-constexpr int SWP_ROUND = SWP_THREADS * 8;  // events ranked per round: 8 per lane
+#ifndef SWP_PER_LANE_CFG
+#define SWP_PER_LANE_CFG 8
+#endif
+constexpr int SWP_ROUND = SWP_THREADS * SWP_PER_LANE_CFG;  // events ranked per round: 8 per lane
 constexpr int SWP_SEG = SWP_ROUND / SWP_WAVES;
 constexpr int SWP_SUB = SWP_SEG / 64;
 // solve
