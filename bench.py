@@ -36,7 +36,7 @@ BYTES_PER_MATCH = {"pairs32": 8,  # (e2 batch index, e2 seq - e1 seq) as two u32
                    "pairs": 16,  # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
                    "agg": 12,    # (key u32, aggregate f64) per match (SHP_LAYOUT_AGG, C5)
                    "full": 16}
-KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_lean", "sw_solve", "sw_spill", "sw_expand",
+KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_win", "sw_win_tail", "sw_lean", "sw_solve", "sw_spill", "sw_expand",
            "radix_sort", "clock_scan", "key_hist", "key_scan", "sort_keys", "iota", "clamp_clock",
            "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry", "nfa_lanes",
            "cseq_count", "cseq_scan", "cseq", "cs_pack", "cs_sort", "cs_count", "cs_scan", "cs_emit", "cs_state", "labs_pack", "labs_sort", "labs_gather", "labs_count", "labs_scan", "labs", "labs_pos", "labs_out",

@@ -180,6 +180,13 @@ int shp_restore(shp_engine* e, const void* buf, size_t len);
  * Writes at most cap bytes (NUL-terminated) and returns the full length, or a negative status. */
 int64_t shp_snapshot_describe(shp_engine* e, const void* buf, size_t len, char* out, size_t cap);
 int shp_engine_num_states(const shp_engine* e);
+/* The stream (index in the program's "streams" order, i.e. the receiver) state `state` reads, or
+ * -1.  States are numbered as StateInputStreamParser.parse adds their MetaStreamEvents
+ * (core/util/parser/StateInputStreamParser.java:167-177: stateIndex = getStreamEventCount() - 1),
+ * so a host builds one SingleStreamRuntime per state, in MetaStateEvent order, on the receiver of
+ * this stream (QueryParserHelper.initStreamRuntime indexes getSingleStreamRuntimes() by state,
+ * core/util/parser/helper/QueryParserHelper.java:161-167). */
+int shp_engine_state_stream(const shp_engine* e, int state);
 /* Which kernels the engine runs: 2 = sweep (owner partition + LDS sweep), 1 = specialised 2-state
  * scan kernel, 0 = general NFA lanes, 3 = count-sequence automaton (`every e1=S[f1]<1:M>, e2=S[f2]`
  * with f2 over e2 and e1[last], M <= 8, no within; siddhi_amd/csrc/cseq.h), 4 = logical-absent

@@ -12,7 +12,13 @@
  *     (shp_engine_create_siddhiql; SHP_ERR_UNSUPPORTED = a construct outside the state path, and
  *     the host keeps the reference runtime for that query).
  *   core/util/SiddhiAppRuntimeBuilder.java:172-190 — unchanged: it subscribes the receivers
- *     getSingleStreamRuntimes() returns (GpuStateReceiver, one per distinct stream).
+ *     getSingleStreamRuntimes() returns.  As the reference does, the runtime returns one
+ *     SingleStreamRuntime per state, in MetaStateEvent order (StateInputStreamParser.java:86-125
+ *     builds one ProcessStreamReceiver per stream id and StreamInnerStateRuntime.java:63-67 one
+ *     SingleStreamRuntime per state on it), so QueryParserHelper.initStreamRuntime
+ *     (core/util/parser/helper/QueryParserHelper.java:161-167) finds runtime i for state i; states
+ *     of one stream share that stream's GpuStateReceiver, which StreamJunction.subscribe
+ *     (core/stream/StreamJunction.java:334-338) subscribes once.
  *   core/partition/PartitionStreamReceiver.java:176-283 — for a partitioned GPU query, append
  *     (key string, event) to the same batch instead of one send() per key
  *     (GpuStateReceiver.append(ts, key, data), then endOfChunk()); the runtime maps the key to a
@@ -30,6 +36,7 @@ import io.siddhi.core.event.ComplexEventChunk;
 import io.siddhi.core.event.MetaComplexEvent;
 import io.siddhi.core.event.state.MetaStateEvent;
 import io.siddhi.core.event.state.StateEvent;
+import io.siddhi.core.event.stream.MetaStreamEvent;
 import io.siddhi.core.event.stream.StreamEvent;
 import io.siddhi.core.exception.SiddhiAppCreationException;
 import io.siddhi.core.exception.SiddhiAppRuntimeException;
@@ -38,11 +45,14 @@ import io.siddhi.core.query.input.stream.single.SingleStreamRuntime;
 import io.siddhi.core.query.processor.ProcessingMode;
 import io.siddhi.core.query.processor.Processor;
 import io.siddhi.core.query.selector.QuerySelector;
+import io.siddhi.query.api.definition.AbstractDefinition;
+import io.siddhi.query.api.definition.Attribute;
 
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
 import java.util.ArrayList;
 import java.util.List;
+import java.util.Map;
 import java.util.concurrent.Executors;
 import java.util.concurrent.ScheduledExecutorService;
 import java.util.concurrent.ScheduledFuture;
@@ -82,6 +92,9 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
     private final FlushPolicy policy;
     private final ScheduledExecutorService flusher;
     private final ScheduledFuture<?> flushTask;
+    // DEFERRED: a push that failed on the flusher thread, rethrown to the next caller (append,
+    // flush, advanceClock, snapshot) so the sender sees it; the flusher keeps running
+    private volatile RuntimeException deferredFailure;
 
     /**
      * The Java host's entry point: the library lowers the query from the app text
@@ -92,6 +105,7 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
      */
     public static GpuStateStreamRuntime fromSiddhiQL(String appText, String queryName, int maxKeys, long maxBatch,
                                                      int device, long startClock, MetaStateEvent metaStateEvent,
+                                                     Map<String, AbstractDefinition> streamDefinitionMap,
                                                      SiddhiQueryContext queryContext, FlushPolicy policy,
                                                      long maxDelayMillis) {
         NativeDictionary strings = new NativeDictionary(0, "string values");
@@ -103,66 +117,150 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
             throw new SiddhiAppCreationException("shp_compile_siddhiql: " + e.getMessage(), e);
         }
         ProgramInfo info = ProgramInfo.parse(program);
-        return new GpuStateStreamRuntime(appText, queryName, info.streams, info.columns,
-                info.partitioned ? maxKeys : 1, maxBatch, device, startClock, metaStateEvent, queryContext, strings,
-                policy, maxDelayMillis);
+        try {
+            populateMeta(metaStateEvent, info, streamDefinitionMap);
+            return new GpuStateStreamRuntime(appText, queryName, info, info.partitioned ? maxKeys : 1, maxBatch,
+                    device, startClock, metaStateEvent, queryContext, strings, policy, maxDelayMillis);
+        } catch (RuntimeException e) {
+            strings.close();  // the constructor released everything else it had made
+            throw e;
+        }
+    }
+
+    /**
+     * One MetaStreamEvent per state, in state order, as SingleInputStreamParser.parseInputStream /
+     * initMetaStreamEvent (core/util/parser/SingleInputStreamParser.java:99-104, 261-296) add them
+     * while StateInputStreamParser walks the state tree: the stream's definition, the state's
+     * reference id when it differs from the stream id, multiValue for a count state.  Every
+     * attribute of the definition is registered as output data in definition order, because the
+     * match events are rebuilt from the rows as sent (ColumnarBatch.event); the selector's
+     * variables (ExpressionParser.parseVariable, addOutputData) then resolve to those positions.
+     * A MetaStateEvent that already holds the states (a host that ran the reference parser for
+     * them) is left as it is.
+     */
+    static void populateMeta(MetaStateEvent meta, ProgramInfo info, Map<String, AbstractDefinition> defs) {
+        int n = info.stateStream.length;
+        if (meta.getStreamEventCount() == n) {
+            return;
+        }
+        if (meta.getStreamEventCount() != 0) {
+            throw new SiddhiAppCreationException("MetaStateEvent holds " + meta.getStreamEventCount()
+                    + " stream events, the lowered query " + n + " states");
+        }
+        for (int st = 0; st < n; st++) {
+            String streamId = info.streams[info.stateStream[st]];
+            AbstractDefinition def = defs == null ? null : defs.get(streamId);
+            if (def == null) {
+                throw new SiddhiAppCreationException("Stream definition with ID '" + streamId + "' has not been defined");
+            }
+            MetaStreamEvent m = new MetaStreamEvent();
+            m.addInputDefinition(def);
+            String ref = info.stateRef[st];
+            if (ref != null && !ref.equals(streamId)) {
+                m.setInputReferenceId(ref);
+            }
+            m.setMultiValue(info.stateMulti[st]);
+            for (Attribute a : def.getAttributeList()) {
+                m.addOutputData(a);
+            }
+            meta.addEvent(m);
+        }
     }
 
     /**
      * @param appText      the SiddhiQL app; the library lowers query `queryName` of it
      *                     (shp_engine_create_siddhiql), interning string constants in `strings`
-     * @param streamIds    the program's streams, in program["streams"] order
-     * @param columns      program["columns"]
+     * @param info         the lowered program's streams, columns and per-state streams (ProgramInfo)
      * @param maxKeys      partition-key dictionary capacity (1 when the query is not partitioned)
      * @param maxBatch     events per push (a batch is flushed when full, on send return, or by timer)
      * @param device       HIP device ordinal
      * @param startClock   the event-time clock at start() (0 in playback mode)
+     * On failure every native handle made here (engine, key dictionary) and the arena are released
+     * before the exception leaves; `strings` stays the caller's.
      */
-    GpuStateStreamRuntime(String appText, String queryName, String[] streamIds, ColumnarBatch.Column[] columns,
-                          int maxKeys, long maxBatch, int device, long startClock,
-                          MetaStateEvent metaStateEvent, SiddhiQueryContext queryContext,
+    GpuStateStreamRuntime(String appText, String queryName, ProgramInfo info, int maxKeys, long maxBatch, int device,
+                          long startClock, MetaStateEvent metaStateEvent, SiddhiQueryContext queryContext,
                           NativeDictionary strings, FlushPolicy policy, long maxDelayMillis) {
         this.metaStateEvent = metaStateEvent;
         this.strings = strings;
-        this.keys = new NativeDictionary(maxKeys, "partition keys (max_keys = " + maxKeys + ")");
         this.policy = policy;
         this.outputDataSize = metaStateEvent.getOutputDataAttributes() == null ? 0
                 : metaStateEvent.getOutputDataAttributes().size();
-        MemorySegment cfg = arena.allocate(ShpNative.CONFIG);
-        cfg.set(JAVA_INT, 0, device);
-        cfg.set(JAVA_INT, 4, maxKeys);
-        cfg.set(JAVA_LONG, 8, maxBatch);
-        cfg.set(JAVA_LONG, 16, 0L);                 // max_matches: engine default
-        cfg.set(JAVA_LONG, 24, startClock);
-        cfg.set(JAVA_INT, 32, 0);                   // force_general: auto path
-        cfg.set(JAVA_INT, 36, 0);                   // profile_kernels
-        cfg.set(JAVA_INT, 40, ShpNative.LAYOUT_FULL);
-        MemorySegment out = arena.allocate(ADDRESS);
-        int rc;
+        NativeDictionary keyDict = null;
+        MemorySegment eng = MemorySegment.NULL;
         try {
-            rc = (int) ShpNative.ENGINE_CREATE_SIDDHIQL.invokeExact(arena.allocateFrom(appText),
-                    queryName == null ? MemorySegment.NULL : arena.allocateFrom(queryName), strings.handle(), cfg, out);
-        } catch (Throwable t) {
-            throw new SiddhiAppCreationException("shp_engine_create_siddhiql failed: " + t, t);
+            keyDict = new NativeDictionary(maxKeys, "partition keys (max_keys = " + maxKeys + ")");
+            MemorySegment cfg = arena.allocate(ShpNative.CONFIG);
+            cfg.set(JAVA_INT, ShpNative.CFG_DEVICE, device);
+            cfg.set(JAVA_INT, ShpNative.CFG_MAX_KEYS, maxKeys);
+            cfg.set(JAVA_LONG, ShpNative.CFG_MAX_BATCH, maxBatch);
+            cfg.set(JAVA_LONG, ShpNative.CFG_MAX_MATCHES, 0L);       // engine default
+            cfg.set(JAVA_LONG, ShpNative.CFG_START_CLOCK, startClock);
+            cfg.set(JAVA_INT, ShpNative.CFG_FORCE_GENERAL, 0);       // auto path
+            cfg.set(JAVA_INT, ShpNative.CFG_PROFILE_KERNELS, 0);
+            cfg.set(JAVA_INT, ShpNative.CFG_MATCH_LAYOUT, ShpNative.LAYOUT_FULL);
+            MemorySegment out = arena.allocate(ADDRESS);
+            int rc;
+            try {
+                rc = (int) ShpNative.ENGINE_CREATE_SIDDHIQL.invokeExact(arena.allocateFrom(appText),
+                        queryName == null ? MemorySegment.NULL : arena.allocateFrom(queryName), strings.handle(), cfg,
+                        out);
+            } catch (Throwable t) {
+                throw new SiddhiAppCreationException("shp_engine_create_siddhiql failed: " + t, t);
+            }
+            if (rc != ShpNative.OK) {
+                // SHP_ERR_UNSUPPORTED = a construct outside the state path: the host falls back to
+                // StateInputStreamParser (the reference runtime) for this query
+                throw new SiddhiAppCreationException("shp_engine_create_siddhiql: " + ShpNative.codeName(rc));
+            }
+            eng = out.get(ADDRESS, 0);
+            try {
+                numStates = (int) ShpNative.NUM_STATES.invokeExact(eng);
+            } catch (Throwable t) {
+                throw new SiddhiAppCreationException("shp_engine_num_states failed", t);
+            }
+            if (numStates != metaStateEvent.getStreamEventCount() || numStates != info.stateStream.length) {
+                throw new SiddhiAppCreationException("state count mismatch: engine " + numStates + ", MetaStateEvent "
+                        + metaStateEvent.getStreamEventCount() + ", program " + info.stateStream.length);
+            }
+            // one receiver per stream id, one SingleStreamRuntime per state on its stream's receiver,
+            // paired with that state's MetaStreamEvent (QueryParserHelper.java:161-167 indexes by state)
+            GpuStateReceiver[] receivers = new GpuStateReceiver[info.streams.length];
+            for (int st = 0; st < numStates; st++) {
+                int s;
+                try {
+                    s = (int) ShpNative.STATE_STREAM.invokeExact(eng, st);
+                } catch (Throwable t) {
+                    throw new SiddhiAppCreationException("shp_engine_state_stream failed", t);
+                }
+                if (s < 0 || s >= receivers.length || s != info.stateStream[st]) {
+                    throw new SiddhiAppCreationException("state " + st + ": engine stream " + s + ", program stream "
+                            + info.stateStream[st]);
+                }
+                if (receivers[s] == null) {
+                    receivers[s] = new GpuStateReceiver(info.streams[s], s, this, queryContext);
+                }
+                singleStreamRuntimes.add(new SingleStreamRuntime(receivers[s], null, ProcessingMode.BATCH,
+                        metaStateEvent.getMetaStreamEvent(st)));
+            }
+            matches = arena.allocate(ShpNative.MATCHES);
+            batch = new ColumnarBatch(arena, maxBatch, info.columns, strings, 64);
+        } catch (RuntimeException e) {
+            if (!eng.equals(MemorySegment.NULL)) {
+                try {
+                    ShpNative.ENGINE_DESTROY.invokeExact(eng);
+                } catch (Throwable ignored) {
+                    // the creation error is the one to report
+                }
+            }
+            if (keyDict != null) {
+                keyDict.close();
+            }
+            arena.close();
+            throw e;
         }
-        if (rc != ShpNative.OK) {
-            // SHP_ERR_UNSUPPORTED = a construct outside the state path: the host falls back to
-            // StateInputStreamParser (the reference runtime) for this query
-            throw new SiddhiAppCreationException("shp_engine_create_siddhiql: " + ShpNative.codeName(rc));
-        }
-        engine = out.get(ADDRESS, 0);
-        matches = arena.allocate(ShpNative.MATCHES);
-        try {
-            numStates = (int) ShpNative.NUM_STATES.invokeExact(engine);
-        } catch (Throwable t) {
-            throw new SiddhiAppCreationException("shp_engine_num_states failed", t);
-        }
-        batch = new ColumnarBatch(arena, maxBatch, columns, strings, 64);
-        for (int s = 0; s < streamIds.length; s++) {
-            GpuStateReceiver r = new GpuStateReceiver(streamIds[s], s, this, queryContext);
-            singleStreamRuntimes.add(new SingleStreamRuntime(r, null, ProcessingMode.BATCH,
-                    metaStateEvent.getMetaStreamEvent(s)));
-        }
+        this.engine = eng;
+        this.keys = keyDict;
         if (policy == FlushPolicy.DEFERRED) {
             flusher = Executors.newSingleThreadScheduledExecutor(r -> {
                 Thread t = new Thread(r, "siddhi-gpu-flush");
@@ -170,10 +268,28 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
                 return t;
             });
             long d = Math.max(1, maxDelayMillis);
-            flushTask = flusher.scheduleWithFixedDelay(this::flush, d, d, TimeUnit.MILLISECONDS);
+            // a failing push must not cancel the periodic task (ScheduledExecutorService suppresses
+            // every later run after an exception): keep it, hand it to the next caller
+            flushTask = flusher.scheduleWithFixedDelay(() -> {
+                try {
+                    flush();
+                } catch (RuntimeException e) {
+                    deferredFailure = e;
+                }
+            }, d, d, TimeUnit.MILLISECONDS);
         } else {
             flusher = null;
             flushTask = null;
+        }
+    }
+
+    /** A push that failed on the flusher thread (DEFERRED): thrown to the caller that comes next. */
+    private void rethrowDeferred() {
+        RuntimeException e = deferredFailure;
+        if (e != null) {
+            deferredFailure = null;
+            throw new SiddhiAppRuntimeException("a deferred push failed (its events were dropped): " + e.getMessage(),
+                    e);
         }
     }
 
@@ -217,6 +333,7 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
 
     // ---------------------------------------------------------------- ingress (GpuStateReceiver)
     void append(long timestamp, int keyId, int streamIndex, Object[] data) {
+        rethrowDeferred();
         lock.lock();
         try {
             batch.append(timestamp, keyId, streamIndex, data);
@@ -260,6 +377,7 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
 
     /** TimestampGeneratorImpl.setCurrentTimestamp with no event (absent-state timers). */
     void advanceClock(long now) {
+        rethrowDeferred();
         lock.lock();
         try {
             flush();
@@ -316,6 +434,7 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
 
     // ---------------------------------------------------------------- snapshot (GpuStateHolder)
     byte[] snapshot() {
+        rethrowDeferred();
         lock.lock();
         try {
             flush();

@@ -1,8 +1,11 @@
 /*
  * ProgramInfo — what the host reads back from a lowered program (shp_compile_siddhiql's JSON): the
- * stream names in program["streams"] order (receiver stream index) and program["columns"] (the
- * SoA columns a batch carries: stream index, attribute position, type).  A minimal JSON reader for
- * that fixed document; the engine itself parses the program (siddhi_amd/csrc/compile.h).
+ * stream names in program["streams"] order (receiver stream index), program["columns"] (the SoA
+ * columns a batch carries: stream index, attribute position, type) and, per state in
+ * MetaStateEvent order (program["states"][i]["id"] = StateInputStreamParser's stateIndex,
+ * core/util/parser/StateInputStreamParser.java:177), its stream, its reference id (e1, ...) and
+ * whether it is a count state (multi-valued, :380-403).  A minimal JSON reader for that fixed
+ * document; the engine itself parses the program (siddhi_amd/csrc/compile.h).
  * Source only: no JDK in this repository's image (DESIGN.md §6).
  */
 package io.siddhi.core.query.input.stream.state.gpu;
@@ -17,11 +20,18 @@ final class ProgramInfo {
     final String[] streams;
     final ColumnarBatch.Column[] columns;
     final boolean partitioned;
+    final int[] stateStream;        // per state id: index into streams
+    final String[] stateRef;        // per state id: the reference id (e1, ...), null when none
+    final boolean[] stateMulti;     // per state id: a count state (multi-valued slot)
 
-    private ProgramInfo(String[] streams, ColumnarBatch.Column[] columns, boolean partitioned) {
+    private ProgramInfo(String[] streams, ColumnarBatch.Column[] columns, boolean partitioned, int[] stateStream,
+                        String[] stateRef, boolean[] stateMulti) {
         this.streams = streams;
         this.columns = columns;
         this.partitioned = partitioned;
+        this.stateStream = stateStream;
+        this.stateRef = stateRef;
+        this.stateMulti = stateMulti;
     }
 
     @SuppressWarnings("unchecked")
@@ -42,7 +52,35 @@ final class ProgramInfo {
             cols[i] = new ColumnarBatch.Column(((Number) c.get("stream")).intValue(),
                     ((Number) c.get("attr")).intValue(), tag);
         }
-        return new ProgramInfo(names, cols, Boolean.TRUE.equals(p.get("partitioned")));
+        List<Object> st = (List<Object>) p.get("states");
+        int[] sst = new int[st.size()];
+        String[] sref = new String[st.size()];
+        boolean[] smulti = new boolean[st.size()];
+        for (Object o : st) {
+            Map<String, Object> m = (Map<String, Object>) o;
+            int id = ((Number) m.get("id")).intValue();
+            sst[id] = ((Number) m.get("stream")).intValue();
+            sref[id] = (String) m.get("ref");
+        }
+        markCounts(p.get("tree"), smulti);
+        return new ProgramInfo(names, cols, Boolean.TRUE.equals(p.get("partitioned")), sst, sref, smulti);
+    }
+
+    // the states under a "count" node of program["tree"] (CountStateElement: multiValue = true)
+    @SuppressWarnings("unchecked")
+    private static void markCounts(Object node, boolean[] multi) {
+        if (!(node instanceof Map)) {
+            return;
+        }
+        Map<String, Object> n = (Map<String, Object>) node;
+        if ("count".equals(n.get("t")) && n.get("state") instanceof Number) {
+            multi[((Number) n.get("state")).intValue()] = true;
+        }
+        for (Object v : n.values()) {
+            if (v instanceof Map) {
+                markCounts(v, multi);
+            }
+        }
     }
 
     private static final class Reader {

@@ -3,8 +3,9 @@
  * Source only: this repository's image has no JDK, so it is not compiled here (DESIGN.md §6).
  *
  * Every downcall mirrors one C-ABI entry point; struct layouts mirror shp_config, shp_batch and
- * shp_matches field for field (tests/test_abi.py checks the C layouts against the ctypes mirror
- * siddhi_amd/native.py; the offsets below are the same).
+ * shp_matches field for field.  tests/test_java_binding.py parses the layouts and the CFG_* offsets
+ * below out of this file and checks them against the header compiled with gcc (offsetof), and
+ * checks that every symbol a downcall names is declared in include/siddhi_hip.h.
  */
 package io.siddhi.core.query.input.stream.state.gpu;
 
@@ -51,6 +52,10 @@ final class ShpNative {
             JAVA_INT.withName("profile_kernels"), JAVA_INT.withName("match_layout"),
             MemoryLayout.paddingLayout(4));
 
+    /** Field offsets of shp_config (GpuStateStreamRuntime fills the struct by offset). */
+    static final long CFG_DEVICE = 0, CFG_MAX_KEYS = 4, CFG_MAX_BATCH = 8, CFG_MAX_MATCHES = 16,
+            CFG_START_CLOCK = 24, CFG_FORCE_GENERAL = 32, CFG_PROFILE_KERNELS = 36, CFG_MATCH_LAYOUT = 40;
+
     /** struct shp_batch (64 bytes): n, ts, key, stream, cols, nulls, clock, seq. */
     static final StructLayout BATCH = MemoryLayout.structLayout(
             JAVA_LONG.withName("n"), ADDRESS.withName("ts"), ADDRESS.withName("key"),
@@ -76,6 +81,8 @@ final class ShpNative {
     static final MethodHandle SNAPSHOT_DESCRIBE = fn("shp_snapshot_describe", JAVA_LONG, ADDRESS, ADDRESS, JAVA_LONG,
             ADDRESS, JAVA_LONG);
     static final MethodHandle NUM_STATES = fn("shp_engine_num_states", JAVA_INT, ADDRESS);
+    // the stream (program order) a state reads: one SingleStreamRuntime per state on that receiver
+    static final MethodHandle STATE_STREAM = fn("shp_engine_state_stream", JAVA_INT, ADDRESS, JAVA_INT);
     static final MethodHandle ENGINE_PATH = fn("shp_engine_path", JAVA_INT, ADDRESS);
     static final MethodHandle ENGINE_STAT = fn("shp_engine_stat", JAVA_LONG, ADDRESS, ADDRESS);  // monitoring counters
     static final MethodHandle LAST_ERROR = fn("shp_last_error", ADDRESS, ADDRESS);

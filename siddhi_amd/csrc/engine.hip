@@ -273,6 +273,7 @@ struct shp_engine {
   double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
   int64_t last_m = 0;
   int64_t pushes = 0, lean_pushes = 0, lean_fallbacks = 0, labs_fallbacks = 0;  // shp_engine_stat
+  int64_t win_pushes = 0, win_fallbacks = 0;
   int64_t spill_reruns = 0;
 
   ~shp_engine() { release(); }
@@ -501,6 +502,7 @@ struct shp_engine {
       HIP_OK(hipEventRecord(ev1, stream));
       if (!clock_only && n > 0 && sw.lean_push_for(B)) lean_pushes++;
       if (!clock_only) sw.run(B, x_key, O, d_err, stream, kt);
+      if (!clock_only && sw.last_win) win_pushes++;
       if (!clock_only && n > 0) sw.spill(B, O, d_err, stream, kt);  // spilled owners (none: no launch)
       lastB = B;
       lastKey = x_key;
@@ -607,6 +609,22 @@ struct shp_engine {
     HIP_OK(hipStreamSynchronize(stream));
     int herr = 0;
     std::memcpy(&herr, h_status + 2, sizeof(int));
+    if (fast == 2 && sw.last_win && (herr & SWE_LEAN) && !(herr & (SWE_KEYS | SWE_RANGE))) {
+      // k_sw_win handed the push back (a ts decrease within a key, more open candidates than a
+      // wave holds, a wide push): k_sw_lean re-runs it from the same committed state, and hands
+      // it on to the exact solve below if it does not cover it either
+      win_fallbacks++;
+      HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
+      kt.mark("sw_lean", stream);
+      sw.launch_lean(B, O, d_err, stream);
+      kt.mark(nullptr, stream);
+      if (cfg.match_layout == SHP_LAYOUT_FULL) sw.expand(B, x_key, O, d_err, stream, kt);
+      HIP_OK(hipEventRecord(ev2, stream));
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      std::memcpy(&herr, h_status + 2, sizeof(int));
+    }
     if (fast == 2 && (herr & SWE_LEAN) && !(herr & (SWE_KEYS | SWE_RANGE))) {
       // k_sw_lean handed the push back (a ts decrease within a key, a wide ts span, a large
       // carry): the exact solve re-runs it over the same partition from the same committed state
@@ -1496,6 +1514,13 @@ int64_t shp_snapshot_describe(shp_engine* e, const void* blob, size_t len, char*
 }
 
 int shp_engine_num_states(const shp_engine* e) { return e ? e->comp.P.nstates : 0; }
+int shp_engine_state_stream(const shp_engine* e, int state) {
+  if (!e || state < 0 || state >= e->comp.P.nstates) return -1;
+  const DevProg& P = e->comp.P;
+  for (int p = 0; p < P.npre; p++)
+    if (P.pre[p].stateId == state) return P.pre[p].stream;
+  return -1;
+}
 int shp_engine_path(const shp_engine* e) { return e ? e->fast : -1; }
 
 int64_t shp_engine_stat(const shp_engine* e, const char* which) {
@@ -1504,6 +1529,8 @@ int64_t shp_engine_stat(const shp_engine* e, const char* which) {
   if (w == "pushes") return e->pushes;
   if (w == "lean_pushes") return e->lean_pushes;
   if (w == "lean_fallbacks") return e->lean_fallbacks;
+  if (w == "win_pushes") return e->win_pushes;
+  if (w == "win_fallbacks") return e->win_fallbacks;
   if (w == "cseq_wide_reruns") return e->cseq_wide_reruns;
   if (w == "labs_fallbacks") return e->labs_fallbacks;
   if (w == "spill_reruns") return e->spill_reruns;

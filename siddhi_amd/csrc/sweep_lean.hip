@@ -42,6 +42,31 @@ void sw_launch_lean(int ct, int opc, unsigned grid, hipStream_t s, const SweepDe
 #undef SL_CASE
 }
 
+// k_sw_win (sweep_win.h): one 64-lane wave per unit of SWW_U records, then one per owner
+void sw_launch_win(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                   const MatchOut& O, int* err) {
+#define SW_CASE(c, p) \
+  case c * 8 + p: k_sw_win<c, p><<<grid, 64, 0, s>>>(D, B, O, err); break;
+  switch (ct * 8 + opc) {
+    SW_CASE(1, 1) SW_CASE(1, 2) SW_CASE(1, 3) SW_CASE(1, 4) SW_CASE(1, 5) SW_CASE(1, 6)
+    SW_CASE(2, 1) SW_CASE(2, 2) SW_CASE(2, 3) SW_CASE(2, 4) SW_CASE(2, 5) SW_CASE(2, 6)
+    default: break;
+  }
+#undef SW_CASE
+}
+
+void sw_launch_win_tail(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
+                        int* err) {
+#define SW_CASE(c, p) \
+  case c * 8 + p: k_sw_win_tail<c, p><<<grid, 64, 0, s>>>(D, B, err); break;
+  switch (ct * 8 + opc) {
+    SW_CASE(1, 1) SW_CASE(1, 2) SW_CASE(1, 3) SW_CASE(1, 4) SW_CASE(1, 5) SW_CASE(1, 6)
+    SW_CASE(2, 1) SW_CASE(2, 2) SW_CASE(2, 3) SW_CASE(2, 4) SW_CASE(2, 5) SW_CASE(2, 6)
+    default: break;
+  }
+#undef SW_CASE
+}
+
 void sw_launch_spill(int nt2, int ct, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                      const MatchOut& O, int* err) {
   switch (nt2 * 3 + ct) {

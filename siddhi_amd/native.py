@@ -23,7 +23,7 @@ SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACIT
               -4: "SHP_ERR_OUTPUT", -5: "SHP_ERR_DEVICE", -6: "SHP_ERR_KEYS"}
 
 SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches",
-           "shp_advance_clock", "shp_engine_num_states", "shp_engine_path", "shp_last_kernel_ms", "shp_engine_stat",
+           "shp_advance_clock", "shp_engine_num_states", "shp_engine_state_stream", "shp_engine_path", "shp_last_kernel_ms", "shp_engine_stat",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
            "shp_dev_to_host", "shp_host_alloc", "shp_host_free", "shp_host_register",
            "shp_host_unregister", "shp_snapshot", "shp_restore", "shp_snapshot_describe", "shp_shard_workspace_bytes",
@@ -81,6 +81,7 @@ def lib():
         L.shp_fetch_matches.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpMatches)]
         L.shp_advance_clock.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ShpMatches)]
         L.shp_engine_num_states.argtypes = [ctypes.c_void_p]
+        L.shp_engine_state_stream.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         L.shp_engine_path.argtypes = [ctypes.c_void_p]
         L.shp_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.shp_last_kernel_ms.restype = ctypes.c_double
@@ -269,6 +270,12 @@ class HipEngine:
     @property
     def path(self):
         return lib().shp_engine_path(self.h)
+
+    @property
+    def state_streams(self):
+        """shp_engine_state_stream per state: the receiver (program stream index) of each state, in
+        MetaStateEvent order."""
+        return [lib().shp_engine_state_stream(self.h, s) for s in range(self.S)]
 
     def _check(self, rc):
         if rc != 0:

@@ -1,0 +1,237 @@
+"""CPU checks of the Java (Panama FFM) binding under java/ -- there is no JDK in this image, so the
+sources are checked as text against the C header compiled with gcc and against the program the
+library lowers:
+
+* ShpNative.java's struct layouts (CONFIG, BATCH, MATCHES: field list, padding, size) and the CFG_*
+  offsets GpuStateStreamRuntime fills shp_config by, against offsetof/sizeof of include/siddhi_hip.h;
+* every symbol a downcall handle names is declared in the header, and every ShpNative handle the
+  other Java files use exists;
+* GpuStateStreamRuntime returns one SingleStreamRuntime per state (the reference's query builder
+  indexes getSingleStreamRuntimes() by state, QueryParserHelper.java:161-167), built from
+  shp_engine_state_stream;
+* the state numbering of every lowered fixture app is the reference's MetaStateEvent order: the
+  order StateInputStreamParser.parse reaches the stream states (Next: current then next,
+  StateInputStreamParser.java:227-262; Logical: the second operand first, :336-351; Every and
+  Count: their inner state), and each state's stream is the one it reads -- the map the Java side
+  pairs receivers and MetaStreamEvents by (ProgramInfo.stateStream, shp_engine_state_stream).
+"""
+import json
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from golden_runner import load_fixtures
+from siddhi_amd import native, synth
+from siddhi_amd.query.compiler import Dictionary, QueryCompiler
+from siddhi_amd.query.siddhiql import parse_app
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JAVA = os.path.join(ROOT, "java", "io", "siddhi", "core", "query", "input", "stream", "state", "gpu")
+SIZES = {"JAVA_INT": (4, 4), "JAVA_LONG": (8, 8), "ADDRESS": (8, 8), "JAVA_DOUBLE": (8, 8), "JAVA_SHORT": (2, 2),
+         "JAVA_BYTE": (1, 1)}
+
+
+def _java(name):
+    return open(os.path.join(JAVA, name)).read()
+
+
+def _struct_layouts(src):
+    """{LAYOUT: [(field or None for padding, offset, size)], total size} from ShpNative's
+    MemoryLayout.structLayout(...) declarations (natural alignment, as the FFM linker requires)."""
+    out = {}
+    for name, body in re.findall(r"static final StructLayout (\w+) = MemoryLayout\.structLayout\((.*?)\);", src, re.S):
+        fields, off, align = [], 0, 1
+        for m in re.finditer(r"(JAVA_\w+|ADDRESS)\.withName\(\"(\w+)\"\)|MemoryLayout\.paddingLayout\((\d+)\)", body):
+            if m.group(3):
+                n = int(m.group(3))
+                fields.append((None, off, n))
+                off += n
+                continue
+            sz, al = SIZES[m.group(1)]
+            assert off % al == 0, f"{name}.{m.group(2)} misaligned at {off}"
+            fields.append((m.group(2), off, sz))
+            off += sz
+            align = max(align, al)
+        assert off % align == 0, f"{name}: size {off} not a multiple of {align}"
+        out[name] = (fields, off)
+    return out
+
+
+def _c_offsets(structs):
+    """offsetof/sizeof of the header's structs, compiled with gcc."""
+    body = []
+    for st, fs in structs.items():
+        body.append(f'printf("{st} %zu", sizeof({st}));')
+        for f in fs:
+            body.append(f'printf(" {f}=%zu", offsetof({st}, {f}));')
+        body.append('printf("\\n");')
+    src = ("#include <stdio.h>\n#include <stddef.h>\n#include \"siddhi_hip.h\"\nint main(void){" + "".join(body)
+           + "return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "l")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", exe, c])
+        lines = subprocess.check_output([exe]).decode().strip().split("\n")
+    res = {}
+    for line in lines:
+        parts = line.split()
+        res[parts[0]] = (int(parts[1]), {k: int(v) for k, v in (p.split("=") for p in parts[2:])})
+    return res
+
+
+LAYOUT_STRUCT = {"CONFIG": "shp_config", "BATCH": "shp_batch", "MATCHES": "shp_matches"}
+
+
+def test_shpnative_struct_layouts_match_the_header():
+    lay = _struct_layouts(_java("ShpNative.java"))
+    assert set(LAYOUT_STRUCT) <= set(lay)
+    want = _c_offsets({LAYOUT_STRUCT[k]: [f for f, _, _ in lay[k][0] if f] for k in LAYOUT_STRUCT})
+    for jname, cname in LAYOUT_STRUCT.items():
+        fields, size = lay[jname]
+        csize, coff = want[cname]
+        assert size == csize, (jname, size, csize)
+        named = [(f, o) for f, o, _ in fields if f]
+        assert [f for f, _ in named] == list(coff), (jname, [f for f, _ in named], list(coff))
+        for f, o in named:
+            assert o == coff[f], f"{jname}.{f}: Java offset {o}, C offsetof {coff[f]}"
+    # the sizes the Javadoc comments state
+    src = _java("ShpNative.java")
+    for jname, cname in LAYOUT_STRUCT.items():
+        m = re.search(r"/\*\* struct " + cname + r" \((\d+) bytes\)", src)
+        assert m and int(m.group(1)) == want[cname][0], cname
+
+
+def test_config_is_filled_by_header_offsets():
+    src = _java("ShpNative.java")
+    consts = {k: int(v) for k, v in re.findall(r"CFG_(\w+) = (\d+)", src)}
+    want = _c_offsets({"shp_config": [k.lower() for k in consts]})["shp_config"][1]
+    assert consts and {k.lower(): v for k, v in consts.items()} == want
+    rt = _java("GpuStateStreamRuntime.java")
+    sets = re.findall(r"cfg\.set\((JAVA_\w+), ([^,]+),", rt)
+    assert len(sets) == 8
+    for typ, off in sets:  # every field written by its named offset, never a literal
+        assert off.startswith("ShpNative.CFG_"), off
+        field = off[len("ShpNative.CFG_"):].lower()
+        assert field in want
+        assert SIZES[typ][0] == (8 if field in ("max_batch", "max_matches", "start_clock") else 4), (typ, field)
+
+
+def test_downcalls_name_declared_symbols():
+    from test_abi import declared_symbols
+    src = _java("ShpNative.java")
+    named = set(re.findall(r"fn(?:Void)?\(\"(shp_\w+)\"", src))
+    assert named, "no downcalls found"
+    missing = named - set(declared_symbols())
+    assert not missing, missing
+    handles = set(re.findall(r"static final MethodHandle (\w+) =", src))
+    for f in os.listdir(JAVA):
+        if f.endswith(".java") and f != "ShpNative.java":
+            used = set(re.findall(r"ShpNative\.([A-Z][A-Z0-9_]+)\.invokeExact", _java(f)))
+            assert used <= handles, (f, used - handles)
+
+
+def test_runtime_builds_one_single_stream_runtime_per_state():
+    rt = _java("GpuStateStreamRuntime.java")
+    body = rt[rt.index("GpuStateStreamRuntime(String appText, String queryName, ProgramInfo info"):]
+    loop = re.search(r"for \(int st = 0; st < numStates; st\+\+\) \{(.*?)\n            \}", body, re.S)
+    assert loop, "no per-state loop in the constructor"
+    text = loop.group(1)
+    assert "ShpNative.STATE_STREAM.invokeExact(eng, st)" in text
+    assert "singleStreamRuntimes.add(new SingleStreamRuntime(receivers[s]" in text
+    assert "metaStateEvent.getMetaStreamEvent(st)" in text
+    # one receiver per stream, shared by the states that read it
+    assert "if (receivers[s] == null)" in text
+    assert rt.count("singleStreamRuntimes.add(") == 1
+
+
+def _reference_state_order(tree):
+    """State ids in the order StateInputStreamParser.parse adds their MetaStreamEvents."""
+    t = tree["t"]
+    if t in ("stream", "absent", "count"):
+        return [tree["state"]]
+    if t == "next":
+        return _reference_state_order(tree["a"]) + _reference_state_order(tree["b"])
+    if t == "every":
+        return _reference_state_order(tree["x"])
+    if t == "logical":  # getStreamStateElement2 is parsed before getStreamStateElement1
+        return _reference_state_order(tree["s2"]) + _reference_state_order(tree["s1"])
+    raise AssertionError(f"unknown tree node {t}")
+
+
+def _reader(p, node_state_streams):
+    """ProgramInfo.parse's per-state map, restated: state id -> stream, ref, count state."""
+    st = {s["id"]: (s["stream"], s["ref"]) for s in p["states"]}
+    multi = set()
+
+    def walk(n):
+        if isinstance(n, dict):
+            if n.get("t") == "count":
+                multi.add(n["state"])
+            for v in n.values():
+                walk(v)
+    walk(p["tree"])
+    return [(st[i][0], st[i][1], i in multi) for i in range(len(st))]
+
+
+def _programs():
+    seen = set()
+    apps = [fx["app"] for fx in load_fixtures()] + list(synth.QUERIES.values())
+    for app_text in apps:
+        if app_text in seen:
+            continue
+        seen.add(app_text)
+        try:
+            app = parse_app(app_text)
+        except Exception:  # noqa: BLE001 (apps outside the state path's grammar)
+            continue
+        d = Dictionary()
+        for q in app.queries:
+            try:
+                yield app, q, json.loads(QueryCompiler(app, q, d).compile().program_json())
+            except Exception:  # noqa: BLE001 (queries the lowering rejects: the host keeps the reference)
+                break
+
+
+def test_state_numbering_is_the_reference_meta_order():
+    n = 0
+    for app, q, p in _programs():
+        order = _reference_state_order(p["tree"])
+        assert order == list(range(len(p["states"]))), (q.name, order)
+        streams = [s["name"] for s in p["streams"]]
+        for sid, (stream, ref, multi) in enumerate(_reader(p, None)):
+            assert 0 <= stream < len(streams)
+        n += 1
+    assert n >= 200
+
+
+def test_state_stream_map_for_c2_and_c4():
+    """C2: two states on one stream (two SingleStreamRuntimes, one receiver); C4: the logical
+    element's second operand is state 0 (S2), so state order differs from stream order."""
+    progs = {}
+    for key in (2, 4):
+        _, qs, _ = __import__("siddhi_amd.query.compiler", fromlist=["compile_app"]).compile_app(synth.QUERIES[key])
+        progs[key] = json.loads(qs[0].program_json())
+    assert [s for s, _, _ in _reader(progs[2], None)] == [0, 0]
+    assert [s for s, _, _ in _reader(progs[4], None)] == [1, 0, 2]
+    assert [r for _, r, _ in _reader(progs[4], None)] == ["e2", "e1", None]
+
+
+@pytest.mark.gpu
+def test_engine_state_stream_matches_the_program():
+    """shp_engine_state_stream (what GpuStateStreamRuntime calls) on every lowered fixture query."""
+    checked = 0
+    for app, q, p in _programs():
+        try:
+            eng = native.HipEngine(json.dumps(p), 0, max_keys=64, max_batch=256)
+        except native.ShpError:
+            continue
+        try:
+            assert eng.state_streams == [s for s, _, _ in _reader(p, None)], q.name
+            checked += 1
+        finally:
+            eng.close()
+    assert checked >= 150
