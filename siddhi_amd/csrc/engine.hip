@@ -894,6 +894,16 @@ struct shp_engine {
       }
       if (sz.size() < 5) return fail(SHP_ERR_ARG, "snapshot layout mismatch");
       const int64_t pc = (int64_t)(sz[sz.size() - 5] / 8);
+      // validate the whole blob against the layout it implies before anything changes: a
+      // rejected blob leaves the committed pool (and everything else) as it was
+      auto want = state_sections();
+      if ((size_t)h.sections != want.size() || sizeof h + (size_t)h.payload != len || sz.size() != want.size())
+        return fail(SHP_ERR_ARG, "snapshot layout mismatch");
+      static const size_t pool_elem[5] = {8, 8, 4, 1, 1};  // the pool's ts, seq, value, local key, null
+      for (size_t i = 0; i < want.size(); i++) {
+        const size_t exp = i + 5 >= want.size() ? (size_t)pc * pool_elem[i + 5 - want.size()] : want[i].bytes;
+        if (sz[i] != exp) return fail(SHP_ERR_ARG, "snapshot section size mismatch");
+      }
       HIP_OK(hipStreamSynchronize(stream));
       sw.pool_exact(sw.D.cur, pc);
     }
@@ -1062,14 +1072,17 @@ struct shp_engine {
         const int64_t* p_ts = (const int64_t*)sp[s0 + 3];
         const int64_t* p_seq = (const int64_t*)sp[s0 + 4];
         const uint8_t* p_lk = (const uint8_t*)sp[s0 + 6];
+        const int64_t npool = (int64_t)(secs[s0 + 3].bytes / 8);
         for (int32_t ow = 0; ow < nown; ow++) {
           if (spl[ow] && spn[ow] >= 0) {  // a spilled owner: its open candidates are in the pool
+            if (spb[ow] < 0 || spb[ow] + spn[ow] > npool) throw std::runtime_error("snapshot pool segment out of range");
             for (int64_t i = 0; i < spn[ow]; i++) {
               const int64_t c = spb[ow] + i;
               const int32_t k = inv[(size_t)ow * SW_LK + p_lk[c]];
               if (k >= 0) open[k].push_back({p_seq[c], p_ts[c]});
             }
           } else {
+            if (c_n[ow] < 0 || c_n[ow] > SWS_CCAP) throw std::runtime_error("snapshot carry count out of range");
             for (int i = 0; i < c_n[ow]; i++) {
               const int64_t c = (int64_t)ow * SWS_CCAP + i;
               const int32_t k = inv[(size_t)ow * SW_LK + c_lk[c]];

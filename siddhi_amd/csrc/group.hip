@@ -703,28 +703,44 @@ int gather_impl(shp_group& g, int root, shp_matches* out) {
   if (root < 0 || root >= G) return g.fail(SHP_ERR_ARG, "root outside the group");
   const int S = shp_engine_num_states(g.L[0].eng);
   std::vector<shp_matches> dm(g.nlocal);
-  std::vector<int64_t> mine(3 * (size_t)g.nlocal);
+  // per local rank: records, refs, layout, and its status -- a rank whose records cannot be
+  // prepared reports it through the all-gather instead of returning early, so no rank is left
+  // waiting in the collectives below: every rank sees every status and all fail together
+  std::vector<int64_t> mine(4 * (size_t)g.nlocal);
+  std::string why;
   for (int i = 0; i < g.nlocal; i++) {
     int64_t nr = 0;
     const int rc = shp_engine_device_records(g.L[i].eng, &dm[i], &nr);
-    if (rc != SHP_OK) return g.fail(rc, "rank " + std::to_string(g.L[i].rank) + ": " + shp_last_error(g.L[i].eng));
-    mine[3 * i] = dm[i].m;
-    mine[3 * i + 1] = nr;
-    mine[3 * i + 2] = dm[i].layout;
+    if (rc != SHP_OK && why.empty()) why = "rank " + std::to_string(g.L[i].rank) + ": " + shp_last_error(g.L[i].eng);
+    mine[4 * i] = rc == SHP_OK ? dm[i].m : 0;
+    mine[4 * i + 1] = rc == SHP_OK ? nr : 0;
+    mine[4 * i + 2] = rc == SHP_OK ? dm[i].layout : 0;
+    mine[4 * i + 3] = rc;
   }
-  std::vector<int64_t> all(3 * (size_t)G);
+  std::vector<int64_t> all4(4 * (size_t)G);
   if (g.rccl) {
     shp_group::Local& l = g.L[0];
     GH(hipSetDevice(l.dev));
     DevBuf a, b;
-    a.ensure(3 * 8);
-    b.ensure((size_t)G * 3 * 8);
-    GH(hipMemcpyAsync(a.p, mine.data(), 3 * 8, hipMemcpyHostToDevice, l.s));
-    GN(ncclAllGather(a.p, b.p, 3, ncclInt64, g.comm, l.s));
-    GH(hipMemcpyAsync(all.data(), b.p, all.size() * 8, hipMemcpyDeviceToHost, l.s));
+    a.ensure(4 * 8);
+    b.ensure((size_t)G * 4 * 8);
+    GH(hipMemcpyAsync(a.p, mine.data(), 4 * 8, hipMemcpyHostToDevice, l.s));
+    GN(ncclAllGather(a.p, b.p, 4, ncclInt64, g.comm, l.s));
+    GH(hipMemcpyAsync(all4.data(), b.p, all4.size() * 8, hipMemcpyDeviceToHost, l.s));
     GH(hipStreamSynchronize(l.s));
   } else {
-    all = mine;
+    all4 = mine;
+  }
+  for (int r = 0; r < G; r++)
+    if (all4[4 * r + 3] != SHP_OK)
+      return g.fail((int)all4[4 * r + 3], why.empty() ? "rank " + std::to_string(r) + " could not prepare its matches" : why);
+  std::vector<int64_t> all(3 * (size_t)G);
+  for (int r = 0; r < G; r++)
+    for (int k = 0; k < 3; k++) all[3 * r + k] = all4[4 * r + k];
+  for (int i = 0; i < g.nlocal; i++) {
+    mine[3 * i] = mine[4 * i];
+    mine[3 * i + 1] = mine[4 * i + 1];
+    mine[3 * i + 2] = mine[4 * i + 2];
   }
   const bool agg = all[2] == SHP_LAYOUT_AGG;
   std::vector<int64_t> mb(G + 1, 0), rb(G + 1, 0);

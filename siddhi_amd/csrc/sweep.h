@@ -1854,6 +1854,9 @@ struct SweepState {
     if (B.nulls[0]) D.maybe_null = 1;
     D.nst = (int32_t)((B.n + st_len - 1) / st_len);
     (void)hipMemsetAsync(D.tsmax, 0, 2 * sizeof(unsigned long long), s);
+    // overflow flags describe this push only: flags a failed push left must not be promoted to
+    // spilled owners by a later push's SWE_SPILL re-run
+    (void)hipMemsetAsync(D.ovf, 0, (size_t)D.nown, s);
     size_t nc = (size_t)D.nown * D.nst + 1;
     kt.mark("sw_count", s);
     k_sw_count<<<D.nst, SW_THREADS, 0, s>>>(D, B, key, err);
@@ -1979,7 +1982,10 @@ struct SweepState {
     for (uint8_t x : f) n += x ? 1 : 0;
     return n;
   }
-  // the push's overflowing owners become spilled in the committed state (the push then re-runs)
+  // the push's overflowing owners become spilled in the committed state (the push then re-runs).
+  // If the re-run fails, they stay marked: that changes no state a later push or a snapshot reads
+  // (sp_n = -1 keeps their carry in the c_* arrays, where describe() and every solve read it), only
+  // which kernel solves them -- k_sw_spill, exact for every owner -- until spill_settle clears it
   void mark_spilled(hipStream_t s) {
     k_sw_mark_spilled<<<(unsigned)((D.nown + 255) / 256), 256, 0, s>>>(D);
     D.spill_on = 1;

@@ -115,6 +115,31 @@ def test_spilled_owner_snapshot_restore():
     assert opens > 3000
 
 
+def test_rejected_restore_leaves_spilled_state():
+    """A truncated blob, and one whose pool sections disagree with each other, are rejected before
+    anything changes: the engine holding a spilled owner (its carry in the HBM pool) then goes on
+    exactly as the oracle (restore used to resize the pool before validating)."""
+    from siddhi_amd.native import ShpError
+    cq = _cq(_app())
+    ts, key, v = _falling_stream(200, 30_000, 3, hot=(11,), fall=5000)
+    cut = 3000 + 4000
+    eng = _eng(cq, 200, 1 << 15, max_matches=1 << 18)
+    first = _push_all(eng, ts[:cut], key[:cut], v[:cut], 2_500)
+    assert eng.stat("spilled_owners") >= 1
+    blob = eng.snapshot()
+    for bad in (blob[:-1], blob[:-9] + blob[-8:], blob + b"\0"):
+        with pytest.raises(ShpError):
+            eng.restore(bad)
+    assert eng.stat("spilled_owners") >= 1
+    want = _push_all(OracleEngine(cq.program_json(), 0), ts, key, v, 2_500)
+    rest = _push_all(eng, ts[cut:], key[cut:], v[cut:], 2_500)
+    got = {}
+    for part in (first, rest):
+        for k, recs in part.items():
+            got.setdefault(k, []).extend(recs)
+    assert compare(want, got) is None, compare(want, got)
+
+
 def test_spill_with_device_average():
     """C5's selector (avg over e2's value) folded on a spilled owner in emission order."""
     from siddhi_amd.native import LAYOUT_AGG
