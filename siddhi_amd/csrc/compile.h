@@ -42,6 +42,9 @@ class ProgramCompiler {
       if (!agg_fn) throw CompileError(-2, "aggregate: avg, sum, count, min or max");
       agg_state = a.present("state") ? (int)a.get("state").i() : -1;
       agg_col = a.present("column") ? (int)a.get("column").i() : -1;
+      P.aggFn = (int8_t)agg_fn;
+      P.aggState = (int8_t)agg_state;
+      P.aggCol = (int8_t)agg_col;
     }
     P.type = root.get("type").sv == "sequence" ? SEQUENCE : PATTERN;
     P.within = root.get("within").i();

@@ -373,10 +373,16 @@ struct shp_engine {
     if ((cfg.match_layout == SHP_LAYOUT_PAIRS || cfg.match_layout == SHP_LAYOUT_PAIRS32) && fast != 2)
       throw CompileError(-2, "match_layout PAIRS / PAIRS32 needs the sweep path");
     if (cfg.match_layout == SHP_LAYOUT_AGG) {
-      // the aggregate reads e2's value: the sweep's single predicate column (count: none)
-      const bool col_ok = comp.agg_fn == 3 || (comp.agg_state == 1 && comp.agg_col == 0 && comp.P.ncol == 1);
-      if (fast != 2 || !comp.agg_fn || !col_ok)
-        throw CompileError(-2, "match_layout AGG needs the sweep path and an avg/sum/count over e2's filtered column");
+      // the sweep folds an aggregate of e2's value (its single predicate column; count: none);
+      // the general lanes fold one over any state's column at emission (nfa_lane.h aggregate()),
+      // so every other shape -- the count-sequence and logical-absent ones included -- runs its
+      // aggregate there
+      if (!comp.agg_fn) throw CompileError(-2, "match_layout AGG: the query's select has no device aggregate");
+      const bool arg_ok = comp.agg_fn == 3 || (comp.agg_state >= 0 && comp.agg_state < comp.P.nstates &&
+                                               comp.agg_col >= 0 && comp.agg_col < comp.P.ncol);
+      if (!arg_ok) throw CompileError(-2, "match_layout AGG: the aggregate's argument is not a state's column");
+      const bool sweep_ok = comp.agg_fn == 3 || (comp.agg_state == 1 && comp.agg_col == 0 && comp.P.ncol == 1);
+      if (fast != 2 || !sweep_ok) fast = 0;
     } else if (cfg.match_layout != SHP_LAYOUT_FULL && cfg.match_layout != SHP_LAYOUT_PAIRS &&
                cfg.match_layout != SHP_LAYOUT_PAIRS32) {
       throw CompileError(-1, "unknown match_layout");
@@ -728,7 +734,8 @@ struct shp_engine {
       if (herr & SWE_MONO) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state scan kernels");
       if (herr & SWE_RANGE)
         return fail(SHP_ERR_UNSUPPORTED, "timestamps of one push (and the carried candidates) span 2^49 ms or more");
-      if (herr & SWE_AGGNULL) return fail(SHP_ERR_UNSUPPORTED, "null value in the aggregated column (match_layout AGG)");
+      if ((herr & SWE_AGGNULL) || (fast == 0 && (herr & E_AGGNULL)))
+        return fail(SHP_ERR_UNSUPPORTED, "null value in the aggregated column (match_layout AGG)");
       if (herr & SWE_P32)
         return fail(SHP_ERR_UNSUPPORTED, "a match spans 2^32 or more events (match_layout PAIRS32; use PAIRS)");
       return fail(SHP_ERR_CAPACITY, "per-key table capacity exceeded (code " + std::to_string(herr) + ")");

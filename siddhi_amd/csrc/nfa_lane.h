@@ -38,7 +38,7 @@ struct LaneCaps {
 };
 constexpr int LANE_TIERS = 5;
 
-enum LaneErr : int32_t { E_SE = 1, E_ND = 2, E_LIST = 4, E_Q = 8, E_OUT = 16, E_REF = 32 };
+enum LaneErr : int32_t { E_SE = 1, E_ND = 2, E_LIST = 4, E_Q = 8, E_OUT = 16, E_REF = 32, E_AGGNULL = 64 };
 enum PFlag : uint8_t { F_CHANGED = 1, F_INIT = 2, F_STARTED = 4, F_SUCCESS = 8, F_SSRESET = 16, F_INACTIVE = 32 };
 
 struct LaneLayout {
@@ -46,7 +46,7 @@ struct LaneLayout {
   int32_t tier, nse, nn, lcap, qcap, pad_;  // the capacity tier (LaneCaps) the layout is built for
   int64_t o_se_ts, o_se_slot, o_se_type, o_nd_seq, o_nd_ts, o_nd_val, o_nd_next, o_nd_null;
   int64_t o_se_used, o_nd_used, o_lst_len, o_lst, o_pflags, o_lsched, o_larr, o_ret, o_q, o_qhead, o_qlen;
-  int64_t o_kinit, o_err, bytes;
+  int64_t o_kinit, o_err, o_agg, bytes;
   // the field table (offset, elements per lane, element bytes), for copying one lane's state
   // between two layouts (k_nfa_lanes_lds)
   int32_t nf;
@@ -91,6 +91,7 @@ struct LaneLayout {
     f(o_qlen, MAXQ, 2);
     f(o_kinit, 1, 1);
     f(o_err, 1, 4);
+    f(o_agg, 2, 8);  // the key's selector aggregate (SHP_LAYOUT_AGG): value / sum, count
     bytes = o;
   }
 };
@@ -667,6 +668,45 @@ struct LaneT {
       O.slot_len[mi * MAXS + s] = (int16_t)lens[s];
       for (int nd = slot(se, s); nd >= 0; nd = nnext(nd)) O.refs[r++] = nseq(nd);
     }
+    if (P.aggFn && O.agg) O.agg[mi] = aggregate(se);
+  }
+
+  // The selector's running aggregate of this key over its matches in emission order
+  // (QuerySelector.processInBatchNoGroupBy :271-313, one output per match; per partition key
+  // its own state, AttributeAggregatorExecutor.initAggregator :43-60), folded as the match is
+  // emitted: AvgAttributeAggregatorExecutor (`value += x; count++`, value / count), Sum, Count,
+  // Min / MaxAttributeAggregatorExecutor (first value, then `if (value > x) value = x`).  A null
+  // argument leaves the state and returns the current value (processAdd :110-115); a result that
+  // is itself null (no value yet) flags E_AGGNULL and the push fails, as on the sweep.
+  SHP_HD double aggregate(int se) {
+    double& a = at<double>(Y.o_agg, 0);  // avg / sum: the sum; min / max: the value (NaN: first was NaN)
+    double& c = at<double>(Y.o_agg, 1);  // values folded (count: matches)
+    const int fn = P.aggFn;
+    if (fn == 3) {
+      c += 1.0;
+      return c;
+    }
+    Res R{this, se};
+    const Val v = R.value(P.aggState, 0, P.aggCol);
+    if (v.tag != T_NULL) {
+      double x;
+      if (v.tag == T_FLOAT) x = (double)bits_f(v.bits);
+      else if (v.tag == T_DOUBLE) x = bits_d(v.bits);
+      else x = (double)v.bits;  // int / long (exact to 2^53, as the sweep's double state)
+      if (fn <= 2) {
+        a += x;
+      } else if (c == 0.0) {
+        a = x;
+      } else if (!(a != a) && x == x) {
+        a = fn == 4 ? (a > x ? x : a) : (a < x ? x : a);
+      }
+      c += 1.0;
+    }
+    if (c == 0.0) {
+      err |= E_AGGNULL;
+      return 0.0;
+    }
+    return fn == 1 ? a / c : a;
   }
 
   // ------------------------------------------------------------ timers

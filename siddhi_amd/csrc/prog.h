@@ -93,6 +93,10 @@ struct DevProg {
   int8_t colPos[MAXCOL];
   int8_t streamNcol[MAXSTREAM];
   int8_t streamCols[MAXSTREAM][NV];
+  // select-side aggregate folded at emission (SHP_LAYOUT_AGG on the general lanes): 0 none, 1 avg,
+  // 2 sum, 3 count, 4 min, 5 max, over the value of state aggState (first event of its chain: the
+  // selector's default index 0) in predicate column aggCol
+  int8_t aggFn, aggState, aggCol, pad5;
   Instr code[MAXCODE];
 };
 

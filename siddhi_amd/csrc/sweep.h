@@ -1673,8 +1673,9 @@ struct SweepState {
     // about two keys: one rank of a key-sharded job holds K/N keys (1250 of C2's 10k at N=8),
     // and K/N/20 owners would leave most CUs without a solve workgroup
     static const int minown = getenv("SHP_SW_MINOWN") ? std::max(1, atoi(getenv("SHP_SW_MINOWN"))) : SW_MIN_OWN;
+    static const int prefown = getenv("SHP_SW_PREFOWN") ? std::max(1, atoi(getenv("SHP_SW_PREFOWN"))) : SW_PREF_OWN;
     while (nown < SW_MAXOWN &&
-           (((int64_t)nown * kpo < max_keys && (nown < SW_PREF_OWN || (int64_t)nown * 200 < max_keys)) ||
+           (((int64_t)nown * kpo < max_keys && (nown < prefown || (int64_t)nown * 200 < max_keys)) ||
             (nown < minown && (int64_t)nown * 2 <= max_keys)))
       nown *= 2;
     for (;;) {
@@ -1888,8 +1889,8 @@ struct SweepState {
   }
 
   // does this push run k_sw_lean (so SWE_LEAN may come back and ask for solve())?
-  // (SHP_LAYOUT_AGG: avg / sum / count fold in k_sw_lean; min / max on k_sw_solve)
-  bool lean_push() const { return lean_opc && D.agg <= 3 && !D.maybe_null; }
+  // (SHP_LAYOUT_AGG: every selector aggregate -- avg / sum / count / min / max -- folds in k_sw_lean)
+  bool lean_push() const { return lean_opc && D.agg <= 5 && !D.maybe_null; }
   bool lean_push_for(const BatchView& B) const { return lean_push() && !B.nulls[0]; }
   // k_sw_win (sweep_win.h): the pair layouts of the lean shape, no spilled owner
   bool win_push_for(const BatchView& B) const {

@@ -93,9 +93,10 @@ __device__ __forceinline__ int sl_probe(const int2* tv, int qb, int end, int32_t
 
 __device__ __forceinline__ uint32_t sl_closes(uint32_t c) { return (uint32_t)__popc(c & 0xFFFFFFu) + (c >> 24); }
 
-// AGG: SHP_LAYOUT_AGG with avg / sum / count (D.agg 1..3) -- the selector's running aggregate per
-// match (QuerySelector.processInBatchNoGroupBy, AvgAttributeAggregatorExecutor: `value += x;
-// count++`) in place of the pairs; min / max stay on k_sw_solve
+// AGG: SHP_LAYOUT_AGG -- the selector's running aggregate per match
+// (QuerySelector.processInBatchNoGroupBy) in place of the pairs: avg / sum / count (D.agg 1..3;
+// AvgAttributeAggregatorExecutor: `value += x; count++`) and, since round 4, min / max (D.agg 4 / 5;
+// MinAttributeAggregatorExecutor.java:126-130, bit-exact with k_sw_solve's fold)
 template <int CT, int OPC, bool AGG = false>
 __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView B, MatchOut O, int* err) {
   using T = typename SwTy<CT>::T;
@@ -282,6 +283,84 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       clk = __shfl(lk, 63, 64);
     }
   };
+  // AGG with min / max (D.agg 4 / 5; MinAttributeAggregatorExecutor / Max...: value = first value,
+  // then `if (value > x) value = x`): a segmented wave scan of k_sw_solve's fold (best non-NaN
+  // value, count, first value was NaN) over the closing positions; every match of q outputs the
+  // fold after q's value (folding the same value again changes nothing).  The per-key state in
+  // ag[] is (value -- NaN when the first value was NaN, 0 before any --, count), as k_sw_solve keeps it.
+  auto emit_mm = [&](int PS, int PE, bool MAX) {
+    const unsigned long long gb = S.gbase + S.wb[w];
+    const double ident = MAX ? -INFINITY : INFINITY;
+    auto best = [&](double a, double b) { return MAX ? (a < b ? b : a) : (a > b ? b : a); };  // a folded first
+    double cm = ident, cn = 0;   // the running fold at the end of the previous 64-block
+    int cfn = 0;
+    uint32_t clk = 0xFFFFFFFFu;  // ... and its key
+    for (int g0 = PS; g0 < PE; g0 += 64) {
+      const int q = g0 + (int)lane;
+      const bool v = q < PE;
+      const uint32_t lk = v ? (S.meta[q] & 0xFFu) : 0xFFFFu;
+      const uint32_t c = v ? sl_closes(S.cl[q]) : 0u;
+      const uint32_t vb = v ? (uint32_t)S.tv[q].y : 0u;
+      const double x = CT == 1 ? (double)__uint_as_float(vb) : (double)(int32_t)vb;
+      const uint32_t lkp = __shfl_up(lk, 1, 64);
+      const bool head = lane == 0 || lk != lkp;
+      double m = ident, n = 0;
+      int fn = 0;
+      if (head && v) {  // the key's fold before this block: carried from the previous block or from ag[]
+        if (lane == 0 && lk == clk) {
+          m = cm;
+          n = cn;
+          fn = cfn;
+        } else {
+          const double sv = ag[lk];
+          n = ag[256 + lk];
+          fn = n > 0 && sv != sv;
+          m = (n > 0 && !fn) ? sv : ident;
+        }
+      }
+      if (c) {  // fold q's value once, count its c matches
+        if (n == 0) {
+          fn = x != x;
+          m = fn ? ident : x;
+        } else if (x == x) {
+          m = best(m, x);
+        }
+        n += (double)c;
+      }
+      int f = head ? 1 : 0;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const double ym = __shfl_up(m, d, 64), yn = __shfl_up(n, d, 64);
+        const int yfn = __shfl_up(fn, d, 64), yf = __shfl_up(f, d, 64);
+        if (lane >= (uint32_t)d && !f) {
+          m = best(ym, m);
+          fn = yn > 0 ? yfn : fn;
+          n = yn + n;
+        }
+        if (lane >= (uint32_t)d) f |= yf;
+      }
+      if (c) {
+        const int32_t kid = D.inv[(int64_t)o * SW_LK + lk];
+        const double val = fn ? __longlong_as_double(0x7ff8000000000000ll) : m;
+        const uint64_t s0l = gb + (uint32_t)S.tv[q].x;
+        for (uint32_t r = 0; r < c; r++) {
+          const uint64_t slot = s0l + r;
+          if (slot < (uint64_t)O.cap) {
+            O.key[slot] = kid;
+            O.agg[slot] = val;
+          }
+        }
+      }
+      if (v && (q + 1 >= PE || (S.meta[q + 1] & 0xFFu) != lk)) {  // the run's end: the key's new state
+        ag[lk] = n == 0 ? 0.0 : (fn ? __longlong_as_double(0x7ff8000000000000ll) : m);
+        ag[256 + lk] = n;
+      }
+      cm = __shfl(m, 63, 64);
+      cn = __shfl(n, 63, 64);
+      cfn = __shfl(fn, 63, 64);
+      clk = __shfl(lk, 63, 64);
+    }
+  };
   int pPS = 0, pPE = 0, pcur = 0;  // this wave's range of the previous chunk, and its carry buffer
 #ifdef SHP_SW_STAMPS  // diagnostic build: wave cycles per phase (barrier waits count in the phase before)
   unsigned long long stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -325,8 +404,12 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     // threads take the same branch)
     if (S.flag) break;
     if (cb != rb) {  // the previous chunk's matches
-      if constexpr (AGG) emit_agg(pPS, pPE);
-      else emit(pPS, pPE, pcur);
+      if constexpr (AGG) {
+        if (D.agg >= 4) emit_mm(pPS, pPE, D.agg == 5);
+        else emit_agg(pPS, pPE);
+      } else {
+        emit(pPS, pPE, pcur);
+      }
     }
     SL_STAMP(1);
     const int E = S.cn[cur] + nchunk;
@@ -610,8 +693,12 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     if (tid == 0) atomicOr(err, SWE_LEAN);
     return;
   }
-  if constexpr (AGG) emit_agg(pPS, pPE);  // the last chunk's matches
-  else emit(pPS, pPE, pcur);
+  if constexpr (AGG) {  // the last chunk's matches
+    if (D.agg >= 4) emit_mm(pPS, pPE, D.agg == 5);
+    else emit_agg(pPS, pPE);
+  } else {
+    emit(pPS, pPE, pcur);
+  }
 #ifdef SHP_SW_STAMPS
   SL_STAMP(1);
   {

@@ -510,6 +510,36 @@ def test_c5_aggregate_at_100k_keys():
     assert sum(len(v) for v in want.values()) > 500_000
 
 
+@pytest.mark.parametrize("fn", ["min", "max"])
+def test_c5_minmax_at_100k_keys_on_lean(fn):
+    """C5's shape with min / max (round 4: folded in k_sw_lean, no longer k_sw_solve) at 100k keys:
+    every push on the lean kernel, and every value bitwise equal to the reference fold
+    (MinAttributeAggregatorExecutor.java:126-130) over the oracle's matches."""
+    from siddhi_amd.native import LAYOUT_AGG
+    cq = compile_app_q(_agg_app(fn))
+    g = small_stream(5, 2_000_000, 100_000)
+    a = run(OracleEngine(cq.program_json(), 0), cq, g)
+    want = _expected_agg(a, columns_for(cq, g)[0], fn)
+    eng = hip(0, max_keys=100_000, max_batch=1 << 20, match_layout=LAYOUT_AGG)(cq.program_json(), 0)
+    assert eng.path == 2
+    b = run(eng, cq, g, 700_001)
+    assert eng.stat("lean_pushes") == eng.stat("pushes") == 3 and eng.stat("lean_fallbacks") == 0
+    got = {}
+    for k, v in zip(b["key"], b["agg"]):
+        got.setdefault(int(k), []).append(float(v))
+    assert set(got) == set(want)
+    for k in want:
+        w, h = np.array(want[k]), np.array(got[k])
+        assert len(w) == len(h), k
+        assert (w.view(np.uint64) == h.view(np.uint64)).all(), k
+    assert sum(len(v) for v in want.values()) > 500_000
+
+
+def compile_app_q(app):
+    from siddhi_amd.query.compiler import compile_app
+    return compile_app(app)[1][0]
+
+
 @pytest.mark.parametrize("within", ["6 days", "30 days"])
 def test_long_within_at_many_keys_vs_oracle(within):
     """`within` longer than the sweep's 2^29 ms probe span (30 days) must not take the sweep
