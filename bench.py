@@ -74,7 +74,9 @@ def parse():
     ap.add_argument("--same-device", action="store_true",
                     help="N>1 rehearsal on a one-GPU box without torchrun: one process, an in-process group of "
                          "--gpus ranks all on cuda:0 (device copies stand in for RCCL)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03_s3_pmc_traffic.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic_c2.json"),
+                    help="PMC traffic per kernel (tools/pmc_run.sh); used only when it was measured on this "
+                         "library build (lib_sha16), this config and key count")
     ap.add_argument("--latency-batches", type=int, default=200,
                     help="§8d latency: batches of --latency-events, push + D2H of the match payload (0: skip)")
     ap.add_argument("--latency-events", type=int, default=16_000_000)
@@ -252,15 +254,25 @@ def main():
         m_per_launch = m_total / G / a.steps
         alg_bytes = BYTES_PER_EVENT * ev_per_launch + BYTES_PER_MATCH[layout] * m_per_launch
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = step_traffic = None
+        pmc_src = None
         if os.path.exists(a.pmc):
             try:
                 pm = json.load(open(a.pmc))
-                # PMC passes are of one bench command (tools/pmc_run.sh): its config only
-                if str(pm.get("config", "2")) == str(cfg_id) and int(pm.get("keys", K)) == K and G == 1:
-                    traffic = pm.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+                # PMC passes are of one bench command (tools/pmc_run.sh) on one library build: used
+                # only for that config, key count and build (the same .so as this run loaded)
+                if (str(pm.get("config", "2")) == str(cfg_id) and int(pm.get("keys", K)) == K and G == 1
+                        and pm.get("lib_sha16") == _lib_sha16(native.LIB_PATH)):
+                    ks = pm.get("kernels", {})
+                    traffic = ks.get(dom, {}).get("hbm_bytes_per_launch")
+                    # the whole push: every kernel of the run but the input generator and the
+                    # one-time state initialisation (one launch each per push)
+                    step_traffic = sum(v["hbm_bytes_per_launch"] for k, v in ks.items()
+                                       if k not in ("synth", "sw_init", "labs_init", "cseq_init", "fast_init", "iota")
+                                       and not k.startswith("__amd_rocclr"))
+                    pmc_src = os.path.relpath(a.pmc, ROOT)
             except Exception:
-                traffic = None
+                traffic = step_traffic = None
         cpu = None
         if not a.no_cpu_baseline and G == 1:
             cpu = cpu_baseline(cq, a.cpu_sample, K, spec.config, a.cpu_threads)
@@ -312,7 +324,10 @@ def main():
                 "kernel_ms_per_launch": {k: v / a.steps for k, v in sorted(kernel_ms.items()) if v > 0},
                 # the same algorithmic bytes over the whole step (every kernel of the push, plus the
                 # host round trip), the fraction the headline `value` corresponds to
-                "step": {"achieved": step_achieved, "frac": step_achieved / HBM_PEAK_GBS, "ms": step_ms},
+                "step": {"achieved": step_achieved, "frac": step_achieved / HBM_PEAK_GBS, "ms": step_ms,
+                         "traffic": step_traffic,
+                         "traffic_x": (step_traffic / alg_bytes) if step_traffic else None},
+                "traffic_source": pmc_src,
             },
             "cpu_baseline": cpu,
         }
@@ -389,6 +404,14 @@ def batch_latency(eng, L, native, spec, K, layout, n, batches, start):
             "host_buffer": "page-locked (shp_host_alloc)",
             "pageable_p50_ms": float(np.percentile(pg, 50)), "pageable_p99_ms": float(np.percentile(pg, 99)),
             "what": "shp_push_batch_device entry -> match payload in host memory"}
+
+
+def _lib_sha16(path):
+    import hashlib
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
 
 
 def _sweep_shape(cq, device, keys):

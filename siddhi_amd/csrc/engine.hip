@@ -846,7 +846,7 @@ struct shp_engine {
     snap.assign(sizeof(SnapHeader) + payload, 0);
     SnapHeader h{};
     memcpy(h.magic, "SHPSNAP1", 8);
-    h.version = 3;
+    h.version = 4;  // 4: round 4's owner map (sw_owner / sw_local: low / high bits of the key id)
     h.path = fast;
     h.max_keys = cfg.max_keys;
     h.seq = seq;
@@ -873,7 +873,7 @@ struct shp_engine {
     SnapHeader h;
     if (!buf || len < sizeof h) return fail(SHP_ERR_ARG, "snapshot too short");
     memcpy(&h, buf, sizeof h);
-    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 3) return fail(SHP_ERR_ARG, "not a snapshot (or of another version)");
+    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 4) return fail(SHP_ERR_ARG, "not a snapshot (or of another version)");
     if (h.path != fast || h.max_keys != cfg.max_keys || h.program_hash != fnv1a(program))
       return fail(SHP_ERR_ARG, "snapshot is of a different query, path or key capacity");
     if (fast == 0 && (h.pad < 0 || h.pad >= LANE_TIERS)) return fail(SHP_ERR_ARG, "snapshot capacity tier unknown");
@@ -952,7 +952,7 @@ struct shp_engine {
     SnapHeader h;
     if (!buf || len < sizeof h) throw std::runtime_error("snapshot too short");
     memcpy(&h, buf, sizeof h);
-    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 3 || h.path != fast || h.max_keys != cfg.max_keys ||
+    if (memcmp(h.magic, "SHPSNAP1", 8) != 0 || h.version != 4 || h.path != fast || h.max_keys != cfg.max_keys ||
         h.program_hash != fnv1a(program))
       throw std::runtime_error("not a snapshot of this engine's query, path and key capacity");
     LaneLayout Yb = Y;  // lanes: the layout of the snapshot's capacity tier

@@ -155,8 +155,8 @@ struct SweepDev {
   int64_t st_len;
   int32_t cur;           // which copy of the double-buffered per-owner state the next push reads
   int32_t f1ct;          // e1's filter in the scatter: typed compare class (1 float, 2 int; 0 generic doubles)
-  const uint8_t* lk8;    // key -> local key id within its owner (the owner is sw_owner(key))
-  int32_t lk_lds;        // scatter stages lk8 in LDS (max_keys <= SW_LKTAB)
+  const uint8_t* lk8;    // unused since round 4 (the local key is sw_local(key)); kept null
+  int32_t lk_lds;
   uint32_t* cnt;         // nown * nst + 1: counts, scanned into off
   uint32_t* off;
   SwRec* recs;           // batch capacity
@@ -339,10 +339,14 @@ __device__ __forceinline__ void sw_conv(uint32_t v, bool isfloat, double& f, dou
   }
 }
 
-// key -> owner: Fibonacci hashing (build_map uses the same function, so owners need no table)
+// key -> owner: the low bits of the dense dictionary id, and the local key its high bits (round 4;
+// rounds 1-3 hashed the id onto the owner and looked the local key up in a table, a byte load per
+// event that the 100k-key C5 took from L2).  Dictionary ids are dense (shp_dict, and k / N on rank
+// k % N of a key-sharded group), so every owner gets max_keys / nown keys, one more at most.
 __host__ __device__ __forceinline__ uint32_t sw_owner(uint32_t k, int bits) {
-  return bits == 0 ? 0u : (k * 2654435769u) >> (32 - bits);
+  return bits == 0 ? 0u : (k & ((1u << bits) - 1u));
 }
+__host__ __device__ __forceinline__ uint32_t sw_local(uint32_t k, int bits) { return k >> bits; }
 
 __device__ __forceinline__ uint64_t sw_match_peers(uint32_t bin, int bits, bool valid) {
   uint64_t peers = __ballot(valid);
@@ -455,22 +459,16 @@ static __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, Batc
 // ------------------------------------------------------------------ pass 2: stable scatter by owner
 static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchView B, const int32_t* __restrict__ key,
                                                            int* err) {
-  // dynamic LDS: per-wave counts (then write cursors) [SWP_WAVES][nown], running owner offsets
-  // [nown], and (lk_lds) the key -> local key table
+  // dynamic LDS: per-wave counts (then write cursors) [SWP_WAVES][nown] and the running owner
+  // offsets [nown]
   extern __shared__ uint32_t sw_dyn[];
   const int nown = D.nown;
   uint32_t* grun = sw_dyn + SWP_WAVES * nown;
-  uint8_t* lkt = (uint8_t*)(grun + nown);
   const int st = blockIdx.x;
   const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
   uint32_t* wcw = sw_dyn + w * nown;
   const uint64_t lt = sw_lanemask_lt();
   for (int b = threadIdx.x; b < nown; b += SWP_THREADS) grun[b] = D.off[(int64_t)b * D.nst + st];
-  if (D.lk_lds) {
-    const uint32_t* src = (const uint32_t*)D.lk8;
-    for (int b = threadIdx.x; b < (D.maxkeys + 3) / 4; b += SWP_THREADS) ((uint32_t*)lkt)[b] = src[b];
-  }
-  const uint8_t* lkq = D.lk_lds ? (const uint8_t*)lkt : D.lk8;
   const int64_t lo = (int64_t)st * D.st_len, hi = min(B.n, lo + D.st_len);
   const int64_t base = B.n > 0 ? B.ts[0] : 0;
   const uint32_t* vcol = (const uint32_t*)B.cols[0];
@@ -505,7 +503,7 @@ static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, B
     }
     uint32_t lk[SWP_SUB];
 #pragma unroll
-    for (int s = 0; s < SWP_SUB; s++) lk[s] = kk[s] >= 0 ? lkq[kk[s] & 0x3fffffff] : 0u;
+    for (int s = 0; s < SWP_SUB; s++) lk[s] = kk[s] >= 0 ? sw_local((uint32_t)(kk[s] & 0x3fffffff), D.own_bits) : 0u;
 #pragma unroll
     for (int s = 0; s < SWP_SUB; s++) {
       const bool valid = kk[s] >= 0;
@@ -1685,10 +1683,9 @@ struct SweepState {
       int bits = 0;
       while ((1 << bits) < nown) bits++;
       for (int32_t k = 0; k < max_keys; k++) {
-        // Fibonacci hashing: consecutive ids, and any arithmetic progression of ids (the keys
-        // one rank of a key-sharded job sees), spread evenly over the owners
-        uint32_t o = sw_owner((uint32_t)k, bits);
-        int32_t lk = nloc[o]++;
+        const uint32_t o = sw_owner((uint32_t)k, bits);
+        const int32_t lk = (int32_t)sw_local((uint32_t)k, bits);
+        nloc[o]++;
         mx = std::max(mx, lk + 1);
         kmap[k] = o | ((uint32_t)lk << 16);
       }
@@ -1735,19 +1732,13 @@ struct SweepState {
     nst_max = (int32_t)std::max<int64_t>(1, (cap + st_len - 1) / st_len);
     D.st_len = st_len;
     {
-      std::vector<uint8_t> l8((size_t)(max_keys + 3) / 4 * 4, 0);
-      for (int32_t k = 0; k < max_keys; k++) {
-        if ((kmap[k] & 0xffffu) != sw_owner((uint32_t)k, D.own_bits))
-          throw std::runtime_error("sweep: key map disagrees with sw_owner");
-        l8[k] = (uint8_t)(kmap[k] >> 16);
-      }
-      uint8_t* lk = nullptr;
-      al(lk, (int64_t)l8.size());
-      if (hipMemcpy(lk, l8.data(), l8.size(), hipMemcpyHostToDevice) != hipSuccess)
-        throw std::runtime_error("hipMemcpy failed (sweep key map)");
-      D.lk8 = lk;
-      D.lk_lds = (int64_t)(SWP_WAVES + 1) * nown * 4 + (int64_t)l8.size() <= SW_LKTAB;
-      const size_t lds = (size_t)(SWP_WAVES + 1) * nown * 4 + (D.lk_lds ? l8.size() : 0);
+      for (int32_t k = 0; k < max_keys; k++)
+        if ((kmap[k] & 0xffffu) != sw_owner((uint32_t)k, D.own_bits) ||
+            (kmap[k] >> 16) != sw_local((uint32_t)k, D.own_bits))
+          throw std::runtime_error("sweep: key map disagrees with sw_owner / sw_local");
+      D.lk8 = nullptr;
+      D.lk_lds = 0;
+      const size_t lds = (size_t)(SWP_WAVES + 1) * nown * 4;
       if (lds > 65536 &&
           hipFuncSetAttribute((const void*)k_sw_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
               hipSuccess)
@@ -1865,7 +1856,7 @@ struct SweepState {
     size_t tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.cnt, D.off, 0u, nc, rocprim::plus<uint32_t>(), s);
     kt.mark("sw_scatter", s);
-    const size_t lds = (size_t)(SWP_WAVES + 1) * D.nown * 4 + (D.lk_lds ? (size_t)(D.maxkeys + 3) / 4 * 4 : 0);
+    const size_t lds = (size_t)(SWP_WAVES + 1) * D.nown * 4;
     k_sw_scatter<<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
     last_win = false;
     if (win_push_for(B)) {

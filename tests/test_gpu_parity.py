@@ -102,8 +102,8 @@ def test_c2_10k_keys_fast_path_vs_oracle():
 
 @pytest.mark.parametrize("keys", [300, 9_000, 200_000])
 def test_sweep_key_counts_vs_oracle(keys):
-    """Sweep at key counts that change its owner layout: few owners, the key -> local key table
-    in LDS (scatter), and the table read from global memory (too many keys for LDS)."""
+    """Sweep at key counts that change its owner layout: few owners (300 keys), ~18 keys per
+    owner, and ~100 keys per owner (200k keys: local key ids past 64 in the owner's table)."""
     cq = program_for(2)
     g = small_stream(2, 600_000, keys)
     a = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
@@ -362,8 +362,10 @@ def test_device_aggregate_rejects_other_shapes():
     from siddhi_amd.native import LAYOUT_AGG, ShpError
     with pytest.raises(ShpError):
         hip(0, max_keys=300, match_layout=LAYOUT_AGG)(program_for(2).program_json(), 0)  # no aggregate
-    with pytest.raises(ShpError):
-        hip(1, max_keys=300, match_layout=LAYOUT_AGG)(program_for(5).program_json(), 0)  # lanes path
+    # round 4: the general lanes fold aggregates too (tests/test_lanes_agg.py), so C5 forced onto
+    # them is accepted rather than rejected
+    e = hip(1, max_keys=300, match_layout=LAYOUT_AGG)(program_for(5).program_json(), 0)
+    assert e.path == 0
 
 
 FUNC_APPS = [

@@ -34,13 +34,24 @@ def per_kernel(d: str, counter: str):
     return {k: v[0] / max(1, len(v[1])) for k, v in acc.items()}
 
 
+def lib_sha16():
+    """The library the passes measured (bench.py reports the traffic only for the same build)."""
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.environ.get("SIDDHI_HIP_DIAG_LIB") or os.path.join(root, "siddhi_amd", "libsiddhi_hip.so")
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def main():
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
     out = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
                      "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 read correction)",
            "config": os.environ.get("PMC_CONFIG", "2"), "keys": int(os.environ.get("PMC_KEYS", "10000")),
-           "kernels": {}}
+           "lib_sha16": lib_sha16(), "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f, w = fetch.get(k, 0.0), write.get(k, 0.0)
         out["kernels"][k] = {"fetch_kb": f, "write_kb": w, "hbm_bytes_per_launch": (2 * f + w) * 1024}
