@@ -35,11 +35,12 @@ BYTES_PER_EVENT = 16    # ts 8 + key 4 + price 4
 BYTES_PER_MATCH = {"pairs32": 8,  # (e2 batch index, e2 seq - e1 seq) as two u32 (SHP_LAYOUT_PAIRS32)
                    "pairs": 16,  # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
                    "agg": 12,    # (key u32, aggregate f64) per match (SHP_LAYOUT_AGG, C5)
+                   "chain32": 4,  # e2 batch index | L << 28, the e1 chain implied (SHP_LAYOUT_CHAIN32, C3')
                    "full": 16}
 KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_win", "sw_win_tail", "sw_lean", "sw_solve", "sw_spill", "sw_expand",
            "radix_sort", "clock_scan", "key_hist", "key_scan", "sort_keys", "iota", "clamp_clock",
            "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry", "nfa_lanes",
-           "cseq_count", "cseq_scan", "cseq", "cs_pack", "cs_sort", "cs_count", "cs_scan", "cs_emit", "cs_state", "labs_pack", "labs_sort", "labs_gather", "labs_count", "labs_scan", "labs", "labs_pos", "labs_out",
+           "cseq_count", "cseq_scan", "cseq", "co_count", "co_scan", "co_scatter", "co_run", "cs_pack", "cs_sort", "cs_count", "cs_scan", "cs_emit", "cs_state", "labs_pack", "labs_sort", "labs_gather", "labs_count", "labs_scan", "labs", "labs_pos", "labs_out",
            "key_bounds")
 WORKLOADS = {
     "1": "C1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec (one key)",
@@ -82,6 +83,8 @@ def parse():
     ap.add_argument("--latency-events", type=int, default=16_000_000)
     ap.add_argument("--pairs-layout", choices=["pairs32", "pairs"], default="pairs32",
                     help="match payload of the 2-state sweep: 8-byte PAIRS32 (default) or 16-byte PAIRS")
+    ap.add_argument("--cseq-layout", choices=["chain32", "full"], default="chain32",
+                    help="match payload of the count-sequence path (C3'): 4-byte CHAIN32 words (default) or FULL")
     return ap.parse_args()
 
 
@@ -118,8 +121,10 @@ def main():
     force = {"auto": 0, "general": 1, "scan": 2, "labs": 4}[a.path]
     sweep = force == 0 and _sweep_shape(cq, local, K_local)
     layout = ("agg" if "aggregate" in cq.program else a.pairs_layout) if sweep else "full"
+    if cfg_id == "3b" and force == 0:  # the count-sequence path takes C3' by default
+        layout = a.cseq_layout
     mlay = {"agg": native.LAYOUT_AGG, "pairs": native.LAYOUT_PAIRS, "pairs32": native.LAYOUT_PAIRS32,
-            "full": native.LAYOUT_FULL}[layout]
+            "chain32": native.LAYOUT_CHAIN32, "full": native.LAYOUT_FULL}[layout]
     L = native.lib()
     grp = None
     if G == 1:
@@ -302,7 +307,7 @@ def main():
                 "events_per_gpu_per_step": N,
                 "keys": K,
                 "parallelism": par,
-                "engine_path": PATHS.get(eng.path, str(eng.path)),
+                "engine_path": _path_desc(eng, layout),
                 "matches_per_s": m_total / elapsed,
                 "matches_per_step_gpu0": m_per_launch,
                 "p50_batch_ms": float(np.percentile(lat, 50)),
@@ -353,6 +358,20 @@ class _EngineView:
     def kernel_ms(self, which="total"):
         from siddhi_amd import native
         return native.lib().shp_last_kernel_ms(self.h, which.encode())
+
+
+def _path_desc(eng, layout):
+    d = PATHS.get(eng.path, str(eng.path))
+    if eng.path == 3 and layout == "chain32":
+        own = native_stat(eng, "cseq_owner")
+        d = ("count-sequence automaton by owners (owner multisplit + per-owner key order in LDS, cseq_own.h)"
+             if own else d) + ", CHAIN32 words"
+    return d
+
+
+def native_stat(eng, which):
+    from siddhi_amd import native
+    return native.lib().shp_engine_stat(eng.h, which.encode())
 
 
 def batch_latency(eng, L, native, spec, K, layout, n, batches, start):

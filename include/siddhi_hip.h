@@ -57,8 +57,9 @@ typedef struct shp_config {
                               y=Y) -> not Z for T [within W]` (labs.h): needs non-decreasing
                               timestamps per key (a push breaking that fails, engine unchanged). */
   int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
-  int32_t match_layout;    /* SHP_LAYOUT_FULL (0), SHP_LAYOUT_PAIRS (1), SHP_LAYOUT_AGG (2) or
-                              SHP_LAYOUT_PAIRS32 (3); PAIRS, PAIRS32 and AGG need the sweep path */
+  int32_t match_layout;    /* SHP_LAYOUT_FULL (0), SHP_LAYOUT_PAIRS (1), SHP_LAYOUT_AGG (2),
+                              SHP_LAYOUT_PAIRS32 (3) or SHP_LAYOUT_CHAIN32 (4); PAIRS and PAIRS32
+                              need the sweep path, CHAIN32 the count-sequence path */
 } shp_config;
 
 /* Match layouts. FULL: every field of shp_matches is valid. PAIRS (2-state sweep path,
@@ -78,6 +79,14 @@ typedef struct shp_config {
  * value after that match, double), in per-key emission order. The aggregate state per key
  * carries across pushes. Null values in the aggregated column are rejected (SHP_ERR_UNSUPPORTED). */
 #define SHP_LAYOUT_AGG 2
+/* CHAIN32 (count-sequence path, `every e1=S[f1]<1:M>, e2=S[f2]` in a partition): `refs` holds m
+ * uint32 words, word = e2's index in the pushed batch (bits 0-27) | L << 28.  The match's e1 chain
+ * is the L events of e2's partition key immediately before e2 in that key's arrival order (the
+ * pattern is a sequence: CountPreStateProcessor.java:53-95 keeps them consecutive), some possibly
+ * from earlier pushes; the other fields are implied as for PAIRS (type CURRENT, ts / pos of e2,
+ * slot_len {L, 1}).  shp_fetch_matches / shp_group_gather_matches expand to FULL.  Needs
+ * max_batch < 2^28. */
+#define SHP_LAYOUT_CHAIN32 4
 
 /* One batch of events in SoA form. Column c follows program["columns"][c]:
  * int->int32, long->int64, float->float32, double->float64, bool->uint8,
@@ -118,7 +127,7 @@ typedef struct shp_matches {
   const int64_t* ref_off;
   const int16_t* slot_len;
   const int64_t* refs;
-  int32_t layout;          /* SHP_LAYOUT_FULL, SHP_LAYOUT_PAIRS, SHP_LAYOUT_AGG or SHP_LAYOUT_PAIRS32 */
+  int32_t layout;          /* SHP_LAYOUT_FULL, _PAIRS, _AGG, _PAIRS32 or _CHAIN32 */
   const double* agg;       /* SHP_LAYOUT_AGG: the aggregate's value per match */
 } shp_matches;
 

@@ -77,6 +77,7 @@ __device__ __forceinline__ void cs_set_ts(CsRec12& r, int64_t t, int64_t base, b
 struct CseqDev {
   SwPred f1, f2;     // f1: e1 slot = the arriving event; f2: e1 slot = e1[last], e2 slot = the arriving event
   int32_t M, vtag, nk, cur;
+  int32_t ch32, pad0;  // SHP_LAYOUT_CHAIN32: k_cs3's emit writes one word per match (cseq_own.h)
   uint8_t* len[2];   // nk: L
   uint32_t* prev[2]; // nk: the previous event's value bits
   uint8_t* pnull[2]; // nk: ... and whether it was null
@@ -583,7 +584,10 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
         const uint32_t La = cs_at(a ? (em ? t11 : t10) : 0ull, Lb);  // (Lb = 0: T11 and T10 agree)
         const uint32_t k = kl;
         const R rj = sv[j];
-        if (em) {
+        if (em && C.ch32) {  // CHAIN32: e2's batch index | L << 28 (the chain is implied)
+          if (mi >= O.cap) e |= E_OUT;
+          else reinterpret_cast<uint32_t*>(O.refs)[mi] = (rj.g & 0x7FFFFFFFu) | (Lb << 28);
+        } else if (em) {
           const uint32_t rfs = Lb + 1u;
           if (mi >= O.cap || ri + rfs > O.refcap) {
             e |= E_OUT;
@@ -833,6 +837,12 @@ static __global__ void k_cseq_init(CseqDev C) {
   }
 }
 
+}  // namespace shp
+
+#include "cseq_own.h"
+
+namespace shp {
+
 struct CseqState {
   CseqDev D{};
 
@@ -864,8 +874,38 @@ struct CseqState {
 #endif
   }
 
-  void create(const DevProg& P, const CseqShape& s, int32_t max_keys, int64_t batch_cap, int key_bits,
-              hipStream_t st) {
+  // the owner path (cseq_own.h): CHAIN32 pushes whose keys and M fit its per-owner LDS state
+  CoDev P{};
+  bool own = false;
+  uint32_t* ch = nullptr;  // CHAIN32 words staged for the expansion (mcap)
+  int64_t mcap = 0;
+
+  // owners and local keys for nk keys with M history slots: false when they do not fit
+  bool own_plan(int M, int32_t nk) {
+    const int per = 8 + 4 * M;  // value, L / null / ring head / ring fill, the ring
+    int kmax = 1;
+    while (kmax * 2 <= CO_KPO_MAX && kmax * 2 * per <= CO_KEY_LDS) kmax *= 2;
+    const int64_t need = ((int64_t)nk + kmax - 1) / kmax;
+    int64_t nown = 1, pk = 1;
+    while (nown < need) nown *= 2;
+    while (pk < nk) pk *= 2;
+    nown = std::max<int64_t>(nown, std::min<int64_t>(CO_MINOWN, pk));
+    if (const char* o = getenv("SHP_CO_OWN")) {  // A/B: a fixed owner count (a power of two)
+      const int64_t x = atoll(o);
+      if (x > 0 && (x & (x - 1)) == 0 && x * kmax >= nk) nown = x;
+    }
+    if (nown > CO_MAXOWN) return false;
+    P.nown = (int32_t)nown;
+    P.bits = 0;
+    while ((1 << P.bits) < nown) P.bits++;
+    P.kpo = (int32_t)(((int64_t)nk + nown - 1) >> P.bits);
+    P.lkbits = 0;
+    while ((1 << P.lkbits) < P.kpo) P.lkbits++;
+    return true;
+  }
+
+  void create(const DevProg& Pg, const CseqShape& s, int32_t max_keys, int64_t batch_cap, int key_bits,
+              hipStream_t st, bool chain32 = false, int64_t match_cap = 0) {
     cap = std::max<int64_t>(batch_cap, 1);
     al(D.pk, cap);
     al(D.sk, cap);
@@ -885,8 +925,33 @@ struct CseqState {
     sort_records<CsRec12>(nullptr, b3, cap, key_bits, st);
     (void)rocprim::exclusive_scan(nullptr, b2, D.wcm, D.wom, 0u, (size_t)nwmax, rocprim::plus<uint32_t>(), st);
     tmp_bytes = std::max<size_t>(std::max(std::max(b1, b2), b3), 16);
+    D.ch32 = chain32 ? 1 : 0;
+    if (chain32) {
+      mcap = std::max<int64_t>(match_cap, 1);
+      al(ch, mcap);
+      size_t b4 = 0;
+      (void)rocprim::exclusive_scan(nullptr, b4, rocprim::make_transform_iterator((const uint32_t*)ch, ChRefs{}),
+                                    (int64_t*)nullptr, (int64_t)0, (size_t)mcap, rocprim::plus<int64_t>(), st);
+      tmp_bytes = std::max(tmp_bytes, b4);
+      own = getenv("SHP_CO_OFF") == nullptr && own_plan(s.M, max_keys);
+      if (own) {
+        const int64_t nst_max = (cap + CO_STLEN - 1) / CO_STLEN;
+        const int64_t nc = (int64_t)P.nown * nst_max + 1;
+        al(P.cnt, nc);
+        al(P.off, nc);
+        al(P.recs, cap);
+        size_t b5 = 0;
+        (void)rocprim::exclusive_scan(nullptr, b5, P.cnt, P.off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), st);
+        tmp_bytes = std::max(tmp_bytes, b5);
+        const int dyn = (int)co_dyn_bytes(P.kpo, s.M);
+        const void* runs[3] = {(const void*)k_co_run<0>, (const void*)k_co_run<1>, (const void*)k_co_run<2>};
+        for (const void* f : runs)
+          if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, dyn) != hipSuccess)
+            throw std::runtime_error("count-sequence owner path: LDS request refused");
+      }
+    }
     if (hipMalloc(&tmp, tmp_bytes) != hipSuccess) throw std::runtime_error("hipMalloc failed (count-sequence sort)");
-    create_state(P, s, max_keys, st);
+    create_state(Pg, s, max_keys, st);
   }
 
   void create_state(const DevProg& P, const CseqShape& s, int32_t max_keys, hipStream_t st) {
@@ -975,7 +1040,9 @@ struct CseqState {
   // narrow: the 12-byte records (a push beyond their ts range sets CS_WIDE; the engine re-runs it wide)
   void run2(const BatchView& B, const int32_t* key, const int32_t* stream, int key_bits, const MatchOut& O, int* err,
             hipStream_t s, KTimer& kt, bool narrow) {
-    if (narrow)
+    if (own && B.n > 0)
+      run_own(B, key, stream, O, err, s, kt);
+    else if (narrow)
       run2t<CsRec12>(B, key, stream, key_bits, O, err, s, kt);
     else
       run2t<CsRec>(B, key, stream, key_bits, O, err, s, kt);
@@ -1030,6 +1097,60 @@ struct CseqState {
     kt.mark(nullptr, s);
   }
 
+  // the owner path over one push (cseq_own.h): count, scan, scatter, per-owner run
+  void run_own(const BatchView& B, const int32_t* key, const int32_t* stream, const MatchOut& O, int* err,
+               hipStream_t s, KTimer& kt) {
+    const int64_t n = B.n;
+    P.nst = (int32_t)((n + CO_STLEN - 1) / CO_STLEN);
+    if ((int64_t)P.nst * CO_STLEN < n || n > cap) throw std::runtime_error("count-sequence owner path: batch beyond capacity");
+    (void)hipMemsetAsync(D.tsmax, 0, sizeof(unsigned long long), s);
+    kt.mark("co_count", s);
+    k_co_count<<<(unsigned)P.nst, CO_CNT_THREADS, 0, s>>>(P, B, key, stream, (uint32_t)D.nk, D.tsmax, err);
+    kt.mark("co_scan", s);
+    size_t tb = tmp_bytes;
+    (void)rocprim::exclusive_scan(tmp, tb, P.cnt, P.off, 0u, (size_t)P.nown * P.nst + 1, rocprim::plus<uint32_t>(), s);
+    kt.mark("co_scatter", s);
+    const size_t lds = (size_t)(CO_SCT_WAVES + 1) * P.nown * 4;
+    switch (D.f1.n) {
+      case 0: k_co_scatter<0><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream); break;
+      case 1: k_co_scatter<1><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream); break;
+      default: k_co_scatter<2><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream); break;
+    }
+    kt.mark("co_run", s);
+    const size_t dyn = co_dyn_bytes(P.kpo, D.M);
+    switch (D.f2.n) {
+      case 0: k_co_run<0><<<(unsigned)P.nown, CO_THREADS, dyn, s>>>(P, D, B, O, err); break;
+      case 1: k_co_run<1><<<(unsigned)P.nown, CO_THREADS, dyn, s>>>(P, D, B, O, err); break;
+      default: k_co_run<2><<<(unsigned)P.nown, CO_THREADS, dyn, s>>>(P, D, B, O, err); break;
+    }
+    kt.mark(nullptr, s);
+  }
+
+  // CHAIN32 -> FULL for the last push's m words (in O.refs), after its commit: the push's events
+  // sorted by key again (the 16-byte records), each match's refs placed by a scan of L + 1
+  void expand(const BatchView& B, const int32_t* key, const int32_t* stream, int key_bits, const MatchOut& O, int64_t m,
+              int* err, hipStream_t s, KTimer& kt) {
+    if (m <= 0 || B.n <= 0) {
+      (void)hipMemsetAsync(O.count + 1, 0, sizeof(unsigned long long), s);
+      return;
+    }
+    if (m > mcap) throw std::runtime_error("count-sequence expansion: more matches than the staging buffer");
+    const int64_t n = B.n;
+    kt.mark("cs_expand", s);
+    (void)hipMemcpyAsync(ch, O.refs, (size_t)m * 4, hipMemcpyDeviceToDevice, s);
+    const unsigned gp = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    k_cs_pack<CsRec><<<gp, 256, 0, s>>>(B.ts, key, stream, (const uint32_t*)B.cols[0], B.nulls[0], n, B.partitioned,
+                                        (uint32_t)D.nk, D.pk, D.pr, D.tsmax, err);
+    size_t tb = tmp_bytes;
+    sort_records<CsRec>(tmp, tb, n, key_bits, s);
+    tb = tmp_bytes;
+    (void)rocprim::exclusive_scan(tmp, tb, rocprim::make_transform_iterator((const uint32_t*)ch, ChRefs{}), O.ref_off,
+                                  (int64_t)0, (size_t)m, rocprim::plus<int64_t>(), s);
+    const unsigned ge = (unsigned)std::min<int64_t>((m + 255) / 256, 4096);
+    k_cs_expand<CsRec><<<ge, 256, 0, s>>>(D, B, key, D.sk, D.sr, ch, m, D.cur ^ 1, O, err);
+    kt.mark(nullptr, s);
+  }
+
   void commit() { D.cur ^= 1; }
 
   void release() {
@@ -1038,11 +1159,15 @@ struct CseqState {
       for (void* p : ps)
         if (p) (void)hipFree(p);
     }
-    void* qs[] = {D.tsmax, D.cm, D.cr, D.om, D.orf, D.pk, D.sk, D.pr, D.sr, D.ws, D.wcm, D.wcr, D.wom, D.wor, D.kend, tmp};
+    void* qs[] = {D.tsmax, D.cm, D.cr, D.om, D.orf, D.pk, D.sk, D.pr, D.sr, D.ws, D.wcm, D.wcr, D.wom, D.wor, D.kend, tmp,
+                  ch, P.cnt, P.off, P.recs};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = CseqDev{};
+    P = CoDev{};
     tmp = nullptr;
+    ch = nullptr;
+    own = false;
   }
 };
 

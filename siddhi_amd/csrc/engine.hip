@@ -222,6 +222,7 @@ struct shp_engine {
   bool expanded = true;  // sweep matches materialised as full records
   BatchView lastB{};
   const int32_t* lastKey = nullptr;
+  const int32_t* lastStream = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   std::string err;
@@ -372,6 +373,10 @@ struct shp_engine {
     }
     if ((cfg.match_layout == SHP_LAYOUT_PAIRS || cfg.match_layout == SHP_LAYOUT_PAIRS32) && fast != 2)
       throw CompileError(-2, "match_layout PAIRS / PAIRS32 needs the sweep path");
+    if (cfg.match_layout == SHP_LAYOUT_CHAIN32) {
+      if (fast != 3 || cseq_v1) throw CompileError(-2, "match_layout CHAIN32 needs the count-sequence path");
+      if (cfg.max_batch > (int64_t)CH32_G) throw CompileError(-1, "match_layout CHAIN32: max_batch must be below 2^28");
+    }
     if (cfg.match_layout == SHP_LAYOUT_AGG) {
       // the sweep folds an aggregate of e2's value (its single predicate column; count: none);
       // the general lanes fold one over any state's column at emission (nfa_lane.h aggregate()),
@@ -384,7 +389,7 @@ struct shp_engine {
       const bool sweep_ok = comp.agg_fn == 3 || (comp.agg_state == 1 && comp.agg_col == 0 && comp.P.ncol == 1);
       if (fast != 2 || !sweep_ok) fast = 0;
     } else if (cfg.match_layout != SHP_LAYOUT_FULL && cfg.match_layout != SHP_LAYOUT_PAIRS &&
-               cfg.match_layout != SHP_LAYOUT_PAIRS32) {
+               cfg.match_layout != SHP_LAYOUT_PAIRS32 && cfg.match_layout != SHP_LAYOUT_CHAIN32) {
       throw CompileError(-1, "unknown match_layout");
     }
     kt.enabled = cfg.profile_kernels != 0;
@@ -440,7 +445,8 @@ struct shp_engine {
     } else if (fast == 1) {
       fs.create(comp.P, comp.fast, cfg.max_keys, cap, mcap, stream);
     } else if (fast == 3) {
-      cs.create(comp.P, comp.cseq, cfg.max_keys, cfg.max_batch, key_bits, stream);
+      cs.create(comp.P, comp.cseq, cfg.max_keys, cfg.max_batch, key_bits, stream,
+                cfg.match_layout == SHP_LAYOUT_CHAIN32, mcap);
     } else if (fast == 4) {
       la.create(comp.P, comp.labs, cfg.max_keys, mcap, cap, stream);
       if (!labs_v1) la.sort_scratch(cap, key_bits, stream);
@@ -523,6 +529,10 @@ struct shp_engine {
       HIP_OK(hipEventRecord(ev1, stream));
       cs.run2(B, x_key, x_stream, key_bits, O, d_err, stream, kt, !cseq_wide);
       HIP_OK(hipMemcpyAsync(h_tsmax, cs.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+      lastB = B;
+      lastKey = x_key;
+      lastStream = x_stream;
+      expanded = cfg.match_layout != SHP_LAYOUT_CHAIN32;  // CHAIN32: materialised on demand
     } else {
       int gb = (int)std::min<int64_t>((n + 255) / 256, 2048);
       if (gb < 1) gb = 1;
@@ -1222,14 +1232,16 @@ struct shp_engine {
 
   // sweep path, PAIRS layout: materialise the full records of the last push on demand
   void ensure_expanded() {
-    if (fast != 2 || expanded || cfg.match_layout == SHP_LAYOUT_AGG) return;
+    if (expanded || cfg.match_layout == SHP_LAYOUT_AGG || (fast != 2 && fast != 3)) return;
     MatchOut O{mcap, rcap, d_mcount, d_mkey, d_mts, d_mtype, d_mpos, d_moff, d_mslot, d_refs, d_magg};
     HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), stream));
-    sw.expand(lastB, lastKey, O, d_err, stream, kt, last_m);
+    if (fast == 2) sw.expand(lastB, lastKey, O, d_err, stream, kt, last_m);
+    else cs.expand(lastB, lastKey, lastStream, key_bits, O, last_m, d_err, stream, kt);
     int herr = 0;
     HIP_OK(hipMemcpyAsync(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
     if (herr & SWE_BOUND) throw DevError("internal: a match pair names an event outside its push (SWE_BOUND)");
+    if (herr & E_OUT) throw DevError("match refs beyond the engine's ref capacity (CHAIN32 expansion)");
     expanded = true;
   }
 
@@ -1552,6 +1564,7 @@ int64_t shp_engine_stat(const shp_engine* e, const char* which) {
   if (w == "win_pushes") return e->win_pushes;
   if (w == "win_fallbacks") return e->win_fallbacks;
   if (w == "cseq_wide_reruns") return e->cseq_wide_reruns;
+  if (w == "cseq_owner") return e->fast == 3 && e->cs.own ? 1 : 0;  // CHAIN32 pushes on the owner kernels
   if (w == "labs_fallbacks") return e->labs_fallbacks;
   if (w == "spill_reruns") return e->spill_reruns;
   if (w == "spilled_owners") return e->fast == 2 ? e->sw.count_spilled() : 0;

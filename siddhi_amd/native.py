@@ -41,7 +41,7 @@ class ShpConfig(ctypes.Structure):
                 ("force_general", ctypes.c_int32), ("profile_kernels", ctypes.c_int32),
                 ("match_layout", ctypes.c_int32)]
 
-LAYOUT_FULL, LAYOUT_PAIRS, LAYOUT_AGG, LAYOUT_PAIRS32 = 0, 1, 2, 3
+LAYOUT_FULL, LAYOUT_PAIRS, LAYOUT_AGG, LAYOUT_PAIRS32, LAYOUT_CHAIN32 = 0, 1, 2, 3, 4
 
 
 class ShpBatch(ctypes.Structure):
