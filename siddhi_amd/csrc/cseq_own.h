@@ -232,8 +232,9 @@ __host__ __device__ inline size_t co_dyn_bytes(int kpo, int M) {
   return (size_t)CO_WAVES * co_wc_stride(kpo) * 2 + (size_t)kpo * (4 + 4 * (size_t)M + 4);
 }
 
+// (<= 128 VGPRs: two 512-thread workgroups per CU, as their LDS allows)
 template <int NT2>
-__global__ __launch_bounds__(CO_THREADS) void k_co_run(CoDev P, CseqDev C, BatchView B, MatchOut O, int* err) {
+__global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_co_run(CoDev P, CseqDev C, BatchView B, MatchOut O, int* err) {
   __shared__ CoSmem S;
   extern __shared__ uint8_t co_key[];
   const int kpo = P.kpo, M = C.M;
@@ -270,18 +271,22 @@ __global__ __launch_bounds__(CO_THREADS) void k_co_run(CoDev P, CseqDev C, Batch
   const uint64_t lt = sw_lanemask_lt();
   uint32_t* words = reinterpret_cast<uint32_t*>(O.refs);
   int e = 0;
+  // the chunk's records, loaded one chunk ahead (in flight while the previous chunk is solved)
+  CoRec r[CO_SUB];
+#pragma unroll
+  for (int s = 0; s < CO_SUB; s++) {
+    const int64_t i = rb + (int64_t)w * CO_SEG + s * 64 + lane;
+    r[s] = i < re ? P.recs[i] : CoRec{0u, 0u, 0u};
+  }
   for (int64_t c0 = rb; c0 < re; c0 += CO_CHUNK) {
     const int nc = (int)min((int64_t)CO_CHUNK, re - c0);
-    for (int i = lane; i <= kpo; i += 64) wc[w * wst + i] = 0;
+    {
+      uint32_t* z = reinterpret_cast<uint32_t*>(wc + w * wst);  // (wst is even)
+      for (int i = lane; i < (int)(wst >> 1); i += 64) z[i] = 0;
+    }
     __syncthreads();
     // rank: stable within the chunk (waves own consecutive segments, sub-rounds in order)
-    CoRec r[CO_SUB];
     uint32_t lkq[CO_SUB], rk[CO_SUB];
-#pragma unroll
-    for (int s = 0; s < CO_SUB; s++) {
-      const int i = (int)w * CO_SEG + s * 64 + (int)lane;
-      r[s] = i < nc ? P.recs[c0 + i] : CoRec{0u, 0u, 0u};
-    }
 #pragma unroll
     for (int s = 0; s < CO_SUB; s++) {
       const int i = (int)w * CO_SEG + s * 64 + (int)lane;
@@ -327,6 +332,11 @@ __global__ __launch_bounds__(CO_THREADS) void k_co_run(CoDev P, CseqDev C, Batch
       }
     }
     if (tid == 0) S.cl[nc] = 0xffffu;  // run-end sentinel
+#pragma unroll
+    for (int s = 0; s < CO_SUB; s++) {  // the next chunk's records
+      const int64_t i = c0 + CO_CHUNK + (int64_t)w * CO_SEG + s * 64 + lane;
+      r[s] = i < re ? P.recs[i] : CoRec{0u, 0u, 0u};
+    }
     __syncthreads();
     // walk 1: per position f1 / f2 / run start bits, the key's stored L at a run start, and the
     // thread's composed transition table
@@ -342,15 +352,23 @@ __global__ __launch_bounds__(CO_THREADS) void k_co_run(CoDev P, CseqDev C, Batch
       pxn = vnull || (S.cg[p0 - 1] >> 31) != 0;
     }
     uint32_t kprev = p0 > 0 && p0 <= nc ? (S.cl[p0 - 1] & 0x7fffu) : 0xffffu;
+    // the thread's positions in one 16-byte (values, batch indices) and 8-byte (keys) LDS read each
+    static_assert(CO_PER == 4, "vector LDS reads of 4 positions");
+    const uint4 xv4 = reinterpret_cast<const uint4*>(S.cv)[tid];
+    const uint4 xg4 = reinterpret_cast<const uint4*>(S.cg)[tid];
+    const uint2 xl2 = reinterpret_cast<const uint2*>(S.cl)[tid];
+    const uint32_t xv[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
+    const uint32_t xg[4] = {xg4.x, xg4.y, xg4.z, xg4.w};
+    const uint32_t xl[4] = {xl2.x & 0xffffu, xl2.x >> 16, xl2.y & 0xffffu, xl2.y >> 16};
 #pragma unroll
     for (int q = 0; q < CO_PER; q++) {
       const int p = p0 + q;
       if (p >= nc) break;
-      const uint32_t cl = S.cl[p], lk = cl & 0x7fffu;
+      const uint32_t cl = xl[q], lk = cl & 0x7fffu;
       const bool head = p == 0 || lk != kprev;
       kprev = lk;
-      const uint32_t x = S.cv[p];
-      const bool xn = vnull || (S.cg[p] >> 31) != 0;
+      const uint32_t x = xv[q];
+      const bool xn = vnull || (xg[q] >> 31) != 0;
       uint32_t L0 = 0;
       if (head) {
         L0 = sL[lk];
@@ -440,29 +458,35 @@ __global__ __launch_bounds__(CO_THREADS) void k_co_run(CoDev P, CseqDev C, Batch
     // walk 3: the words, and at each run end the key's state after the run
     uint32_t k_ = 0;
     int rs = rs_in;
+    const uint32_t lnext = p0 + CO_PER <= nc ? (S.cl[p0 + CO_PER] & 0x7fffu) : 0xffffu;
 #pragma unroll
     for (int q = 0; q < CO_PER; q++) {
       if (!((vb >> q) & 1u)) break;
       const int p = p0 + q;
       if ((hb >> q) & 1u) rs = p;
       const uint32_t Lb = (lbw >> (4 * q)) & 15u;
-      const uint32_t gq = S.cg[p];
+      const uint32_t gq = xg[q];
       if ((emw >> q) & 1u) {
         const int64_t mi = base + mo + k_;
         k_++;
         if (mi >= O.cap) e |= E_OUT;
         else words[mi] = (gq & 0x7fffffffu) | (Lb << 28);
       }
-      const uint32_t lk = S.cl[p] & 0x7fffu;
-      if ((S.cl[p + 1] & 0x7fffu) != lk) {  // the key's run ends here
+      const uint32_t lk = xl[q] & 0x7fffu;
+      const uint32_t ln = q + 1 < CO_PER ? (p + 1 < nc ? (xl[q + 1 < CO_PER ? q + 1 : q] & 0x7fffu) : 0xffffu) : lnext;
+      if (ln != lk) {  // the key's run ends here
         const int n = p - rs + 1;
         sL[lk] = (uint8_t)((law >> (4 * q)) & 15u);
-        sP[lk] = S.cv[p];
+        sP[lk] = xv[q];
         sN[lk] = (vnull || (gq >> 31) != 0) ? 1 : 0;
         const int h = sRh[lk];
         const int c = min(M, n);
-        for (int i = n - c; i < n; i++) sH[(size_t)((h + i) % M) * kpo + lk] = S.cg[rs + i] & 0x7fffffffu;
-        sRh[lk] = (uint8_t)((h + n) % M);
+        int slot = (h + n - c) % M;  // the ring slot of the run's (n - c)-th event
+        for (int i = n - c; i < n; i++) {
+          sH[(size_t)slot * kpo + lk] = S.cg[rs + i] & 0x7fffffffu;
+          slot = slot + 1 == M ? 0 : slot + 1;
+        }
+        sRh[lk] = (uint8_t)slot;
         sRf[lk] = (uint8_t)min(M, (int)sRf[lk] + n);
       }
     }
