@@ -882,6 +882,7 @@ struct CseqState {
 
   // owners and local keys for nk keys with M history slots: false when they do not fit
   bool own_plan(int M, int32_t nk) {
+    if (M > CO_MAXM) return false;  // (k_co_run's 8-byte transition tables)
     const int per = 8 + 4 * M;  // value, L / null / ring head / ring fill, the ring
     int kmax = 1;
     while (kmax * 2 <= CO_KPO_MAX && kmax * 2 * per <= CO_KEY_LDS) kmax *= 2;

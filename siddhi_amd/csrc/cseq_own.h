@@ -214,6 +214,30 @@ __device__ __forceinline__ uint32_t co_block_scan(uint32_t v, uint32_t* sc, uint
   return pre + x - v;
 }
 
+// Transition tables as 8 bytes (byte i = L after, from L = i), composed with two byte permutes.
+// Every table the automaton makes maps L = 0 and L = M alike (T0, T10, T11 do, so their
+// compositions do), so inputs 0..7 cover M <= 7 and every output value (<= M) is a valid selector
+// of the next composition; the owner path takes M <= 7 (M = 8 runs on the sorted records).
+__device__ __forceinline__ uint64_t co_const(uint32_t c) { return 0x0101010101010101ull * (uint64_t)c; }
+__device__ __forceinline__ uint32_t co_at(uint64_t f, uint32_t i) { return (uint32_t)(f >> (8 * i)) & 0xffu; }
+__device__ __forceinline__ uint64_t co_comp(uint64_t g, uint64_t f) {  // g after f
+  const uint32_t gl = (uint32_t)g, gh = (uint32_t)(g >> 32);
+  const uint32_t lo = __builtin_amdgcn_perm(gh, gl, (uint32_t)f);
+  const uint32_t hi = __builtin_amdgcn_perm(gh, gl, (uint32_t)(f >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ void co_tables(int M, uint64_t& t10, uint64_t& t11) {
+  t10 = t11 = 0;
+  for (int i = 0; i < 8; i++) {
+    const uint64_t a = (i == 0 || i >= M) ? 1u : (uint64_t)(i + 1);  // T10: 0 -> 1, L -> L + 1, M -> 1
+    const uint64_t b = (i == 0 || i == M) ? 1u : 0u;                   // T11: 0 -> 1, M -> 1, else 0
+    t10 |= a << (8 * i);
+    t11 |= b << (8 * i);
+  }
+}
+constexpr uint64_t CO_IDENT = 0x0706050403020100ull;
+constexpr int CO_MAXM = 7;
+
 struct CoSmem {
   uint32_t cv[CO_CHUNK];       // the chunk in key order: value
   uint32_t cg[CO_CHUNK];       // batch index | null << 31
@@ -253,10 +277,8 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   const uint32_t nk = (uint32_t)C.nk;
   const bool vnull = C.vtag == T_NULL, vflt = C.vtag == T_FLOAT;
   uint64_t t10, t11;
-  cs_tables(M, t10, t11);
-  uint64_t ident = 0;
-#pragma unroll
-  for (int i = 0; i <= CSEQ_MAXM; i++) ident |= (uint64_t)i << (4 * i);
+  co_tables(M, t10, t11);
+  const uint64_t ident = CO_IDENT;
   // the owner's keys' state (the previous push)
   for (int lk = tid; lk < kpo; lk += CO_THREADS) {
     const uint32_t k = ((uint32_t)lk << P.bits) | (uint32_t)o;
@@ -388,10 +410,10 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       bb |= (b ? 1u : 0u) << q;
       vb |= 1u << q;
       if (head) {
-        G = cs_tab_const(cs_at(F, L0));
+        G = co_const(co_at(F, L0));
         gs = 1;
       } else {
-        G = cs_comp(F, G);
+        G = co_comp(F, G);
       }
       px = x;
       pxn = xn;
@@ -406,7 +428,7 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       const int yf = __shfl_up(fl, d, 64);
       const int yh = __shfl_up(hmax, d, 64);
       if (lane >= (uint32_t)d) {
-        if (!fl) val = cs_comp(val, y);
+        if (!fl) val = co_comp(val, y);
         fl |= yf;
         hmax = max(hmax, yh);
       }
@@ -420,7 +442,7 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     uint64_t cin = ident;
     int cfl = 0, chm = -1;
     for (uint32_t ww = 0; ww < w; ww++) {
-      cin = S.wf[ww] ? S.wt[ww] : cs_comp(S.wt[ww], cin);
+      cin = S.wf[ww] ? S.wt[ww] : co_comp(S.wt[ww], cin);
       cfl |= S.wf[ww];
       chm = max(chm, S.wh[ww]);
     }
@@ -431,10 +453,10 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       ev = cin;
       rs_in = chm;
     } else {
-      if (!ef) ev = cs_comp(ev, cin);
+      if (!ef) ev = co_comp(ev, cin);
       rs_in = max(rs_in, chm);
     }
-    const uint32_t Lin = cs_at(ev, 0);
+    const uint32_t Lin = co_at(ev, 0);
     // walk 2: L before each position, the closing ones
     uint32_t L = Lin, lm = 0, lbw = 0, law = 0, emw = 0;
 #pragma unroll
@@ -443,7 +465,7 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       const bool head = (hb >> q) & 1u;
       const uint32_t Lb = head ? (L0q >> (4 * q)) & 15u : L;
       const bool a = (ab >> q) & 1u, b = (bb >> q) & 1u;
-      L = cs_at(a ? (b ? t11 : t10) : 0ull, Lb);
+      L = co_at(a ? (b ? t11 : t10) : 0ull, Lb);
       const bool em = Lb > 0 && b;
       lm += em ? 1u : 0u;
       lbw |= Lb << (4 * q);

@@ -464,6 +464,10 @@ class HipGroup:
         e = lib().shp_group_engine(self.h, i)
         return lib().shp_last_kernel_ms(e, which.encode())
 
+    def engine_stat(self, i, which):
+        """shp_engine_stat of local engine i (shp_group_engine)."""
+        return lib().shp_engine_stat(lib().shp_group_engine(self.h, i), which.encode())
+
     def close(self):
         if getattr(self, "h", None):
             lib().shp_group_destroy(self.h)

@@ -34,11 +34,12 @@ def path(request, monkeypatch):
     return request.param
 
 
-def _eng(cq, keys, batch, path):
+def _eng(cq, keys, batch, path, owner_ok=True):
+    """owner_ok: the owner kernels take the shape (M <= 7: their 8-byte transition tables)."""
     from siddhi_amd.native import LAYOUT_CHAIN32, HipEngine
     e = HipEngine(cq.program_json(), 0, max_keys=keys, max_batch=batch, match_layout=LAYOUT_CHAIN32)
     assert e.path == 3
-    assert e.stat("cseq_owner") == (1 if path == "owner" else 0)
+    assert e.stat("cseq_owner") == (1 if path == "owner" and owner_ok else 0)
     return e
 
 
@@ -58,14 +59,14 @@ def test_chain32_c3b_vs_oracle(keys, n, batch, path):
 @pytest.mark.parametrize("M,op,typ", [(1, "<", "float"), (2, ">=", "float"), (3, "==", "int"), (5, "!=", "float"),
                                       (8, "<=", "int"), (5, ">", "int")])
 def test_chain32_shapes_vs_oracle(M, op, typ, path):
-    """Every M (the owner path's ring of M batch indices per key; M = 8 halves its keys per owner)."""
+    """Every M (the owner path's ring of M batch indices per key); M = 8 runs on the sorted records."""
     rng = np.random.default_rng(M * 7 + len(op))
     ts, key, v = _stream(rng, 150_000, 3_000)
     if typ == "int":
         v = np.nan_to_num(v, nan=17).astype(np.int32)
     cq = _cq(_app(M, op, typ))
     want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 40_009)
-    got = _push(_eng(cq, 3_000, 1 << 16, path), ts, key, v, 40_009)
+    got = _push(_eng(cq, 3_000, 1 << 16, path, owner_ok=M <= 7), ts, key, v, 40_009)
     assert compare(want, got) is None, compare(want, got)
     assert sum(len(x) for x in want.values()) > 100
 

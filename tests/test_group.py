@@ -251,6 +251,33 @@ def test_group_world8(cfg, keys, n):
         assert sum(len(v) for v in want.values()) > 1000
 
 
+@pytest.mark.parametrize("gather", [False, True], ids=["fetch", "gather"])
+def test_group_world8_c3b_chain32(gather):
+    """C3' with SHP_LAYOUT_CHAIN32 at world 8: every rank on the count-sequence owner kernels over its
+    dense local keys with global sequence numbers; the words expand to FULL on fetch / on the
+    gather to the root, per key equal to the single-process oracle."""
+    import torch
+    from siddhi_amd.native import LAYOUT_CHAIN32, HipGroup
+    cq = program_for("3b")
+    keys, n = 8000, 240_000
+    g = small_stream(3, n, keys)
+    grp = HipGroup(cq.program_json(), 0, max_keys=keys, max_batch=1 << 17, max_matches=1 << 17,
+                   devices=[0] * 8, match_layout=LAYOUT_CHAIN32)
+    for r in range(8):
+        assert grp.engine_stat(r, "cseq_owner") == 1
+    cols = columns_for(cq, g)
+    parts = []
+    bounds = np.linspace(0, n, 4).astype(np.int64)
+    for p in range(3):
+        grp.push_device(_slices(g, cols, bounds[p], bounds[p + 1], 8, False))
+        parts.append(grp.gather(3) if gather else grp.fetch())
+        torch.cuda.synchronize()
+    grp.close()
+    want, have = per_key(run(OracleEngine(cq.program_json(), 0), cq, g)), per_key(_concat(parts))
+    assert compare(want, have) is None, compare(want, have)
+    assert sum(len(v) for v in want.values()) > 5_000
+
+
 @pytest.mark.parametrize("cfg,root", [(2, 5), (4, 7)], ids=["c2", "c4"])
 def test_group_world8_gather_to_root(cfg, root):
     """shp_group_gather_matches at world 8: every rank's records of each push on the root."""
