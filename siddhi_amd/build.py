@@ -15,7 +15,7 @@ ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libsiddhi_hip.so")
 SRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build_obj")
-HEADERS = ["nfa_lane.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h", "sweep.h", "sweep_lean.h",
+HEADERS = ["nfa_lane.h", "wave_dpp.h", "fastpath.h", "fast_core.h", "prog.h", "compile.h", "jsonv.h", "sweep.h", "sweep_lean.h",
            "sweep_spill.h", "sweep_win.h", "cseq.h", "cseq_own.h", "labs.h"]
 # (object name, source, extra flags): the kernel families are split over units that build in
 # parallel (sweep_solve.hip once per e1 term count), heaviest first

@@ -194,12 +194,7 @@ __global__ __launch_bounds__(CO_SCT_THREADS) void k_co_scatter(CoDev P, CseqDev 
 // exclusive scan of one value per thread over the CO_THREADS threads (sc: CO_WAVES words of LDS)
 __device__ __forceinline__ uint32_t co_block_scan(uint32_t v, uint32_t* sc, uint32_t& total) {
   const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
-  }
+  const uint32_t x = dpp_incl_add(v, lane);
   if (lane == 63) sc[w] = x;
   __syncthreads();
   uint32_t pre = 0;
@@ -422,17 +417,16 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     // scan of the run starts
     uint64_t val = G;
     int fl = gs, hmax = lh;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t y = __shfl_up(val, d, 64);
-      const int yf = __shfl_up(fl, d, 64);
-      const int yh = __shfl_up(hmax, d, 64);
-      if (lane >= (uint32_t)d) {
+    dpp_scan_steps(lane, [&](auto ctl, bool take) {  // DPP moves, no LDS round trips
+      constexpr int C = decltype(ctl)::value;
+      const uint64_t y = dpp64<C>(val);
+      const int yf = (int)dpp32<C>((uint32_t)fl), yh = (int)dpp32<C>((uint32_t)hmax);
+      if (take) {
         if (!fl) val = co_comp(val, y);
         fl |= yf;
         hmax = max(hmax, yh);
       }
-    }
+    });
     if (lane == 63) {
       S.wt[w] = val;
       S.wf[w] = fl;

@@ -904,7 +904,9 @@ int create_impl(shp_group* g, const char* json, const shp_config* cfg, int world
   const shp::DevProg& P = g->comp.P;
   if (!P.partitioned && world > 1) return g->fail(SHP_ERR_UNSUPPORTED, "only partitioned queries shard by key");
   g->need_clock = P.nsched > 0 && P.playback;  // absent-state timers read the playback clock
-  g->need_seq = cfg->match_layout == SHP_LAYOUT_FULL;
+  // global sequence numbers travel with the events where the records name events by seq: FULL, and
+  // CHAIN32 (its words name batch indices; the expansion on fetch / gather maps them through seq)
+  g->need_seq = cfg->match_layout == SHP_LAYOUT_FULL || cfg->match_layout == SHP_LAYOUT_CHAIN32;
   g->has_stream_col = P.nstream > 1;
   g->ncol = P.ncol;
   g->ctag.assign(P.colTag, P.colTag + P.ncol);

@@ -37,6 +37,7 @@
 #include "fastpath.h"
 #include "nfa_lane.h"
 #include "prog.h"
+#include "wave_dpp.h"
 
 namespace shp {
 

@@ -227,7 +227,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   // q's value once more, (S + (r+1) v) / (N + r + 1) for avg -- k_sw_solve's arithmetic.
   auto emit_agg = [&](int PS, int PE) {
     const unsigned long long gb = S.gbase + S.wb[w];
-    double cs = 0, cn = 0;       // the running state at the end of the previous 64-block
+    double cs = 0;               // the running state at the end of the previous 64-block
+    uint32_t cn = 0;
     uint32_t clk = 0xFFFFFFFFu;  // ... and its key
     for (int g0 = PS; g0 < PE; g0 += 64) {
       const int q = g0 + (int)lane;
@@ -238,35 +239,39 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       const double x = CT == 1 ? (double)__uint_as_float(vb) : (double)(int32_t)vb;
       const uint32_t lkp = __shfl_up(lk, 1, 64);
       const bool head = lane == 0 || lk != lkp;
-      double s0 = 0, n0 = 0;
+      double s0 = 0;
+      uint32_t n0 = 0;  // (counts are integers: 32-bit in the scan, one shuffle a step fewer)
       if (head && v) {
         if (lane == 0 && lk == clk) {
           s0 = cs;
           n0 = cn;
         } else {
           s0 = ag[lk];
-          n0 = ag[256 + lk];
+          n0 = (uint32_t)ag[256 + lk];
         }
       }
-      double is = (head ? s0 : 0.0) + (double)c * x, in = (head ? n0 : 0.0) + (double)c;
-      int f = head ? 1 : 0;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const double ys = __shfl_up(is, d, 64), yn = __shfl_up(in, d, 64);
-        const int yf = __shfl_up(f, d, 64);
-        if (lane >= (uint32_t)d && !f) {
+      double is = (head ? s0 : 0.0) + (double)c * x;
+      uint32_t in = (head ? n0 : 0u) + c;
+      uint32_t f = head ? 1u : 0u;
+      dpp_scan_steps(lane, [&](auto ctl, bool take) {  // segmented (sum, count) scan, DPP moves
+        constexpr int C = decltype(ctl)::value;
+        const double ys = dppf64<C>(is);
+        const uint32_t yn = dpp32<C>(in), yf = dpp32<C>(f);
+        if (take && !f) {
           is += ys;
           in += yn;
         }
-        if (lane >= (uint32_t)d) f |= yf;
-      }
-      const double ps = __shfl_up(is, 1, 64), pn = __shfl_up(in, 1, 64);
-      const double es = head ? s0 : ps, en = head ? n0 : pn;  // the key's state before q
+        if (take) f |= yf;
+      });
+      const double ps = __shfl_up(is, 1, 64);
+      const uint32_t pn = __shfl_up(in, 1, 64);
+      const double es = head ? s0 : ps;  // the key's state before q
+      const uint32_t en = head ? n0 : pn;
       if (c) {
-        const int32_t kid = D.inv[(int64_t)o * SW_LK + lk];
+        const int32_t kid = (int32_t)((lk << D.own_bits) | (uint32_t)o);  // (sw_owner / sw_local inverted)
         const uint64_t s0l = gb + (uint32_t)S.tv[q].x;
         for (uint32_t r = 0; r < c; r++) {
-          const double sr = es + (double)(r + 1) * x, nr = en + (double)(r + 1);
+          const double sr = es + (double)(r + 1) * x, nr = (double)(en + r + 1);
           const uint64_t slot = s0l + r;
           if (slot < (uint64_t)O.cap) {
             O.key[slot] = kid;
@@ -276,11 +281,11 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       }
       if (v && (q + 1 >= PE || (S.meta[q + 1] & 0xFFu) != lk)) {  // the run's end: the key's new state
         ag[lk] = is;
-        ag[256 + lk] = in;
+        ag[256 + lk] = (double)in;
       }
-      cs = __shfl(is, 63, 64);
-      cn = __shfl(in, 63, 64);
-      clk = __shfl(lk, 63, 64);
+      cs = wave_last_f64(is);
+      cn = wave_last(in);
+      clk = wave_last(lk);
     }
   };
   // AGG with min / max (D.agg 4 / 5; MinAttributeAggregatorExecutor / Max...: value = first value,
@@ -327,20 +332,21 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         }
         n += (double)c;
       }
-      int f = head ? 1 : 0;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const double ym = __shfl_up(m, d, 64), yn = __shfl_up(n, d, 64);
-        const int yfn = __shfl_up(fn, d, 64), yf = __shfl_up(f, d, 64);
-        if (lane >= (uint32_t)d && !f) {
+      uint32_t f = head ? 1u : 0u, fnu = (uint32_t)fn;
+      dpp_scan_steps(lane, [&](auto ctl, bool take) {  // segmented fold scan, DPP moves
+        constexpr int C = decltype(ctl)::value;
+        const double ym = dppf64<C>(m), yn = dppf64<C>(n);
+        const uint32_t yfn = dpp32<C>(fnu), yf = dpp32<C>(f);
+        if (take && !f) {
           m = best(ym, m);
-          fn = yn > 0 ? yfn : fn;
+          fnu = yn > 0 ? yfn : fnu;
           n = yn + n;
         }
-        if (lane >= (uint32_t)d) f |= yf;
-      }
+        if (take) f |= yf;
+      });
+      fn = (int)fnu;
       if (c) {
-        const int32_t kid = D.inv[(int64_t)o * SW_LK + lk];
+        const int32_t kid = (int32_t)((lk << D.own_bits) | (uint32_t)o);  // (sw_owner / sw_local inverted)
         const double val = fn ? __longlong_as_double(0x7ff8000000000000ll) : m;
         const uint64_t s0l = gb + (uint32_t)S.tv[q].x;
         for (uint32_t r = 0; r < c; r++) {
@@ -355,10 +361,10 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         ag[lk] = n == 0 ? 0.0 : (fn ? __longlong_as_double(0x7ff8000000000000ll) : m);
         ag[256 + lk] = n;
       }
-      cm = __shfl(m, 63, 64);
-      cn = __shfl(n, 63, 64);
-      cfn = __shfl(fn, 63, 64);
-      clk = __shfl(lk, 63, 64);
+      cm = wave_last_f64(m);
+      cn = wave_last_f64(n);
+      cfn = (int)wave_last((uint32_t)fn);
+      clk = wave_last(lk);
     }
   };
   int pPS = 0, pPE = 0, pcur = 0;  // this wave's range of the previous chunk, and its carry buffer
@@ -431,12 +437,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         }
         const uint32_t nk = v ? S.ncar[b] : 0u;
         t += nk;
-        uint32_t x = t;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint32_t y = __shfl_up(x, d, 64);
-          if (lane >= (uint32_t)d) x += y;
-        }
+        const uint32_t x = dpp_incl_add(t, lane);
         const uint32_t pre = run + x - t;
         if (v) {
           S.binoff[b] = pre;
@@ -454,7 +455,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
           const uint64_t mk = __ballot(v && (int64_t)pre * SL_WAVES >= (int64_t)k * E);
           if (mk && psv[k] < 0) psv[k] = __builtin_amdgcn_readlane((int)pre, __ffsll((unsigned long long)mk) - 1);
         }
-        run += __shfl(x, 63, 64);
+        run += wave_last(x);
       }
       if (lane == 0) {
         S.binoff[nb] = run;  // = E
@@ -614,13 +615,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       os += S.m[q] == -2 ? 1u : 0u;
     }
     const uint32_t pk = (cs << 16) | os;
-    uint32_t incl = pk;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d, 64);
-      if (lane >= (uint32_t)d) incl += y;
-    }
-    const uint32_t tot = __shfl(incl, 63, 64);
+    const uint32_t incl = dpp_incl_add(pk, lane);
+    const uint32_t tot = wave_last(incl);
     const uint32_t ctot = tot >> 16, otot = tot & 0xFFFFu;
     int cbase = 0;
     if (lane == 0) {
