@@ -75,8 +75,9 @@ def parse():
     ap.add_argument("--same-device", action="store_true",
                     help="N>1 rehearsal on a one-GPU box without torchrun: one process, an in-process group of "
                          "--gpus ranks all on cuda:0 (device copies stand in for RCCL)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic_c2.json"),
-                    help="PMC traffic per kernel (tools/pmc_run.sh); used only when it was measured on this "
+    ap.add_argument("--pmc", default=None,
+                    help="PMC traffic per kernel (tools/pmc_run.sh, tools/pmc_cfg.sh; default "
+                         "profiles/pmc_traffic_c<config>.json); used only when it was measured on this "
                          "library build (lib_sha16), this config and key count")
     ap.add_argument("--latency-batches", type=int, default=200,
                     help="§8d latency: batches of --latency-events, push + D2H of the match payload (0: skip)")
@@ -90,6 +91,8 @@ def parse():
 
 def main():
     a = parse()
+    if a.pmc is None:
+        a.pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_c{a.config}.json")
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
