@@ -37,6 +37,8 @@ final class ShpNative {
     static final int LAYOUT_PAIRS = 1;
     static final int LAYOUT_AGG = 2;
     static final int LAYOUT_PAIRS32 = 3;
+    /** count-sequence path: one uint32 per match, e2's batch index | L << 28 (include/siddhi_hip.h). */
+    static final int LAYOUT_CHAIN32 = 4;
 
     static final int COMM_ID_BYTES = 128;
 

@@ -235,3 +235,13 @@ def test_engine_state_stream_matches_the_program():
         finally:
             eng.close()
     assert checked >= 150
+
+
+def test_layout_constants_match_the_header():
+    """SHP_LAYOUT_* of include/siddhi_hip.h, ShpNative.LAYOUT_* and siddhi_amd.native.LAYOUT_* agree."""
+    hdr = open(os.path.join(ROOT, "include", "siddhi_hip.h")).read()
+    want = {k: int(v) for k, v in re.findall(r"#define SHP_LAYOUT_(\w+) (\d+)", hdr)}
+    assert set(want) == {"FULL", "PAIRS", "AGG", "PAIRS32", "CHAIN32"}
+    java = {k: int(v) for k, v in re.findall(r"static final int LAYOUT_(\w+) = (\d+);", _java("ShpNative.java"))}
+    assert java == want
+    assert {k: getattr(native, "LAYOUT_" + k) for k in want} == want
