@@ -1112,11 +1112,16 @@ struct CseqState {
     (void)rocprim::exclusive_scan(tmp, tb, P.cnt, P.off, 0u, (size_t)P.nown * P.nst + 1, rocprim::plus<uint32_t>(), s);
     kt.mark("co_scatter", s);
     const size_t lds = (size_t)(CO_SCT_WAVES + 1) * P.nown * 4;
+    const bool pf = !stream && !B.nulls[0] && !getenv_flag_scatter_nopf();
+#define CO_SCT(N)                                                                              \
+  if (pf) k_co_scatter<N, true><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream); \
+  else k_co_scatter<N, false><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream);
     switch (D.f1.n) {
-      case 0: k_co_scatter<0><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream); break;
-      case 1: k_co_scatter<1><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream); break;
-      default: k_co_scatter<2><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream); break;
+      case 0: CO_SCT(0) break;
+      case 1: CO_SCT(1) break;
+      default: CO_SCT(2) break;
     }
+#undef CO_SCT
     kt.mark("co_run", s);
     const size_t dyn = co_dyn_bytes(P.kpo, D.M);
     switch (D.f2.n) {

@@ -110,7 +110,9 @@ static __global__ __launch_bounds__(CO_CNT_THREADS) void k_co_count(CoDev P, Bat
 // ------------------------------------------------------------------ pass 2: stable scatter by owner
 // dynamic LDS: per-wave counts, then write cursors [CO_SCT_WAVES][nown], and the running owner
 // offsets [nown]
-template <int NT1>
+// PF (no stream column, no null bytes): the next round's keys and values are loaded as soon as this
+// round's are consumed (as k_sw_scatter's PF path)
+template <int NT1, bool PF>
 __global__ __launch_bounds__(CO_SCT_THREADS) void k_co_scatter(CoDev P, CseqDev C, BatchView B,
                                                                const int32_t* __restrict__ key,
                                                                const int32_t* __restrict__ stream) {
@@ -127,9 +129,18 @@ __global__ __launch_bounds__(CO_SCT_THREADS) void k_co_scatter(CoDev P, CseqDev 
   const uint8_t* ncol = B.nulls[0];
   const bool vnull = C.vtag == T_NULL, vflt = C.vtag == T_FLOAT;
   const uint32_t nk = (uint32_t)C.nk, mask = (uint32_t)nown - 1u;
+  int32_t pk[PF ? CO_SCT_SUB : 1];
+  uint32_t pv[PF ? CO_SCT_SUB : 1];
+  auto load_round = [&](int64_t r0) {
+#pragma unroll
+    for (int s = 0; s < (PF ? CO_SCT_SUB : 0); s++) {
+      const int64_t i = r0 + (int64_t)w * CO_SCT_SEG + s * 64 + lane;
+      pk[s] = i < hi ? (B.partitioned ? key[i] : 0) : -1;
+      pv[s] = (i < hi && vcol) ? vcol[i] : 0u;
+    }
+  };
+  if (PF) load_round(lo);
   for (int64_t r0 = lo; r0 < hi; r0 += CO_SCT_ROUND) {
-    for (int b = lane; b < nown; b += 64) wcw[b] = 0;
-    __syncthreads();
     CoRec rec[CO_SCT_SUB];
     int32_t kk[CO_SCT_SUB];
     uint8_t nl[CO_SCT_SUB];
@@ -139,7 +150,10 @@ __global__ __launch_bounds__(CO_SCT_THREADS) void k_co_scatter(CoDev P, CseqDev 
       kk[s] = -1;
       nl[s] = 0;
       rec[s].v = 0;
-      if (i < hi && (!stream || stream[i] >= 0)) {
+      if constexpr (PF) {
+        kk[s] = (pk[s] >= 0 && (uint32_t)pk[s] < nk) ? pk[s] : -1;
+        rec[s].v = pv[s];
+      } else if (i < hi && (!stream || stream[i] >= 0)) {
         const int32_t k = B.partitioned ? key[i] : 0;
         kk[s] = (k >= 0 && (uint32_t)k < nk) ? k : -1;  // (out of range: k_co_count flagged it)
         rec[s].v = vcol ? vcol[i] : 0u;
@@ -147,6 +161,9 @@ __global__ __launch_bounds__(CO_SCT_THREADS) void k_co_scatter(CoDev P, CseqDev 
       }
       rec[s].g = (uint32_t)i;
     }
+    if (PF && r0 + CO_SCT_ROUND < hi) load_round(r0 + CO_SCT_ROUND);
+    for (int b = lane; b < nown; b += 64) wcw[b] = 0;
+    __syncthreads();
     uint32_t own[CO_SCT_SUB], rk[CO_SCT_SUB], pc[CO_SCT_SUB], ld[CO_SCT_SUB];
 #pragma unroll
     for (int s = 0; s < CO_SCT_SUB; s++) {
