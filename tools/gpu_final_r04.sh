@@ -1,0 +1,12 @@
+#!/bin/bash
+# GPU box, end of round 4 (after the last library build): C2 kernel stats + PMC traffic
+# (tools/pmc_run.sh -> gpurun_out/pmc.json, keyed to this library's hash), C3' traffic
+# (tools/pmc_cfg.sh), then bench lines with CPU baselines for C2 (default: latency on), C3', C5.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+bash tools/pmc_run.sh > gpurun_out/pmc_run_c2.log 2>&1 || { tail -5 gpurun_out/pmc_run_c2.log; exit 1; }
+CFG=3b KEYS=1000000 NO_LV=1 bash tools/pmc_cfg.sh > gpurun_out/pmc_cfg_3b.log 2>&1 || { tail -5 gpurun_out/pmc_cfg_3b.log; exit 1; }
+cp gpurun_out/pmc.json profiles/pmc_traffic_c2.json
+cp gpurun_out/pmc_3b_traffic.json profiles/pmc_traffic_c3b.json
+CONFIGS="c2 c3b c5" bash tools/gpu_bench_all.sh
