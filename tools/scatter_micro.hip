@@ -12,6 +12,9 @@
 //   5 LDS-staged      full ranking; records and their destinations placed in LDS in owner order,
 //                     then written out by position (a wave's store covers whole owner runs)
 //   6 staged+prefetch 5 with the loads of 4
+//   7 window          full ranking, but each super-tile's records land in its own 1 MB window of the
+//                     output, grouped by owner inside it (owner segments within the window)
+//   8 window+prefetch 7 with the loads of 4
 // Variants 5 / 6 run with PER 8 (4096-event rounds) and PER 4 (2048).  The staged variants are
 // checked against variant 0 (same record at every position).
 #include <hip/hip_runtime.h>
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(T) void k_scatter(const int32_t* __restrict__ key, 
                                                int nst, const uint32_t* __restrict__ off, Rec* __restrict__ out,
                                                unsigned long long* sink) {
   constexpr int ROUND = T * PER, SEG = ROUND / W, SUB = SEG / 64;
-  constexpr bool STAGED = V == 5 || V == 6, PREFETCH = V == 4 || V == 6;
+  constexpr bool STAGED = V == 5 || V == 6, PREFETCH = V == 4 || V == 6 || V == 8, WINDOW = V == 7 || V == 8;
   extern __shared__ uint32_t dyn[];
   __shared__ uint32_t sc[T];
   uint32_t* grun = dyn + W * nown;
@@ -79,9 +82,29 @@ __global__ __launch_bounds__(T) void k_scatter(const int32_t* __restrict__ key, 
   const int st = blockIdx.x;
   const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  for (int b = threadIdx.x; b < nown; b += T) grun[b] = off[(int64_t)b * nst + st];
   const int64_t lo = (int64_t)st * STLEN, hi = min(n, lo + STLEN);
   const int per = (nown + T - 1) / T;  // owners per thread in the staged offset pass
+  if (WINDOW) {  // the tile's owner segments inside its own window [lo, hi): a scan of its counts
+    const int b0 = (int)threadIdx.x * per, b1 = min(nown, b0 + per);
+    uint32_t tsum = 0;
+    for (int b = b0; b < b1; b++) tsum += off[(int64_t)b * nst + st + 1] - off[(int64_t)b * nst + st];
+    sc[threadIdx.x] = tsum;
+    __syncthreads();
+    for (int d = 1; d < T; d <<= 1) {
+      const uint32_t y = threadIdx.x >= (unsigned)d ? sc[threadIdx.x - d] : 0u;
+      __syncthreads();
+      sc[threadIdx.x] += y;
+      __syncthreads();
+    }
+    uint32_t g = (uint32_t)lo + sc[threadIdx.x] - tsum;
+    for (int b = b0; b < b1; b++) {
+      grun[b] = g;
+      g += off[(int64_t)b * nst + st + 1] - off[(int64_t)b * nst + st];
+    }
+    __syncthreads();
+  } else {
+    for (int b = threadIdx.x; b < nown; b += T) grun[b] = off[(int64_t)b * nst + st];
+  }
   unsigned long long acc = 0;
   int32_t pk[SUB];
   int64_t pt[SUB];
@@ -266,7 +289,9 @@ int main(int argc, char** argv) {
                       {"staged 4096", KV(5, 8), lds_base + stage_bytes<4096>()},
                       {"staged 2048", KV(5, 4), lds_base + stage_bytes<2048>()},
                       {"staged+prefetch 4096", KV(6, 8), lds_base + stage_bytes<4096>()},
-                      {"staged+prefetch 2048", KV(6, 4), lds_base + stage_bytes<2048>()}};
+                      {"staged+prefetch 2048", KV(6, 4), lds_base + stage_bytes<2048>()},
+                      {"window", KV(7, 8), lds_base},
+                      {"window+prefetch", KV(8, 8), lds_base}};
   auto launch = [&](const Var& v) {
     void* args[] = {&key, &ts, &val, (void*)&n, (void*)&nown, &bits, (void*)&nst, &off, &out, &sink};
     CK(hipLaunchKernel(v.fn, dim3(nst), dim3(T), args, v.lds, 0));
@@ -298,6 +323,28 @@ int main(int argc, char** argv) {
     int64_t bad = 0;
     for (int64_t j = 0; j < n; j++) bad += a[j].ref != b[j].ref;
     printf("%-22s vs full: %lld records differ\n", vars[i].name, (long long)bad);
+  }
+  for (int i : {9, 10}) {  // window layout: a permutation, owner-grouped and stable inside each tile's window
+    CK(hipMemset(out, 0, n * sizeof(Rec)));
+    launch(vars[i]);
+    CK(hipMemcpy(b.data(), out, n * sizeof(Rec), hipMemcpyDeviceToHost));
+    std::vector<uint8_t> seen(n, 0);
+    int64_t bad = 0;
+    for (int64_t j = 0; j < n; j++) {
+      const uint32_t r = b[j].ref;
+      if (r >= (uint64_t)n || seen[r]) {
+        bad++;
+        continue;
+      }
+      seen[r] = 1;
+      if (r / STLEN != (uint64_t)j / STLEN) bad++;  // stays in its tile's window
+      if (j % STLEN != 0) {
+        const uint32_t p = b[j - 1].ref;
+        const uint32_t op = (uint32_t)hk[p] & (nown - 1), oc = (uint32_t)hk[r] & (nown - 1);
+        if (op > oc || (op == oc && p >= r)) bad++;
+      }
+    }
+    printf("%-22s layout check: %lld bad\n", vars[i].name, (long long)bad);
   }
   return 0;
 }
