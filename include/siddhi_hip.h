@@ -167,9 +167,12 @@ int shp_engine_create_siddhiql(const char* app_text, const char* query_name, shp
 
 /* Host-memory batch: copied to HBM, processed, matches copied back to host memory. */
 int shp_push_batch(shp_engine* e, const shp_batch* in, shp_matches* out);
-/* HBM-resident batch (device pointers); matches stay in HBM (out holds device pointers). */
+/* HBM-resident batch (device pointers); matches stay in HBM (out holds device pointers).  With a
+ * compact layout (PAIRS, PAIRS32, CHAIN32) the batch's device columns (ts, key, stream, seq) must stay
+ * valid until the matches are fetched: shp_fetch_matches / shp_group_gather_matches expand the
+ * compact records from them. */
 int shp_push_batch_device(shp_engine* e, const shp_batch* in, shp_matches* out);
-/* Copy the matches of the last shp_push_batch_device to host memory. */
+/* Copy the matches of the last shp_push_batch_device to host memory (none after shp_restore). */
 int shp_fetch_matches(shp_engine* e, shp_matches* out);
 int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out);
 /* Per-key state of the engine (partial matches, carried candidates, timers, clock, sequence

@@ -944,6 +944,8 @@ struct shp_engine {
     }
     seq = h.seq;
     clock = h.clock;
+    last_m = 0;  // the last push's records belong to the state the restore replaced
+    expanded = true;
     if (fast == 2) {
       sw.D.maybe_null = h.maybe_null;
       sw.D.spill_on = sw.count_spilled() > 0;
