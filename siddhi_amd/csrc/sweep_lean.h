@@ -93,6 +93,28 @@ __device__ __forceinline__ int sl_probe(const int2* tv, int qb, int end, int32_t
 
 __device__ __forceinline__ uint32_t sl_closes(uint32_t c) { return (uint32_t)__popc(c & 0xFFFFFFu) + (c >> 24); }
 
+// One lane per match for a 64-position block of the AGG emission: the block's matches are the
+// consecutive indices [0, T) (lane q's c matches from ex = exclusive scan of c), taken 64 at a time;
+// index t's source lane is the last one whose first index is <= t: each source writes its lane at
+// its first index inside the window (a byte of the wave's scratch), the rest of the window keeps 0,
+// and a max scan fills the gaps (sources increase with the index).  out(t, src, r) writes the match
+// t, the r-th of lane src.  Every lane of the wave calls it (DPP moves, shuffles).
+template <class Out>
+__device__ __forceinline__ void sl_expand_block(volatile uint8_t* scr, uint32_t lane, uint32_t c, uint32_t ex,
+                                                uint32_t T, Out&& out) {
+  for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+    scr[lane] = 0;
+    if (c && ex < t0 + 64u && ex + c > t0) scr[(ex > t0 ? ex : t0) - t0] = (uint8_t)lane;
+    uint32_t j = scr[lane];
+    dpp_scan_steps(lane, [&](auto ctl, bool take) {
+      const uint32_t y = dpp32<decltype(ctl)::value>(j);
+      if (take) j = y > j ? y : j;
+    });
+    const uint32_t sex = (uint32_t)__shfl((int)ex, (int)j, 64);
+    out(t0 + lane, (int)j, t0 + lane - sex, t0 + lane < T);
+  }
+}
+
 // AGG: SHP_LAYOUT_AGG -- the selector's running aggregate per match
 // (QuerySelector.processInBatchNoGroupBy) in place of the pairs: avg / sum / count (D.agg 1..3;
 // AvgAttributeAggregatorExecutor: `value += x; count++`) and, since round 4, min / max (D.agg 4 / 5;
@@ -225,6 +247,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   // pairs): per closing position q in key order, the key's (sum, count) before q by a segmented
   // wave scan (segments = key runs, seeded with the key's state), then q's c matches: the r-th adds
   // q's value once more, (S + (r+1) v) / (N + r + 1) for avg -- k_sw_solve's arithmetic.
+  // the AGG emissions' per-wave scratch: the wave's worklist, idle from its probe to the next one
+  volatile uint8_t* scr = reinterpret_cast<volatile uint8_t*>(S.wl[w]);
   auto emit_agg = [&](int PS, int PE) {
     const unsigned long long gb = S.gbase + S.wb[w];
     double cs = 0;               // the running state at the end of the previous 64-block
@@ -267,17 +291,22 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
       const uint32_t pn = __shfl_up(in, 1, 64);
       const double es = head ? s0 : ps;  // the key's state before q
       const uint32_t en = head ? n0 : pn;
-      if (c) {
-        const int32_t kid = (int32_t)((lk << D.own_bits) | (uint32_t)o);  // (sw_owner / sw_local inverted)
-        const uint64_t s0l = gb + (uint32_t)S.tv[q].x;
-        for (uint32_t r = 0; r < c; r++) {
-          const double sr = es + (double)(r + 1) * x, nr = (double)(en + r + 1);
-          const uint64_t slot = s0l + r;
-          if (slot < (uint64_t)O.cap) {
-            O.key[slot] = kid;
+      const uint32_t cx = dpp_incl_add(c, lane);
+      const uint32_t T = wave_last(cx);
+      if (T) {  // (S + (r+1) x) / (N + r + 1) for the r-th match of q, one lane per match
+        const uint64_t s0b = gb + (uint32_t)S.tv[g0].x;  // the block's first match (lane 0 is valid)
+        sl_expand_block(scr, lane, c, cx - c, T, [&](uint32_t t, int j, uint32_t r, bool ok) {
+          const double ses = __shfl(es, j, 64);
+          const uint32_t sen = (uint32_t)__shfl((int)en, j, 64), svb = (uint32_t)__shfl((int)vb, j, 64);
+          const uint32_t slk = (uint32_t)__shfl((int)lk, j, 64);
+          const uint64_t slot = s0b + t;
+          if (ok && slot < (uint64_t)O.cap) {
+            const double sx = CT == 1 ? (double)__uint_as_float(svb) : (double)(int32_t)svb;
+            const double sr = ses + (double)(r + 1) * sx, nr = (double)(sen + r + 1);
+            O.key[slot] = (int32_t)((slk << D.own_bits) | (uint32_t)o);  // (sw_owner / sw_local inverted)
             O.agg[slot] = D.agg == 1 ? sr / nr : (D.agg == 2 ? sr : nr);
           }
-        }
+        });
       }
       if (v && (q + 1 >= PE || (S.meta[q + 1] & 0xFFu) != lk)) {  // the run's end: the key's new state
         ag[lk] = is;
@@ -345,17 +374,20 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         if (take) f |= yf;
       });
       fn = (int)fnu;
-      if (c) {
-        const int32_t kid = (int32_t)((lk << D.own_bits) | (uint32_t)o);  // (sw_owner / sw_local inverted)
+      const uint32_t cx = dpp_incl_add(c, lane);
+      const uint32_t T = wave_last(cx);
+      if (T) {  // every match of q outputs the fold after q, one lane per match
         const double val = fn ? __longlong_as_double(0x7ff8000000000000ll) : m;
-        const uint64_t s0l = gb + (uint32_t)S.tv[q].x;
-        for (uint32_t r = 0; r < c; r++) {
-          const uint64_t slot = s0l + r;
-          if (slot < (uint64_t)O.cap) {
-            O.key[slot] = kid;
-            O.agg[slot] = val;
+        const uint64_t s0b = gb + (uint32_t)S.tv[g0].x;  // the block's first match (lane 0 is valid)
+        sl_expand_block(scr, lane, c, cx - c, T, [&](uint32_t t, int j, uint32_t, bool ok) {
+          const double sval = __shfl(val, j, 64);
+          const uint32_t slk = (uint32_t)__shfl((int)lk, j, 64);
+          const uint64_t slot = s0b + t;
+          if (ok && slot < (uint64_t)O.cap) {
+            O.key[slot] = (int32_t)((slk << D.own_bits) | (uint32_t)o);  // (sw_owner / sw_local inverted)
+            O.agg[slot] = sval;
           }
-        }
+        });
       }
       if (v && (q + 1 >= PE || (S.meta[q + 1] & 0xFFu) != lk)) {  // the run's end: the key's new state
         ag[lk] = n == 0 ? 0.0 : (fn ? __longlong_as_double(0x7ff8000000000000ll) : m);
