@@ -387,12 +387,40 @@ __device__ __forceinline__ uint32_t sw_block_scan(uint32_t v, uint32_t* wtot, ui
   return pre + x - v;
 }
 
+// Owner histogram of the count passes in lane-banked copies (round 4): lane l adds to copy l % C of
+// its owner's counters, word o * C + l % C.  With C = 32 the 32 lanes of a half-wave (the LDS
+// atomic's lane group) land on 32 different banks whatever their owners -- one LDS-array cycle per
+// group, where a single counter array took ~3 (random owners: SQ_LDS_BANK_CONFLICT 71 % of the
+// kernel's LDS cycles).  C = SW_HCAP / nown, at most 32 (32 up to 512 owners, 16 at 1024).  The
+// reduction reads copy (c + o) % C at step c, again one bank per lane.
+constexpr int SW_HCAP = 16384;  // words (64 KB)
+constexpr int SW_CNT_THREADS = 512;  // (two workgroups per CU with the 64 KB of copies: 16 waves)
+struct SwHist {
+  uint32_t* h;
+  uint32_t C, sel;
+  __device__ __forceinline__ SwHist(uint32_t* lds, int nown, int nthreads) : h(lds) {
+    const int c = SW_HCAP / nown;
+    C = c >= 32 ? 32u : (uint32_t)c;
+    sel = __lane_id() & (C - 1u);
+    for (int b = threadIdx.x; b < nown * (int)C / 4; b += nthreads) reinterpret_cast<uint4*>(h)[b] = make_uint4(0, 0, 0, 0);
+  }
+  __device__ __forceinline__ void add(uint32_t o) { atomicAdd(&h[o * C + sel], 1u); }
+  __device__ __forceinline__ uint32_t total(uint32_t o) const {
+    uint32_t s = 0;
+    for (uint32_t c = 0; c < C; c++) s += h[o * C + ((c + o) & (C - 1u))];
+    return s;
+  }
+};
+static_assert(SW_HCAP / SW_MAXOWN >= 1, "every owner needs one counter");
+
 // ------------------------------------------------------------------ pass 1: count
-static __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, BatchView B, const int32_t* __restrict__ key,
+static __global__ __launch_bounds__(SW_CNT_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_sw_count(SweepDev D, BatchView B, const int32_t* __restrict__ key,
                                                          int* err) {
-  __shared__ uint32_t h[SW_MAXOWN];
-  const int st = blockIdx.x;
-  for (int b = threadIdx.x; b < D.nown; b += SW_THREADS) h[b] = 0;
+  __shared__ __attribute__((aligned(16))) uint32_t hl[SW_HCAP];
+  // super-tiles in reverse launch order: the workgroups that run last (three rounds of two per CU)
+  // leave the first super-tiles' keys in the caches for the scatter, which starts there
+  const int st = D.nst - 1 - (int)blockIdx.x;
+  SwHist H(hl, D.nown, SW_CNT_THREADS);
   __syncthreads();
   const int64_t lo = (int64_t)st * D.st_len, hi = min(B.n, lo + D.st_len);
   int e = 0;
@@ -401,36 +429,36 @@ static __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, Batc
     constexpr int U = 4;
     const int4* k4 = (const int4*)key;
     const int64_t q0 = lo >> 2, q1 = hi >> 2;
-    for (int64_t i0 = q0 + threadIdx.x; i0 < q1; i0 += (int64_t)SW_THREADS * U) {
+    for (int64_t i0 = q0 + threadIdx.x; i0 < q1; i0 += (int64_t)SW_CNT_THREADS * U) {
       int4 kv[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int64_t i = i0 + (int64_t)u * SW_THREADS;
+        const int64_t i = i0 + (int64_t)u * SW_CNT_THREADS;
         kv[u] = i < q1 ? k4[i] : make_int4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        if (i0 + (int64_t)u * SW_THREADS >= q1) continue;
+        if (i0 + (int64_t)u * SW_CNT_THREADS >= q1) continue;
         const int32_t kq[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
 #pragma unroll
         for (int c = 0; c < 4; c++) {
           if (kq[c] < 0 || kq[c] >= D.maxkeys) e |= SWE_KEYS;
-          else if (D.fstream == 0) atomicAdd(&h[sw_owner((uint32_t)kq[c], D.own_bits)], 1u);
+          else if (D.fstream == 0) H.add(sw_owner((uint32_t)kq[c], D.own_bits));
         }
       }
     }
-    for (int64_t i = q1 * 4 + threadIdx.x; i < hi; i += SW_THREADS) {
+    for (int64_t i = q1 * 4 + threadIdx.x; i < hi; i += SW_CNT_THREADS) {
       const int32_t k = key[i];
       if (k < 0 || k >= D.maxkeys) e |= SWE_KEYS;
-      else if (D.fstream == 0) atomicAdd(&h[sw_owner((uint32_t)k, D.own_bits)], 1u);
+      else if (D.fstream == 0) H.add(sw_owner((uint32_t)k, D.own_bits));
     }
   } else {
   constexpr int U = 8;  // loads of U events in flight per thread before the LDS adds
-  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (int64_t)SW_THREADS * U) {
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (int64_t)SW_CNT_THREADS * U) {
     int32_t kk[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int64_t i = i0 + (int64_t)u * SW_THREADS;
+      const int64_t i = i0 + (int64_t)u * SW_CNT_THREADS;
       int32_t k = -1;
       if (i < hi) {
         const int s = B.stream ? B.stream[i] : 0;
@@ -448,12 +476,12 @@ static __global__ __launch_bounds__(SW_THREADS) void k_sw_count(SweepDev D, Batc
     }
 #pragma unroll
     for (int u = 0; u < U; u++)
-      if (kk[u] >= 0) atomicAdd(&h[sw_owner((uint32_t)kk[u], D.own_bits)], 1u);
+      if (kk[u] >= 0) H.add(sw_owner((uint32_t)kk[u], D.own_bits));
   }
   }
   if (e) atomicOr(err, e);
   __syncthreads();
-  for (int b = threadIdx.x; b < D.nown; b += SW_THREADS) D.cnt[(int64_t)b * D.nst + st] = h[b];
+  for (int b = threadIdx.x; b < D.nown; b += SW_CNT_THREADS) D.cnt[(int64_t)b * D.nst + st] = H.total((uint32_t)b);
   if (st == 0 && threadIdx.x == 0) D.cnt[(int64_t)D.nown * D.nst] = 0;
 }
 
@@ -1885,7 +1913,7 @@ struct SweepState {
     (void)hipMemsetAsync(D.ovf, 0, (size_t)D.nown, s);
     size_t nc = (size_t)D.nown * D.nst + 1;
     kt.mark("sw_count", s);
-    k_sw_count<<<D.nst, SW_THREADS, 0, s>>>(D, B, key, err);
+    k_sw_count<<<D.nst, SW_CNT_THREADS, 0, s>>>(D, B, key, err);
     kt.mark("sw_scan", s);
     size_t tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.cnt, D.off, 0u, nc, rocprim::plus<uint32_t>(), s);

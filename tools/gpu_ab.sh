@@ -12,7 +12,7 @@ if [ -n "$TESTS" ]; then
 fi
 AB=${AB_LIB:-siddhi_amd/base_r4.so}
 for cfg in ${CONFIGS:-2}; do
-  for r in 1 2; do
+  for r in ${REPS:-1 2}; do
     for v in new base; do
       if [ $v = base ]; then export SIDDHI_HIP_DIAG_LIB=$AB; else unset SIDDHI_HIP_DIAG_LIB; fi
       timeout -k 10 300 python3 -u bench.py --config $cfg --no-cpu-baseline --latency-batches 0 --steps ${STEPS:-8} --warmup 2 ${BENCH_ARGS} > gpurun_out/ab_c${cfg}_${v}_$r.log 2>&1 || { tail -20 gpurun_out/ab_c${cfg}_${v}_$r.log; exit 1; }
