@@ -166,3 +166,65 @@ def test_wide_push_falls_back_exactly():
     got = _push_all(eng, ts, key, v, 30_000)
     assert compare(want, got) is None, compare(want, got)
     assert eng.stat("pushes") == 2 and eng.stat("lean_pushes") == 2 and eng.stat("lean_fallbacks") == 1
+
+
+@pytest.mark.parametrize("fn", ["avg", "max"])
+def test_lean_agg_closers_with_many_matches(fn):
+    """SHP_LAYOUT_AGG through k_sw_lean where one event closes up to ~200 candidates of its key
+    (falling prices, then one high price): the one-lane-per-match emission (sl_expand_block) takes
+    a closing position's matches over several 64-match windows, with blocks of 64 positions holding
+    far more than 64 matches.  Per key, the running aggregate equals the reference aggregator's fold
+    over the oracle's matches (avg to 1e-9 relative, max exact)."""
+    from siddhi_amd.native import LAYOUT_AGG, HipEngine
+    from siddhi_amd.query.compiler import compile_app
+    from test_gpu_parity import _agg_app, _expected_agg
+    rng = np.random.default_rng(17)
+    keys = 300
+    ts_, key_, v_ = [], [], []
+    t = 50_000
+    for rnd, run_len in enumerate([30, 70, 130, 200, 90, 160]):
+        hot = 3 * rnd + np.arange(3)  # consecutive ids: three different owners
+        for i in range(run_len):
+            for k in hot:
+                ts_.append(t)
+                key_.append(int(k))
+                v_.append(90.0 - 60.0 * i / run_len)
+            for k in rng.choice(np.arange(20, keys), 4):  # background keys
+                ts_.append(t)
+                key_.append(int(k))
+                v_.append(float(rng.integers(2100, 10000)) / 100.0)
+            t += 1
+        for k in hot:
+            ts_.append(t)
+            key_.append(int(k))
+            v_.append(99.5)
+        t += 2_000  # past the window: the next round starts from empty keys
+    n = len(ts_)
+    g = {"ts": np.array(ts_, np.int64), "key": np.array(key_, np.int32), "stream": np.zeros(n, np.int32),
+         "price": np.array(v_, np.float32), "volume": np.zeros(n, np.int64)}
+    cq = compile_app(_agg_app(fn))[1][0]
+    a = run(OracleEngine(cq.program_json(), 0), cq, g)
+    want = _expected_agg(a, g["price"], fn)
+    e2 = {}
+    S = a["slot_len"].shape[1]
+    off = 0
+    for i in range(len(a["key"])):  # matches per closing event
+        lens = [int(x) for x in a["slot_len"][i]]
+        e2[int(a["refs"][off + lens[0]])] = e2.get(int(a["refs"][off + lens[0]]), 0) + 1
+        off += sum(lens)
+    assert max(e2.values()) >= 150
+    eng = HipEngine(cq.program_json(), 0, max_keys=keys, max_batch=1 << 14, force_general=3,
+                    match_layout=LAYOUT_AGG)
+    assert eng.path == 2
+    b = run(eng, cq, g, 1_700)
+    assert eng.stat("lean_pushes") == eng.stat("pushes") and eng.stat("lean_fallbacks") == 0
+    got = {}
+    for k, x in zip(b["key"], b["agg"]):
+        got.setdefault(int(k), []).append(float(x))
+    assert set(got) == set(want)
+    for k in want:
+        assert len(got[k]) == len(want[k]), k
+        if fn == "max":
+            assert got[k] == want[k], k
+        else:
+            np.testing.assert_allclose(got[k], want[k], rtol=1e-9, atol=0)
