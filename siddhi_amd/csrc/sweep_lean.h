@@ -45,6 +45,15 @@ constexpr int SL_PAD = 16;                    // sentinel positions past E (prob
 constexpr int SL_WL = 120;                    // worklist entries per wave (drained from SL_WLD on)
 constexpr int SL_WLD = 56;
 constexpr int SL_NEAR = 24;                   // closer distances kept as bits
+#ifndef SL_P1_CFG
+#define SL_P1_CFG SW_P1
+#endif
+#ifndef SL_P2_CFG
+#define SL_P2_CFG SW_P2
+#endif
+constexpr int SL_P1 = SL_P1_CFG;              // first-round probes per candidate
+constexpr int SL_P2 = SL_P2_CFG;              // probes per worklist round
+static_assert(SL_P1 < SL_PAD && SL_P2 < SL_PAD, "probes read at most SL_PAD sentinels past E");
 static_assert(SL_CCAP <= SWS_CCAP, "lean carry must fit the HBM carry arrays");
 
 struct SwLeanSmem {
@@ -210,7 +219,11 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   // 6. emit (a chunk's matches are written between barriers A and B of the next chunk, once the
   //    last wave through the chunk has reserved its output range with one global atomic):
   //    slot = offset(q) + (closes(q) - 1 - later), later = closers of q nearer than p
-  auto emit = [&](int PS, int PE, int pc) {
+  // (has_seq: the batch's seq column is present.  Without it the loop issues no global load, so the
+  // compiler's wait counters do not hold each 64-position block for the previous block's stores)
+  auto emit = [&](int PS, int PE, int pc, auto has_seq) {
+    constexpr bool HS = decltype(has_seq)::value;
+    auto seq_of = [&](uint32_t g) -> int64_t { return HS ? B.seq[g] : B.seq0 + (int64_t)g; };
     const unsigned long long gb = S.gbase + S.wb[w];
     for (int g = PS; g < PE; g += 64) {
       const int p = g + (int)lane;
@@ -227,15 +240,15 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         for (int p2 = p + 1; p2 < q - SL_NEAR; p2++) later += S.m[p2] == q ? 1u : 0u;
       }
       const uint32_t r = S.ref[p] & 0x7FFFFFFFu, rq = S.ref[q] & 0x7FFFFFFFu;
-      const int64_t si = p < (int)(S.meta[p] >> 20) ? sbase + S.cseq[pc][r] : bseq(B, r);
-      const int64_t sq = bseq(B, rq);
+      const int64_t si = p < (int)(S.meta[p] >> 20) ? sbase + S.cseq[pc][r] : seq_of(r);
+      const int64_t sq = seq_of(rq);
       const uint64_t slot = gb + (uint32_t)S.tv[q].x + (sl_closes(c) - 1u - later);
       if (slot < (uint64_t)O.cap) {
         if (D.p32) {
           const int64_t dq = sq - si;
           if (dq >= (1ll << 32)) e |= SWE_P32;
           reinterpret_cast<uint2*>(O.refs)[slot] = make_uint2(rq, (uint32_t)dq);
-        } else if (B.seq) {
+        } else if (HS) {
           *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, (int64_t)rq);
         } else {
           *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
@@ -400,6 +413,16 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     }
   };
   int pPS = 0, pPE = 0, pcur = 0;  // this wave's range of the previous chunk, and its carry buffer
+  unsigned long long gres = 0;     // (lane 0 of the chunk's last wave) the reserved output base,
+  uint32_t gres_t = 0;             // the chunk's match count,
+  bool gpend = false;              // and whether S.gbase still has to take them
+  auto publish = [&]() {
+    if (gpend) {
+      if (gres + gres_t > (unsigned long long)O.cap) e |= E_OUT;
+      S.gbase = gres;
+      gpend = false;
+    }
+  };
 #ifdef SHP_SW_STAMPS  // diagnostic build: wave cycles per phase (barrier waits count in the phase before)
   unsigned long long stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t stp = clock64();
@@ -436,6 +459,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         if ((peers & lt) == 0) S.wc[w][lk] = (uint16_t)(before + (uint32_t)__popcll(peers));
       }
     }
+    publish();
     __syncthreads();  // A
     SL_STAMP(0);
     // flags raised by the previous chunk are read here, where no thread writes S.flag (all
@@ -446,7 +470,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         if (D.agg >= 4) emit_mm(pPS, pPE, D.agg == 5);
         else emit_agg(pPS, pPE);
       } else {
-        emit(pPS, pPE, pcur);
+        if (B.seq) emit(pPS, pPE, pcur, std::true_type{});
+        else emit(pPS, pPE, pcur, std::false_type{});
       }
     }
     SL_STAMP(1);
@@ -588,8 +613,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
           const int2 a = S.tv[p];
           const int end = (int)((S.meta[p] >> 8) & 0xFFFu);
           const T bv = bconst ? bc : sw_val<CT>((uint32_t)a.y, 0.0, 0.0, false);
-          res = sl_probe<CT, OPC, SW_P2>(S.tv, (int)qn, end, a.x, W, bv);
-          qn += SW_P2;
+          res = sl_probe<CT, OPC, SL_P2>(S.tv, (int)qn, end, a.x, W, bv);
+          qn += SL_P2;
           if (res == -4 && (int)qn >= end) res = -2;
         }
         const bool unres = res == -4;
@@ -622,8 +647,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         if (p < fe || f1) {  // carried, or e1's filter
           const T bv = bconst ? bc : sw_val<CT>((uint32_t)a.y, 0.0, 0.0, false);
           const int q0 = max(p + 1, fe);
-          res = sl_probe<CT, OPC, SW_P1>(S.tv, q0, end, a.x, W, bv);
-          qn = (uint32_t)(q0 + SW_P1);
+          res = sl_probe<CT, OPC, SL_P1>(S.tv, q0, end, a.x, W, bv);
+          qn = (uint32_t)(q0 + SL_P1);
           if (res == -4 && (int)qn >= end) res = -2;
         }
       }
@@ -662,42 +687,53 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
           S.wb[ww] = t;
           t += S.wt[ww];
         }
-        const unsigned long long g0 = t ? atomicAdd(O.count, (unsigned long long)t) : 0ull;
-        if (g0 + t > (unsigned long long)O.cap) e |= E_OUT;
-        S.gbase = g0;
+        // the returned base is first needed by the next chunk's emission: it is written to LDS
+        // just before the next barrier A, so the atomic's round trip overlaps this wave's carry
+        // bookkeeping and its next rank step instead of holding every wave at that barrier
+        // (+ a lane count that is always 0: an address the compiler cannot prove uniform keeps its
+        // atomic optimizer, which reads the result back at once, off this single-lane add)
+        gres = t ? atomicAdd(O.count + __builtin_amdgcn_mbcnt_lo(0u, 0u), (unsigned long long)t) : 0ull;
+        gres_t = t;
+        gpend = true;
         S.done = 0;
       }
     }
     cbase = __shfl(cbase, 0, 64);
     if (cbase + (int)otot > SL_CCAP) S.flag = 1;
     {
-      uint32_t co = (incl - pk) >> 16, oo = (incl - pk) & 0xFFFFu;
-      for (int q = lb; q < le; q++) {
-        const uint32_t c = sl_closes(S.cl[q]);
-        if (S.m[q] == -2) {
-          const int x = cbase + (int)oo;
-          if (x < SL_CCAP) {
-            const uint32_t f = S.meta[q];
-            const uint32_t r = S.ref[q] & 0x7FFFFFFFu;
-            if (q < (int)(f >> 20)) {  // carried
-              S.cts[nx][x] = S.cts[cur][r];
-              S.cv[nx][x] = S.cv[cur][r];
-              S.cseq[nx][x] = S.cseq[cur][r];
-            } else {
-              const int2 a = S.tv[q];
-              S.cts[nx][x] = tb32 + a.x;  // |.| < 2^30 (the scatter's wide flag)
-              S.cv[nx][x] = (uint32_t)a.y;
-              const int64_t dsq = bseq(B, r) - sbase;
-              if (dsq != (int64_t)(int32_t)dsq) S.flag = 1;
-              S.cseq[nx][x] = (int32_t)dsq;
+      // two copies of the loop: without a seq column it issues no global load, so nothing in it
+      // waits on the output reservation's atomic still in flight (published before barrier A)
+      auto compact = [&](auto has_seq) {
+        uint32_t co = (incl - pk) >> 16, oo = (incl - pk) & 0xFFFFu;
+        for (int q = lb; q < le; q++) {
+          const uint32_t c = sl_closes(S.cl[q]);
+          if (S.m[q] == -2) {
+            const int x = cbase + (int)oo;
+            if (x < SL_CCAP) {
+              const uint32_t f = S.meta[q];
+              const uint32_t r = S.ref[q] & 0x7FFFFFFFu;
+              if (q < (int)(f >> 20)) {  // carried
+                S.cts[nx][x] = S.cts[cur][r];
+                S.cv[nx][x] = S.cv[cur][r];
+                S.cseq[nx][x] = S.cseq[cur][r];
+              } else {
+                const int2 a = S.tv[q];
+                S.cts[nx][x] = tb32 + a.x;  // |.| < 2^30 (the scatter's wide flag)
+                S.cv[nx][x] = (uint32_t)a.y;
+                const int64_t dsq = (decltype(has_seq)::value ? B.seq[r] : B.seq0 + (int64_t)r) - sbase;
+                if (dsq != (int64_t)(int32_t)dsq) S.flag = 1;
+                S.cseq[nx][x] = (int32_t)dsq;
+              }
+              S.clk[nx][x] = (uint8_t)(f & 0xFFu);
             }
-            S.clk[nx][x] = (uint8_t)(f & 0xFFu);
+            oo++;
           }
-          oo++;
+          S.tv[q].x = (int32_t)co;
+          co += c;
         }
-        S.tv[q].x = (int32_t)co;
-        co += c;
-      }
+      };
+      if (B.seq) compact(std::true_type{});
+      else compact(std::false_type{});
     }
     {  // per-key first index and count of the new carry entries
       const int xe = min(cbase + (int)otot, SL_CCAP);
@@ -716,6 +752,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     cur = nx;
     SL_STAMP(5);
   }
+  publish();
   __syncthreads();
   if (S.flag) {
     if (tid == 0) atomicOr(err, SWE_LEAN);
@@ -725,7 +762,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     if (D.agg >= 4) emit_mm(pPS, pPE, D.agg == 5);
     else emit_agg(pPS, pPE);
   } else {
-    emit(pPS, pPE, pcur);
+    if (B.seq) emit(pPS, pPE, pcur, std::true_type{});
+    else emit(pPS, pPE, pcur, std::false_type{});
   }
 #ifdef SHP_SW_STAMPS
   SL_STAMP(1);
