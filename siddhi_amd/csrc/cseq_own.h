@@ -305,6 +305,29 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   const uint64_t lt = sw_lanemask_lt();
   uint32_t* words = reinterpret_cast<uint32_t*>(O.refs);
   int e = 0;
+  // a chunk's words are written during the next chunk, after its rank step: the output
+  // reservation's atomic (tid 0) is then published to LDS at the next chunk's first barrier instead
+  // of being waited on at once, and the stores are no longer the last memory operations before the
+  // wait for the prefetched records (which, with stores in flight, waits for them too)
+  uint32_t pw[CO_PER];        // the previous chunk's words of this thread (positions with pem bits)
+  uint32_t pem = 0, pmo = 0;  // ... which positions emitted, and the thread's offset in the chunk
+  unsigned long long pres = 0;  // (tid 0) the previous chunk's reserved base
+  bool ppend = false;
+#pragma unroll
+  for (int q = 0; q < CO_PER; q++) pw[q] = 0;
+  auto flush_words = [&]() {
+    if (pem) {
+      const int64_t base = (int64_t)S.base;
+#pragma unroll
+      for (int q = 0; q < CO_PER; q++)
+        if ((pem >> q) & 1u) {
+          const int64_t mi = base + pmo + __popc(pem & ((1u << q) - 1u));
+          if (mi >= O.cap) e |= E_OUT;
+          else words[mi] = pw[q];
+        }
+      pem = 0;
+    }
+  };
   // the chunk's records, loaded one chunk ahead (in flight while the previous chunk is solved)
   CoRec r[CO_SUB];
 #pragma unroll
@@ -317,6 +340,11 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     {
       uint32_t* z = reinterpret_cast<uint32_t*>(wc + w * wst);  // (wst is even)
       for (int i = lane; i < (int)(wst >> 1); i += 64) z[i] = 0;
+    }
+    if (ppend) {  // (tid 0; the whole 64-bit result, so its registers stay reserved until here)
+      if (pres >> 32) e |= E_OUT;
+      S.base = (uint32_t)pres;
+      ppend = false;
     }
     __syncthreads();
     // rank: stable within the chunk (waves own consecutive segments, sub-rounds in order)
@@ -337,6 +365,7 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
       rk[s] = below + __shfl(old, (int)ldl, 64);
     }
+    flush_words();  // the previous chunk's (S.base published before the barrier above)
     __syncthreads();
     // per-key totals -> key offsets -> per-wave cursors (a thread takes consecutive local keys)
     {
@@ -485,11 +514,16 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     }
     uint32_t tot;
     const uint32_t mo = co_block_scan(lm, S.sc, tot);
-    if (tid == 0) S.base = tot ? (uint32_t)atomicAdd(O.count, (unsigned long long)tot) : 0u;
+    if (tid == 0) {  // (+ a lane count that is always 0: keeps the atomic optimizer, which reads the
+                     // result back at once, off this one-lane add)
+      pres = tot ? atomicAdd(O.count + __builtin_amdgcn_mbcnt_lo(0u, 0u), (unsigned long long)tot) : 0ull;
+      ppend = true;
+    }
     __syncthreads();
-    const int64_t base = (int64_t)S.base;
-    // walk 3: the words, and at each run end the key's state after the run
-    uint32_t k_ = 0;
+    // walk 3: the words (written during the next chunk), and at each run end the key's state after
+    // the run
+    pem = emw;
+    pmo = mo;
     int rs = rs_in;
     const uint32_t lnext = p0 + CO_PER <= nc ? (S.cl[p0 + CO_PER] & 0x7fffu) : 0xffffu;
 #pragma unroll
@@ -499,12 +533,7 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       if ((hb >> q) & 1u) rs = p;
       const uint32_t Lb = (lbw >> (4 * q)) & 15u;
       const uint32_t gq = xg[q];
-      if ((emw >> q) & 1u) {
-        const int64_t mi = base + mo + k_;
-        k_++;
-        if (mi >= O.cap) e |= E_OUT;
-        else words[mi] = (gq & 0x7fffffffu) | (Lb << 28);
-      }
+      if ((emw >> q) & 1u) pw[q] = (gq & 0x7fffffffu) | (Lb << 28);
       const uint32_t lk = xl[q] & 0x7fffu;
       const uint32_t ln = q + 1 < CO_PER ? (p + 1 < nc ? (xl[q + 1 < CO_PER ? q + 1 : q] & 0x7fffu) : 0xffffu) : lnext;
       if (ln != lk) {  // the key's run ends here
@@ -525,6 +554,12 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     }
     __syncthreads();
   }
+  if (ppend) {  // the last chunk's words
+    if (pres >> 32) e |= E_OUT;
+    S.base = (uint32_t)pres;
+  }
+  __syncthreads();
+  flush_words();
   // the keys' state after the push (copy wr): L, value, null, and the last M events' (seq, ts) --
   // the push's from the ring, the older ones from the stored history
   for (int lk = tid; lk < kpo; lk += CO_THREADS) {

@@ -108,12 +108,15 @@ __device__ __forceinline__ uint32_t sl_closes(uint32_t c) { return (uint32_t)__p
 // its first index inside the window (a byte of the wave's scratch), the rest of the window keeps 0,
 // and a max scan fills the gaps (sources increase with the index).  out(t, src, r) writes the match
 // t, the r-th of lane src.  Every lane of the wave calls it (DPP moves, shuffles).
+// (scr: LDS.  The fence keeps the compiler from forwarding a lane's own store to its load -- the
+// load must see the other lanes' stores; the LDS runs one wave's operations in order.)
 template <class Out>
-__device__ __forceinline__ void sl_expand_block(volatile uint8_t* scr, uint32_t lane, uint32_t c, uint32_t ex,
-                                                uint32_t T, Out&& out) {
+__device__ __forceinline__ void sl_expand_block(uint8_t* scr, uint32_t lane, uint32_t c, uint32_t ex, uint32_t T,
+                                                Out&& out) {
   for (uint32_t t0 = 0; t0 < T; t0 += 64) {
     scr[lane] = 0;
     if (c && ex < t0 + 64u && ex + c > t0) scr[(ex > t0 ? ex : t0) - t0] = (uint8_t)lane;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     uint32_t j = scr[lane];
     dpp_scan_steps(lane, [&](auto ctl, bool take) {
       const uint32_t y = dpp32<decltype(ctl)::value>(j);
@@ -128,7 +131,10 @@ __device__ __forceinline__ void sl_expand_block(volatile uint8_t* scr, uint32_t 
 // (QuerySelector.processInBatchNoGroupBy) in place of the pairs: avg / sum / count (D.agg 1..3;
 // AvgAttributeAggregatorExecutor: `value += x; count++`) and, since round 4, min / max (D.agg 4 / 5;
 // MinAttributeAggregatorExecutor.java:126-130, bit-exact with k_sw_solve's fold)
-template <int CT, int OPC, bool AGG = false>
+// HS: the batch carries a seq column (B.seq).  A template parameter, not a branch: with both
+// variants in one body the compiler's wait counters, merging the variant that loads seqs with the
+// one that does not, held the emission's stores at the scanner step (s_waitcnt vmcnt(0)).
+template <int CT, int OPC, bool AGG = false, bool HS = false>
 __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView B, MatchOut O, int* err) {
   using T = typename SwTy<CT>::T;
   __shared__ SwLeanSmem S;
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     return;
   }
   const int64_t base = B.ts[0];
-  const int64_t sbase = bseq(B, 0);  // carried seqs are kept relative to it
+  const int64_t sbase = HS ? B.seq[0] : B.seq0;  // carried seqs are kept relative to it
   const int32_t W = (int32_t)D.within;  // <= SW_TS_SPAN (SweepState::shape_ok)
   const SwTerm t2 = D.f2.t[0];
   const bool bconst = t2.bk == 0;
@@ -222,8 +228,8 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   // (has_seq: the batch's seq column is present.  Without it the loop issues no global load, so the
   // compiler's wait counters do not hold each 64-position block for the previous block's stores)
   auto emit = [&](int PS, int PE, int pc, auto has_seq) {
-    constexpr bool HS = decltype(has_seq)::value;
-    auto seq_of = [&](uint32_t g) -> int64_t { return HS ? B.seq[g] : B.seq0 + (int64_t)g; };
+    constexpr bool ES = decltype(has_seq)::value;
+    auto seq_of = [&](uint32_t g) -> int64_t { return ES ? B.seq[g] : B.seq0 + (int64_t)g; };
     const unsigned long long gb = S.gbase + S.wb[w];
     for (int g = PS; g < PE; g += 64) {
       const int p = g + (int)lane;
@@ -248,7 +254,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
           const int64_t dq = sq - si;
           if (dq >= (1ll << 32)) e |= SWE_P32;
           reinterpret_cast<uint2*>(O.refs)[slot] = make_uint2(rq, (uint32_t)dq);
-        } else if (HS) {
+        } else if (ES) {
           *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, (int64_t)rq);
         } else {
           *(longlong2*)(O.refs + 2 * slot) = make_longlong2(si, sq);
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   // wave scan (segments = key runs, seeded with the key's state), then q's c matches: the r-th adds
   // q's value once more, (S + (r+1) v) / (N + r + 1) for avg -- k_sw_solve's arithmetic.
   // the AGG emissions' per-wave scratch: the wave's worklist, idle from its probe to the next one
-  volatile uint8_t* scr = reinterpret_cast<volatile uint8_t*>(S.wl[w]);
+  uint8_t* scr = reinterpret_cast<uint8_t*>(&S.wl[w][0]);
   auto emit_agg = [&](int PS, int PE) {
     const unsigned long long gb = S.gbase + S.wb[w];
     double cs = 0;               // the running state at the end of the previous 64-block
@@ -470,8 +476,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
         if (D.agg >= 4) emit_mm(pPS, pPE, D.agg == 5);
         else emit_agg(pPS, pPE);
       } else {
-        if (B.seq) emit(pPS, pPE, pcur, std::true_type{});
-        else emit(pPS, pPE, pcur, std::false_type{});
+        emit(pPS, pPE, pcur, std::integral_constant<bool, HS>{});
       }
     }
     SL_STAMP(1);
@@ -732,8 +737,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
           co += c;
         }
       };
-      if (B.seq) compact(std::true_type{});
-      else compact(std::false_type{});
+      compact(std::integral_constant<bool, HS>{});
     }
     {  // per-key first index and count of the new carry entries
       const int xe = min(cbase + (int)otot, SL_CCAP);
@@ -762,8 +766,7 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     if (D.agg >= 4) emit_mm(pPS, pPE, D.agg == 5);
     else emit_agg(pPS, pPE);
   } else {
-    if (B.seq) emit(pPS, pPE, pcur, std::true_type{});
-    else emit(pPS, pPE, pcur, std::false_type{});
+    emit(pPS, pPE, pcur, std::integral_constant<bool, HS>{});
   }
 #ifdef SHP_SW_STAMPS
   SL_STAMP(1);

@@ -9,7 +9,10 @@ namespace shp {
 void sw_launch_lean_agg(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                         const MatchOut& O, int* err) {
 #define SA_CASE(c, p) \
-  case c * 8 + p: k_sw_lean<c, p, true><<<grid, SL_THREADS, 0, s>>>(D, B, O, err); break;
+  case c * 8 + p:                                                                       \
+    if (B.seq) k_sw_lean<c, p, true, true><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);  \
+    else k_sw_lean<c, p, true, false><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);       \
+    break;
   switch (ct * 8 + opc) {
     SA_CASE(1, 1) SA_CASE(1, 2) SA_CASE(1, 3) SA_CASE(1, 4) SA_CASE(1, 5) SA_CASE(1, 6)
     SA_CASE(2, 1) SA_CASE(2, 2) SA_CASE(2, 3) SA_CASE(2, 4) SA_CASE(2, 5) SA_CASE(2, 6)
@@ -33,7 +36,10 @@ void sw_launch_solve(int nt1, int nt2, int ct, unsigned grid, hipStream_t s, con
 void sw_launch_lean(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                     const MatchOut& O, int* err) {
 #define SL_CASE(c, p) \
-  case c * 8 + p: k_sw_lean<c, p><<<grid, SL_THREADS, 0, s>>>(D, B, O, err); break;
+  case c * 8 + p:                                                                        \
+    if (B.seq) k_sw_lean<c, p, false, true><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);  \
+    else k_sw_lean<c, p, false, false><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);       \
+    break;
   switch (ct * 8 + opc) {
     SL_CASE(1, 1) SL_CASE(1, 2) SL_CASE(1, 3) SL_CASE(1, 4) SL_CASE(1, 5) SL_CASE(1, 6)
     SL_CASE(2, 1) SL_CASE(2, 2) SL_CASE(2, 3) SL_CASE(2, 4) SL_CASE(2, 5) SL_CASE(2, 6)
