@@ -160,7 +160,8 @@ struct SweepDev {
   int32_t lk_lds;
   uint32_t* cnt;         // nown * nst + 1: counts, scanned into off
   uint32_t* off;
-  SwRec* recs;           // batch capacity
+  SwRec* recs;           // batch capacity, plus one record the scatter's unused lanes write
+  int64_t trash;         // (that record's index)
   // per-owner state carried across pushes, double-buffered: a push reads copy `cur` and writes
   // copy cur ^ 1, and the engine flips `cur` only when the push succeeded (a failed push leaves
   // the engine's state as it was)
@@ -623,7 +624,14 @@ static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, B
 #ifdef SHP_SCATTER_DIAG  // diagnostics only: coalesced stores at the event's own index (wrong output)
       if (own[s] != 0xffffffffu) D.recs[rec[s].ref] = rec[s];
 #else
-      if (own[s] != 0xffffffffu) D.recs[wcw[own[s]] + rk[s]] = rec[s];
+    {
+      // every lane stores (lanes without a record into the trash slot): a store count the same on
+      // every path lets the compiler wait for the prefetched loads alone at the next round's start
+      // (vmcnt(8)), not for these stores too
+      const bool ok = own[s] != 0xffffffffu;
+      const int64_t dst = ok ? (int64_t)wcw[ok ? own[s] : 0u] + rk[s] : D.trash;
+      D.recs[dst] = rec[s];
+    }
 #endif
     __syncthreads();
   }
@@ -1809,7 +1817,8 @@ struct SweepState {
     int64_t nc = (int64_t)nown * nst_max + 1;
     al(D.cnt, nc);
     al(D.off, nc);
-    al(D.recs, cap);
+    al(D.recs, cap + 1);
+    D.trash = cap;
     for (int c = 0; c < 2; c++) {
       al(D.c_n[c], nown);
       al(D.c_ts[c], (int64_t)nown * SWS_CCAP);
