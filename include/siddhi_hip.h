@@ -58,8 +58,8 @@ typedef struct shp_config {
                               timestamps per key (a push breaking that fails, engine unchanged). */
   int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
   int32_t match_layout;    /* SHP_LAYOUT_FULL (0), SHP_LAYOUT_PAIRS (1), SHP_LAYOUT_AGG (2),
-                              SHP_LAYOUT_PAIRS32 (3) or SHP_LAYOUT_CHAIN32 (4); PAIRS and PAIRS32
-                              need the sweep path, CHAIN32 the count-sequence path */
+                              SHP_LAYOUT_PAIRS32 (3), SHP_LAYOUT_CHAIN32 (4) or SHP_LAYOUT_COMPACT (5);
+                              PAIRS and PAIRS32 need the sweep path, CHAIN32 the count-sequence path */
 } shp_config;
 
 /* Match layouts. FULL: every field of shp_matches is valid. PAIRS (2-state sweep path,
@@ -87,6 +87,10 @@ typedef struct shp_config {
  * slot_len {L, 1}).  shp_fetch_matches / shp_group_gather_matches expand to FULL.  Needs
  * max_batch < 2^28. */
 #define SHP_LAYOUT_CHAIN32 4
+/* COMPACT: the engine's own compact form, resolved at create -- PAIRS32 on the sweep path, CHAIN32 on
+ * the count-sequence path, FULL on every other (shp_engine_stat(e, "match_layout") reports it).  For a
+ * host that decodes every layout (the Java binding, with shp_push_batch_compact). */
+#define SHP_LAYOUT_COMPACT 5
 
 /* One batch of events in SoA form. Column c follows program["columns"][c]:
  * int->int32, long->int64, float->float32, double->float64, bool->uint8,
@@ -172,6 +176,22 @@ int shp_push_batch(shp_engine* e, const shp_batch* in, shp_matches* out);
  * valid until the matches are fetched: shp_fetch_matches / shp_group_gather_matches expand the
  * compact records from them. */
 int shp_push_batch_device(shp_engine* e, const shp_batch* in, shp_matches* out);
+/* Host-memory batch with compact match records: as shp_push_batch, but the records come back in the
+ * layout the engine produced them in, copied to host memory without expansion -- out->layout says
+ * which: PAIRS32 / PAIRS (sweep path, `refs` holds the 32- / 64-bit words), CHAIN32 (count-sequence
+ * path), AGG, or FULL on every other path.  Per key the compact records are in reference emission
+ * order; across keys in owner order, so a host restoring the global order sorts them stably by
+ * e2's batch index (the reference emits at e2's arrival, PatternSingleProcessStreamReceiver).
+ * The Java binding's push (GpuStateStreamRuntime.flush). */
+int shp_push_batch_compact(shp_engine* e, const shp_batch* in, shp_matches* out);
+/* The oldest event sequence number the engine's committed state still names: an event of any open
+ * partial (pending / new-and-every lists, count chains, logical slots, pairs waiting on an absent
+ * timer, sweep carry).  Every later match names events >= this or of later pushes, so a host that
+ * rebuilds StreamEvents from its own copy of the rows (ColumnarBatch) may drop the rows below it
+ * -- the reference keeps a StreamEvent alive exactly as long as a partial holds it
+ * (StreamPreStateProcessor.java:364-403).  The engine's next sequence number when nothing is open.
+ * Costs a snapshot (device to host copy of the state): call it when the kept rows grow, not per push. */
+int shp_engine_oldest_live_seq(shp_engine* e, int64_t* out);
 /* Copy the matches of the last shp_push_batch_device to host memory (none after shp_restore). */
 int shp_fetch_matches(shp_engine* e, shp_matches* out);
 int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out);

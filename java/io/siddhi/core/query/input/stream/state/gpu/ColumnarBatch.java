@@ -7,7 +7,14 @@
  * float->float32, double->float64, bool->uint8, string->int32 dictionary id) with a null byte per
  * event — and keeps the rows so StateEvents can be rebuilt from the sequence numbers the engine
  * returns (StreamEvents are rebuilt from the batch rows, never copied back from the device).
- * Source only: no JDK in this repository's image (DESIGN.md §6).
+ *
+ * Retention: the reference keeps a StreamEvent alive exactly as long as a partial holds it
+ * (StreamPreStateProcessor.java:364-403).  The rows of committed pushes are kept by sequence
+ * number from shp_engine_oldest_live_seq on (the oldest event an open partial of the engine's
+ * committed state holds): trim() drops everything below it, maybeTrim() asks the engine once the
+ * kept rows have doubled since the last trim, so the query (a state snapshot) stays amortised.
+ * The Python mirror of these rules is siddhi_amd/history.py (RowHistory), tested in
+ * tests/test_retention.py.  Source only: no JDK in this repository's image (DESIGN.md §6).
  */
 package io.siddhi.core.query.input.stream.state.gpu;
 
@@ -15,10 +22,11 @@ import io.siddhi.core.event.stream.StreamEvent;
 
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
-import java.lang.foreign.ValueLayout;
 import java.util.ArrayDeque;
 import java.util.ArrayList;
+import java.util.Arrays;
 import java.util.List;
+import java.util.function.LongSupplier;
 
 import static java.lang.foreign.ValueLayout.ADDRESS;
 import static java.lang.foreign.ValueLayout.JAVA_BYTE;
@@ -46,6 +54,23 @@ final class ColumnarBatch {
         }
     }
 
+    /** The rows of one committed push from sequence number seq0 on (a trimmed push keeps its tail). */
+    static final class Block {
+        final long seq0;
+        final Object[][] rows;
+        final long[] ts;
+
+        Block(long seq0, Object[][] rows, long[] ts) {
+            this.seq0 = seq0;
+            this.rows = rows;
+            this.ts = ts;
+        }
+
+        long end() {
+            return seq0 + rows.length;
+        }
+    }
+
     private final Arena arena;
     private final long capacity;
     private final Column[] columns;
@@ -54,21 +79,23 @@ final class ColumnarBatch {
     private final MemorySegment colPtrs, nullPtrs, descriptor;
     private final NativeDictionary strings;           // string-attribute dictionary (shared with the filters)
     private long n;
-    private long seq0;                                // sequence number of row 0 of this batch
-    // rows of earlier batches still referenced by open partial matches: the engine reports match
-    // slots as sequence numbers, which may point into any earlier push (every e1 waiting for e2)
-    private final ArrayDeque<Object[][]> history = new ArrayDeque<>();
-    private final ArrayDeque<long[]> historySeq = new ArrayDeque<>();
-    private final int historyBatches;
+    private long seq0;                                // sequence number of row 0 of the open batch
+    // rows of committed pushes still named by open partials (or not yet trimmed), oldest first
+    private final ArrayDeque<Block> history = new ArrayDeque<>();
+    private long kept;                                // rows held in `history`
+    private long floor;                               // every row below it was dropped
+    private final long minTrim;
+    private long trimAt;
     private final List<Object[]> rows = new ArrayList<>();
-    private final List<long[]> rowMeta = new ArrayList<>();  // {ts, stream}
+    private final List<Long> rowTs = new ArrayList<>();
 
-    ColumnarBatch(Arena arena, long capacity, Column[] columns, NativeDictionary strings, int historyBatches) {
+    ColumnarBatch(Arena arena, long capacity, Column[] columns, NativeDictionary strings, long minTrim) {
         this.arena = arena;
         this.capacity = capacity;
         this.columns = columns;
         this.strings = strings;
-        this.historyBatches = historyBatches;
+        this.minTrim = Math.max(1, minTrim);
+        this.trimAt = this.minTrim;
         ts = arena.allocate(JAVA_LONG, capacity);
         key = arena.allocate(JAVA_INT, capacity);
         stream = arena.allocate(JAVA_INT, capacity);
@@ -118,7 +145,7 @@ final class ColumnarBatch {
             }
         }
         rows.add(data);
-        rowMeta.add(new long[]{timestamp, streamIndex});
+        rowTs.add(timestamp);
         n++;
     }
 
@@ -140,54 +167,89 @@ final class ColumnarBatch {
     void discard() {
         n = 0;
         rows.clear();
-        rowMeta.clear();
+        rowTs.clear();
     }
 
-    /** After a successful push: the rows move to the history (matches of later pushes may name them). */
-    void clear() {
-        history.addLast(rows.toArray(new Object[0][]));
-        long[] meta = new long[rows.size() * 2 + 1];
-        meta[0] = seq0;
-        for (int i = 0; i < rowMeta.size(); i++) {
-            meta[1 + 2 * i] = rowMeta.get(i)[0];
-            meta[2 + 2 * i] = rowMeta.get(i)[1];
-        }
-        historySeq.addLast(meta);
-        while (history.size() > historyBatches) {
-            history.removeFirst();
-            historySeq.removeFirst();
+    /** After a successful push: the rows join the history (matches of this and later pushes name
+     * them) and the batch is empty again.  The pushed key / ts / stream columns stay readable
+     * (keyAt, tsAt, streamAt) until the next append: the compact records are decoded from them.
+     * Returns the pushed rows' first sequence number. */
+    long commit() {
+        long first = seq0;
+        if (n > 0) {
+            long[] t = new long[rowTs.size()];
+            for (int i = 0; i < t.length; i++) {
+                t[i] = rowTs.get(i);
+            }
+            history.addLast(new Block(seq0, rows.toArray(new Object[0][]), t));
+            kept += n;
         }
         seq0 += n;
         n = 0;
         rows.clear();
-        rowMeta.clear();
+        rowTs.clear();
+        return first;
+    }
+
+    int keyAt(long i) {
+        return key.getAtIndex(JAVA_INT, i);
+    }
+
+    long tsAt(long i) {
+        return ts.getAtIndex(JAVA_LONG, i);
+    }
+
+    int streamAt(long i) {
+        return stream.getAtIndex(JAVA_INT, i);
+    }
+
+    /** Once the kept rows reach minTrim and have doubled since the last trim: ask the engine for its
+     * oldest live sequence number (shp_engine_oldest_live_seq) and drop the rows below it. */
+    void maybeTrim(LongSupplier oldestLive) {
+        if (kept < trimAt) {
+            return;
+        }
+        trim(oldestLive.getAsLong());
+        trimAt = Math.max(minTrim, 2 * kept);
+    }
+
+    /** Drops every row below `lo`; a push partly below keeps its tail. */
+    void trim(long lo) {
+        while (!history.isEmpty() && history.peekFirst().end() <= lo) {
+            kept -= history.removeFirst().rows.length;
+        }
+        Block b = history.peekFirst();
+        if (b != null && b.seq0 < lo) {
+            int cut = (int) (lo - b.seq0);
+            history.removeFirst();
+            history.addFirst(new Block(lo, Arrays.copyOfRange(b.rows, cut, b.rows.length),
+                    Arrays.copyOfRange(b.ts, cut, b.ts.length)));
+            kept -= cut;
+        }
+        floor = Math.max(floor, Math.min(lo, seq0));
     }
 
     /** The StreamEvent of sequence number `seq` (a match slot), rebuilt from the kept row, with the
      * before-window data the query's MetaStreamEvent expects for that stream. */
     StreamEvent event(long seq, int outputDataSize) {
-        Object[][] block = null;
-        long[] meta = null;
-        var hit = history.descendingIterator();
-        var hitSeq = historySeq.descendingIterator();
-        while (hit.hasNext()) {
-            Object[][] b = hit.next();
-            long[] m = hitSeq.next();
-            if (seq >= m[0] && seq < m[0] + b.length) {
+        Block block = null;
+        var it = history.descendingIterator();   // recent pushes first: most matches name them
+        while (it.hasNext()) {
+            Block b = it.next();
+            if (seq >= b.seq0 && seq < b.end()) {
                 block = b;
-                meta = m;
                 break;
             }
         }
         if (block == null) {
-            throw new IllegalStateException("event " + seq + " is older than the kept history (" + historyBatches
-                    + " pushes); raise the history or add `within` to the query");
+            // never expected: the engine names only rows at or after its oldest live one
+            throw new IllegalStateException("event " + seq + " is not held (rows kept from " + floor + " to "
+                    + seq0 + "): the engine named an event below its reported oldest live one");
         }
-        int i = (int) (seq - meta[0]);
-        Object[] data = block[i];
+        int i = (int) (seq - block.seq0);
         StreamEvent e = new StreamEvent(0, 0, outputDataSize);
-        e.setTimestamp(meta[1 + 2 * i]);
-        e.setOutputData(data.clone());
+        e.setTimestamp(block.ts[i]);
+        e.setOutputData(block.rows[i].clone());
         return e;
     }
 
@@ -195,6 +257,50 @@ final class ColumnarBatch {
         return seq0 + n;
     }
 
-    @SuppressWarnings("unused")
-    private static final ValueLayout.OfLong LONG = JAVA_LONG;
+    // ---- snapshot support (GpuStateHolder): the rows the engine's state names travel with its blob,
+    // as the reference's snapshot carries the StreamEvents of its partials
+
+    /** The kept rows from `lo` on: {seqs (long[]), timestamps (long[]), data (Object[][])}. */
+    Object[] liveRows(long lo) {
+        List<Long> s = new ArrayList<>();
+        List<Long> t = new ArrayList<>();
+        List<Object[]> d = new ArrayList<>();
+        for (Block b : history) {
+            for (int i = 0; i < b.rows.length; i++) {
+                if (b.seq0 + i >= lo) {
+                    s.add(b.seq0 + i);
+                    t.add(b.ts[i]);
+                    d.add(b.rows[i]);
+                }
+            }
+        }
+        long[] seqs = new long[s.size()];
+        long[] tss = new long[t.size()];
+        for (int i = 0; i < seqs.length; i++) {
+            seqs[i] = s.get(i);
+            tss[i] = t.get(i);
+        }
+        return new Object[]{seqs, tss, d.toArray(new Object[0][])};
+    }
+
+    /** After shp_restore: the history becomes the snapshot's rows (consecutive runs of sequence
+     * numbers become blocks) and the next push starts at the engine's restored counter. */
+    void restoreRows(long[] seqs, long[] tss, Object[][] data, long nextSeq) {
+        history.clear();
+        kept = 0;
+        int i = 0;
+        while (i < seqs.length) {
+            int j = i + 1;
+            while (j < seqs.length && seqs[j] == seqs[j - 1] + 1) {
+                j++;
+            }
+            history.addLast(new Block(seqs[i], Arrays.copyOfRange(data, i, j), Arrays.copyOfRange(tss, i, j)));
+            kept += j - i;
+            i = j;
+        }
+        discard();
+        seq0 = nextSeq;
+        floor = seqs.length > 0 ? seqs[0] : nextSeq;
+        trimAt = Math.max(minTrim, 2 * kept);
+    }
 }

@@ -11,7 +11,11 @@
  * Initialized, Started (StreamPreStateProcessor.java:450-469), SuccessCondition /
  * StartStateReset (CountPreStateProcessor.java:206-219), IsActive, LastScheduledTime,
  * LastArrivalTime (AbsentStreamPreStateProcessor.java:328-341) and ToNotifyQueue
- * (Scheduler.java:349-360).  restore() takes the blob back (the decoded form is informational).
+ * (Scheduler.java:349-360).  The rows the engine's partials name travel with the blob under
+ * "LiveRows" (the reference's snapshot serialises the StreamEvents inside its partials; here they
+ * are the ColumnarBatch rows from shp_engine_oldest_live_seq on), with "NextSeq" and, for CHAIN32,
+ * the per-key rings.  restore() takes the blob, the rows and the rings back (the decoded form is
+ * informational).
  * Source only: no JDK in this repository's image (DESIGN.md §6).
  */
 package io.siddhi.core.query.input.stream.state.gpu;
@@ -45,16 +49,14 @@ public final class GpuStateHolder {
 
         @Override
         public Map<String, Object> snapshot() {
-            byte[] blob = runtime.snapshot();
             Map<String, Object> m = new HashMap<>();
-            m.put("GpuEngineSnapshot", blob);
-            m.put("StateByKey", runtime.describe(blob));
+            runtime.snapshotInto(m);
             return m;
         }
 
         @Override
         public void restore(Map<String, Object> state) {
-            runtime.restore((byte[]) state.get("GpuEngineSnapshot"));
+            runtime.restoreFrom(state);
         }
     }
 }

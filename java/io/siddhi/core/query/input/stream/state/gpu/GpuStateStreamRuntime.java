@@ -19,10 +19,25 @@
  *     (core/util/parser/helper/QueryParserHelper.java:161-167) finds runtime i for state i; states
  *     of one stream share that stream's GpuStateReceiver, which StreamJunction.subscribe
  *     (core/stream/StreamJunction.java:334-338) subscribes once.
- *   core/partition/PartitionStreamReceiver.java:176-283 — for a partitioned GPU query, append
- *     (key string, event) to the same batch instead of one send() per key
- *     (GpuStateReceiver.append(ts, key, data), then endOfChunk()); the runtime maps the key to a
- *     dense id with its own bounded dictionary and the engine partitions on the device.
+ *   Partitioned queries need no further change: the runtime IS a StateStreamRuntime, so
+ *     PartitionParser.java:76 -> PartitionRuntimeImpl.addPartitionReceiver takes its
+ *     `instanceof StateStreamRuntime` branch (core/partition/PartitionRuntimeImpl.java:243-258) and
+ *     walks the query's state elements (:262-288) to create the outer streams'
+ *     PartitionStreamReceivers; PartitionStreamReceiver.addStreamJunction (:291-310) subscribes
+ *     runtime i's receiver (getSingleStreamRuntimes()) to the inner junction of its stream, and
+ *     PartitionStreamReceiver.send (:262-272) sends each event under its partition key
+ *     (SiddhiAppContext.startPartitionFlow), which GpuStateReceiver maps to a dense key id.  The
+ *     per-key initPartition call (QueryRuntimeImpl.java:167-170) needs nothing: the engine creates
+ *     a key's state on its first event.
+ *   core/partition/PartitionStreamReceiver.java:176-283 — optional batching: append (key string,
+ *     event) to the same batch instead of one send() per key run (GpuStateReceiver.append(ts, key,
+ *     data), then endOfChunk()).
+ *
+ * Match records come back in the engine's compact layout (SHP_LAYOUT_COMPACT through
+ * shp_push_batch_compact: PAIRS32 on the sweep path, CHAIN32 on the count-sequence path, FULL on
+ * the others) and are decoded here against the batch's own rows; the rows are kept by sequence
+ * number from shp_engine_oldest_live_seq on (ColumnarBatch).  The Python mirror of the decoding
+ * and retention rules is siddhi_amd/history.py + runtime.py, tested in tests/test_retention.py.
  *
  * Concurrency: the reference serialises a query with synchronized(patternSyncObject)
  * (SingleProcessStreamReceiver.java:52); every entry point here takes `lock`.
@@ -40,8 +55,8 @@ import io.siddhi.core.event.stream.MetaStreamEvent;
 import io.siddhi.core.event.stream.StreamEvent;
 import io.siddhi.core.exception.SiddhiAppCreationException;
 import io.siddhi.core.exception.SiddhiAppRuntimeException;
-import io.siddhi.core.query.input.stream.StreamRuntime;
 import io.siddhi.core.query.input.stream.single.SingleStreamRuntime;
+import io.siddhi.core.query.input.stream.state.StateStreamRuntime;
 import io.siddhi.core.query.processor.ProcessingMode;
 import io.siddhi.core.query.processor.Processor;
 import io.siddhi.core.query.selector.QuerySelector;
@@ -51,6 +66,7 @@ import io.siddhi.query.api.definition.Attribute;
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
 import java.util.ArrayList;
+import java.util.Arrays;
 import java.util.List;
 import java.util.Map;
 import java.util.concurrent.Executors;
@@ -65,7 +81,7 @@ import static java.lang.foreign.ValueLayout.JAVA_INT;
 import static java.lang.foreign.ValueLayout.JAVA_LONG;
 import static java.lang.foreign.ValueLayout.JAVA_SHORT;
 
-public final class GpuStateStreamRuntime implements StreamRuntime {
+public final class GpuStateStreamRuntime extends StateStreamRuntime {
 
     /** When appended events reach the engine (and so when callbacks fire).
      * SYNC: at the end of every receive(...) call -- one push per InputHandler.send, callbacks
@@ -86,6 +102,11 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
     private final int numStates;
     private final int outputDataSize;
     private final List<SingleStreamRuntime> singleStreamRuntimes = new ArrayList<>();
+    private final int layout;                      // the resolved SHP_LAYOUT_COMPACT: PAIRS32, CHAIN32 or FULL
+    private final int maxKeys;
+    private final int chainM;                      // CHAIN32: a chain's longest length (the count's max)
+    private long[] ring;                           // CHAIN32: per key, its last chainM sequence numbers
+    private int[] ringLen;
     private Processor selector;                    // QuerySelector (setCommonProcessor)
     private final NativeDictionary strings;        // string values, shared with the filters' constants
     private final NativeDictionary keys;           // partition keys, bounded by max_keys
@@ -181,7 +202,10 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
     GpuStateStreamRuntime(String appText, String queryName, ProgramInfo info, int maxKeys, long maxBatch, int device,
                           long startClock, MetaStateEvent metaStateEvent, SiddhiQueryContext queryContext,
                           NativeDictionary strings, FlushPolicy policy, long maxDelayMillis) {
+        super(queryContext, metaStateEvent);
         this.metaStateEvent = metaStateEvent;
+        this.maxKeys = maxKeys;
+        this.chainM = Math.max(1, info.countMax);
         this.strings = strings;
         this.policy = policy;
         this.outputDataSize = metaStateEvent.getOutputDataAttributes() == null ? 0
@@ -198,7 +222,7 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
             cfg.set(JAVA_LONG, ShpNative.CFG_START_CLOCK, startClock);
             cfg.set(JAVA_INT, ShpNative.CFG_FORCE_GENERAL, 0);       // auto path
             cfg.set(JAVA_INT, ShpNative.CFG_PROFILE_KERNELS, 0);
-            cfg.set(JAVA_INT, ShpNative.CFG_MATCH_LAYOUT, ShpNative.LAYOUT_FULL);
+            cfg.set(JAVA_INT, ShpNative.CFG_MATCH_LAYOUT, ShpNative.LAYOUT_COMPACT);
             MemorySegment out = arena.allocate(ADDRESS);
             int rc;
             try {
@@ -243,8 +267,13 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
                 singleStreamRuntimes.add(new SingleStreamRuntime(receivers[s], null, ProcessingMode.BATCH,
                         metaStateEvent.getMetaStreamEvent(st)));
             }
+            try (Arena a = Arena.ofConfined()) {
+                layout = (int) (long) ShpNative.ENGINE_STAT.invokeExact(eng, a.allocateFrom("match_layout"));
+            } catch (Throwable t) {
+                throw new SiddhiAppCreationException("shp_engine_stat failed", t);
+            }
             matches = arena.allocate(ShpNative.MATCHES);
-            batch = new ColumnarBatch(arena, maxBatch, info.columns, strings, 64);
+            batch = new ColumnarBatch(arena, maxBatch, info.columns, strings, 1 << 12);
         } catch (RuntimeException e) {
             if (!eng.equals(MemorySegment.NULL)) {
                 try {
@@ -305,7 +334,7 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
         }
     }
 
-    // ---------------------------------------------------------------- StreamRuntime
+    // ---------------------------------------------------------------- StateStreamRuntime
     @Override
     public List<SingleStreamRuntime> getSingleStreamRuntimes() {
         return singleStreamRuntimes;
@@ -331,6 +360,20 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
         return null;
     }
 
+    /** Called by the Sequence receivers after each event (SequenceSingleProcessStreamReceiver.java:43,
+     * SequenceMultiProcessStreamReceiver.java:49), which GpuStateReceiver replaces: the engine resets
+     * and updates its states per event itself. */
+    @Override
+    public void resetAndUpdate() {
+    }
+
+    /** QueryRuntimeImpl.initPartition (:167-170) for a new partition key (PartitionStreamReceiver.send
+     * :266): the engine creates a key's state -- the start partials and, for absent states, the
+     * partitionCreated timers -- at the key's first event, so nothing happens here. */
+    @Override
+    public void initPartition() {
+    }
+
     // ---------------------------------------------------------------- ingress (GpuStateReceiver)
     void append(long timestamp, int keyId, int streamIndex, Object[] data) {
         rethrowDeferred();
@@ -354,8 +397,9 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
                 return;
             }
             int rc;
+            long pushed = batch.size();
             try {
-                rc = (int) ShpNative.PUSH_BATCH.invokeExact(engine, batch.descriptor(), matches);
+                rc = (int) ShpNative.PUSH_BATCH_COMPACT.invokeExact(engine, batch.descriptor(), matches);
             } catch (Throwable t) {
                 batch.discard();
                 throw new SiddhiAppRuntimeException("shp_push_batch failed: " + t, t);
@@ -368,10 +412,27 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
                 throw new SiddhiAppRuntimeException("shp_push_batch: " + ShpNative.codeName(rc) + ": "
                         + ShpNative.lastError(engine));
             }
-            batch.clear();
-            deliver();
+            long seq0 = batch.commit();
+            deliver(seq0, pushed);
+            batch.maybeTrim(this::oldestLiveSeq);
         } finally {
             lock.unlock();
+        }
+    }
+
+    /** shp_engine_oldest_live_seq: the oldest event an open partial of the committed state holds. */
+    private long oldestLiveSeq() {
+        try (Arena a = Arena.ofConfined()) {
+            MemorySegment out = a.allocate(JAVA_LONG);
+            int rc = (int) ShpNative.OLDEST_LIVE_SEQ.invokeExact(engine, out);
+            if (rc != ShpNative.OK) {
+                throw new SiddhiAppRuntimeException("shp_engine_oldest_live_seq: " + ShpNative.lastError(engine));
+            }
+            return out.get(JAVA_LONG, 0);
+        } catch (RuntimeException e) {
+            throw e;
+        } catch (Throwable t) {
+            throw new SiddhiAppRuntimeException("shp_engine_oldest_live_seq failed: " + t, t);
         }
     }
 
@@ -390,15 +451,110 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
             if (rc != ShpNative.OK) {
                 throw new SiddhiAppRuntimeException("shp_advance_clock: " + ShpNative.lastError(engine));
             }
-            deliver();
+            deliverFull();   // a clock-only event: FULL records (timer matches), no new rows
         } finally {
             lock.unlock();
         }
     }
 
-    // StateEvents from the match records: slot s of match i holds slot_len[i*S+s] event sequence
+    /** The records of the push whose rows start at seq0 (pushed rows, still in the batch columns). */
+    private void deliver(long seq0, long pushed) {
+        int lay = ShpNative.matchesInt(matches, "layout");
+        if (lay == ShpNative.LAYOUT_PAIRS32) {
+            deliverPairs32(seq0);
+        } else if (lay == ShpNative.LAYOUT_CHAIN32) {
+            deliverChain32(seq0, pushed);
+        } else {
+            deliverFull();
+        }
+    }
+
+    /** PAIRS32 (sweep path, 2 states): word pair (e2's batch index, e2 seq - e1 seq).  The engine
+     * writes them per key in emission order, across keys in owner order; the reference emits at
+     * e2's arrival, so they are ordered stably by e2's index (history.decode_pairs32). */
+    private void deliverPairs32(long seq0) {
+        long m = ShpNative.matchesLong(matches, "m");
+        if (m == 0) {
+            return;
+        }
+        MemorySegment w = ShpNative.matchesPtr(matches, "refs", m * 8);
+        long[] order = new long[(int) m];
+        for (int j = 0; j < m; j++) {
+            order[j] = (Integer.toUnsignedLong(w.getAtIndex(JAVA_INT, 2L * j)) << 32) | j;
+        }
+        Arrays.sort(order);   // by e2's index, then the engine's order (stable)
+        int out0 = metaStateEvent.getMetaStreamEvent(0).getOutputData().size();
+        int out1 = metaStateEvent.getMetaStreamEvent(1).getOutputData().size();
+        for (long o : order) {
+            int j = (int) (o & 0xffffffffL);
+            long idx = o >>> 32;
+            long e2 = seq0 + idx;
+            long e1 = e2 - Integer.toUnsignedLong(w.getAtIndex(JAVA_INT, 2L * j + 1));
+            StateEvent se = new StateEvent(numStates, outputDataSize);
+            se.setTimestamp(batch.tsAt(idx));
+            se.setType(ComplexEvent.Type.CURRENT);
+            se.addEvent(0, batch.event(e1, out0));
+            se.addEvent(1, batch.event(e2, out1));
+            selector.process(new ComplexEventChunk<>(se, se));
+        }
+    }
+
+    /** CHAIN32 (count-sequence path `e1=S[..]<1:M>, e2=S[..]`): word = e2's batch index | L << 28; e1's
+     * chain is the L events of e2's key just before e2.  The pushed rows are walked in order with a
+     * ring of each key's last M sequence numbers (history.ChainRings); a sequence emits at most one
+     * match per event, at that event, so batch order is the reference's emission order. */
+    private void deliverChain32(long seq0, long pushed) {
+        long m = ShpNative.matchesLong(matches, "m");
+        if (ring == null) {
+            ring = new long[maxKeys * chainM];
+            ringLen = new int[maxKeys];
+        }
+        int[] lenAt = null;
+        if (m > 0) {
+            MemorySegment w = ShpNative.matchesPtr(matches, "refs", m * 4);
+            lenAt = new int[(int) pushed];
+            Arrays.fill(lenAt, -1);
+            for (long j = 0; j < m; j++) {
+                int x = w.getAtIndex(JAVA_INT, j);
+                lenAt[x & 0x0FFFFFFF] = x >>> 28;
+            }
+        }
+        int out0 = metaStateEvent.getMetaStreamEvent(0).getOutputData().size();
+        int out1 = metaStateEvent.getMetaStreamEvent(1).getOutputData().size();
+        for (int i = 0; i < pushed; i++) {
+            if (batch.streamAt(i) < 0) {
+                continue;   // a clock-only row is no key's event
+            }
+            int k = batch.keyAt(i);
+            int base = k * chainM;
+            int have = ringLen[k];
+            if (lenAt != null && lenAt[i] >= 0) {
+                int len = lenAt[i];
+                if (len > have) {
+                    throw new SiddhiAppRuntimeException("CHAIN32: a chain of " + len + " events before row " + i
+                            + " but key " + k + " holds " + have);
+                }
+                StateEvent se = new StateEvent(numStates, outputDataSize);
+                se.setTimestamp(batch.tsAt(i));
+                se.setType(ComplexEvent.Type.CURRENT);
+                for (int t = have - len; t < have; t++) {
+                    se.addEvent(0, batch.event(ring[base + t], out0));   // the count state's chain, in order
+                }
+                se.addEvent(1, batch.event(seq0 + i, out1));
+                selector.process(new ComplexEventChunk<>(se, se));
+            }
+            if (have == chainM) {
+                System.arraycopy(ring, base + 1, ring, base, chainM - 1);
+                have--;
+            }
+            ring[base + have] = seq0 + i;
+            ringLen[k] = have + 1;
+        }
+    }
+
+    // StateEvents from FULL records: slot s of match i holds slot_len[i*S+s] event sequence
     // numbers from refs[ref_off[i] + ...] (a count state's chain, in order); -1 = an empty slot
-    private void deliver() {
+    private void deliverFull() {
         long m = ShpNative.matchesLong(matches, "m");
         if (m == 0) {
             return;
@@ -474,6 +630,44 @@ public final class GpuStateStreamRuntime implements StreamRuntime {
             throw e;
         } catch (Throwable t) {
             throw new SiddhiAppRuntimeException("shp_snapshot_describe failed: " + t, t);
+        }
+    }
+
+    /** State.snapshot() for GpuStateHolder: the engine blob, the rows its partials name (the reference's
+     * snapshot carries those StreamEvents inside its partials) and, for CHAIN32, the per-key rings. */
+    void snapshotInto(Map<String, Object> m) {
+        lock.lock();
+        try {
+            byte[] blob = snapshot();
+            m.put("GpuEngineSnapshot", blob);
+            m.put("StateByKey", describe(blob));
+            m.put("LiveRows", batch.liveRows(oldestLiveSeq()));
+            m.put("NextSeq", batch.nextSeq());
+            if (ring != null) {
+                m.put("ChainRings", new Object[]{ring.clone(), ringLen.clone()});
+            }
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /** State.restore(): the engine blob, then the rows and rings that travelled with it. */
+    void restoreFrom(Map<String, Object> m) {
+        lock.lock();
+        try {
+            restore((byte[]) m.get("GpuEngineSnapshot"));
+            Object[] rows = (Object[]) m.get("LiveRows");
+            batch.restoreRows((long[]) rows[0], (long[]) rows[1], (Object[][]) rows[2], (Long) m.get("NextSeq"));
+            Object[] rings = (Object[]) m.get("ChainRings");
+            if (rings != null) {
+                ring = ((long[]) rings[0]).clone();
+                ringLen = ((int[]) rings[1]).clone();
+            } else {
+                ring = null;
+                ringLen = null;
+            }
+        } finally {
+            lock.unlock();
         }
     }
 

@@ -23,15 +23,17 @@ final class ProgramInfo {
     final int[] stateStream;        // per state id: index into streams
     final String[] stateRef;        // per state id: the reference id (e1, ...), null when none
     final boolean[] stateMulti;     // per state id: a count state (multi-valued slot)
+    final int countMax;             // the largest <min:max> bound (CHAIN32: a chain's longest length)
 
     private ProgramInfo(String[] streams, ColumnarBatch.Column[] columns, boolean partitioned, int[] stateStream,
-                        String[] stateRef, boolean[] stateMulti) {
+                        String[] stateRef, boolean[] stateMulti, int countMax) {
         this.streams = streams;
         this.columns = columns;
         this.partitioned = partitioned;
         this.stateStream = stateStream;
         this.stateRef = stateRef;
         this.stateMulti = stateMulti;
+        this.countMax = countMax;
     }
 
     @SuppressWarnings("unchecked")
@@ -62,25 +64,29 @@ final class ProgramInfo {
             sst[id] = ((Number) m.get("stream")).intValue();
             sref[id] = (String) m.get("ref");
         }
-        markCounts(p.get("tree"), smulti);
-        return new ProgramInfo(names, cols, Boolean.TRUE.equals(p.get("partitioned")), sst, sref, smulti);
+        int cmax = markCounts(p.get("tree"), smulti);
+        return new ProgramInfo(names, cols, Boolean.TRUE.equals(p.get("partitioned")), sst, sref, smulti, cmax);
     }
 
-    // the states under a "count" node of program["tree"] (CountStateElement: multiValue = true)
+    // the states under a "count" node of program["tree"] (CountStateElement: multiValue = true);
+    // returns the largest count bound ("max") in the tree
     @SuppressWarnings("unchecked")
-    private static void markCounts(Object node, boolean[] multi) {
+    private static int markCounts(Object node, boolean[] multi) {
         if (!(node instanceof Map)) {
-            return;
+            return 0;
         }
         Map<String, Object> n = (Map<String, Object>) node;
+        int mx = 0;
         if ("count".equals(n.get("t")) && n.get("state") instanceof Number) {
             multi[((Number) n.get("state")).intValue()] = true;
+            mx = n.get("max") instanceof Number ? ((Number) n.get("max")).intValue() : 0;
         }
         for (Object v : n.values()) {
             if (v instanceof Map) {
-                markCounts(v, multi);
+                mx = Math.max(mx, markCounts(v, multi));
             }
         }
+        return mx;
     }
 
     private static final class Reader {

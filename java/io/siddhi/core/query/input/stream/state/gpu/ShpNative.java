@@ -39,6 +39,8 @@ final class ShpNative {
     static final int LAYOUT_PAIRS32 = 3;
     /** count-sequence path: one uint32 per match, e2's batch index | L << 28 (include/siddhi_hip.h). */
     static final int LAYOUT_CHAIN32 = 4;
+    /** the engine's own compact form, resolved at create (PAIRS32 / CHAIN32 / FULL; shp_engine_stat "match_layout"). */
+    static final int LAYOUT_COMPACT = 5;
 
     static final int COMM_ID_BYTES = 128;
 
@@ -76,6 +78,10 @@ final class ShpNative {
     static final MethodHandle ENGINE_CREATE = fn("shp_engine_create", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
     static final MethodHandle PUSH_BATCH = fn("shp_push_batch", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
     static final MethodHandle PUSH_BATCH_DEVICE = fn("shp_push_batch_device", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
+    // host push, records in the engine's compact layout (no expansion): the runtime's push
+    static final MethodHandle PUSH_BATCH_COMPACT = fn("shp_push_batch_compact", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
+    // the oldest event an open partial still holds: the rows below it may be dropped (ColumnarBatch.trim)
+    static final MethodHandle OLDEST_LIVE_SEQ = fn("shp_engine_oldest_live_seq", JAVA_INT, ADDRESS, ADDRESS);
     static final MethodHandle FETCH_MATCHES = fn("shp_fetch_matches", JAVA_INT, ADDRESS, ADDRESS);
     static final MethodHandle ADVANCE_CLOCK = fn("shp_advance_clock", JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS);
     static final MethodHandle SNAPSHOT = fn("shp_snapshot", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);

@@ -1692,5 +1692,25 @@ int oracle_fetch(void* hp, int32_t* key, int64_t* ts, int8_t* type, int64_t* pos
   return 0;
 }
 
+// The oldest event (caller's sequence number) any open partial still holds: every StateEvent on a
+// pending or new-and-every list of every key and processor, each slot's chain followed to its end
+// (StreamPreStateProcessor.java:364-403 keeps a partial's StreamEvents alive for as long as it sits
+// on a list).  The next sequence number when nothing is open.  The checker of
+// shp_engine_oldest_live_seq (tests/test_retention.py).
+int64_t oracle_oldest_live_seq(void* hp) {
+  Engine& e = ((OracleHandle*)hp)->e;
+  const int64_t ne = (int64_t)e.ev_gseq.size();
+  int64_t lo = INT64_MAX;
+  for (auto& k : e.keys)
+    for (auto& ps : k->pre)
+      for (const auto* lst : {&ps.pending, &ps.newAndEvery})
+        for (auto& se : *lst)
+          for (auto& slot : se->slots)
+            for (auto ev = slot; ev; ev = ev->next)
+              if (ev->seq >= 0 && ev->seq < ne) lo = std::min(lo, e.ev_gseq[ev->seq]);
+  if (lo != INT64_MAX) return lo;
+  return ne > 0 ? e.ev_gseq[ne - 1] + 1 : 0;
+}
+
 void oracle_destroy(void* hp) { delete (OracleHandle*)hp; }
 }

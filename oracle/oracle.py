@@ -34,7 +34,8 @@ def lib():
         L.oracle_push.argtypes = [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 5
         L.oracle_push2.argtypes = [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 7
         L.oracle_advance.argtypes = [ctypes.c_void_p, ctypes.c_int64]
-        for f in ("oracle_num_matches", "oracle_num_refs", "oracle_timer_ties", "oracle_dropped_returns"):
+        for f in ("oracle_num_matches", "oracle_num_refs", "oracle_timer_ties", "oracle_dropped_returns",
+                  "oracle_oldest_live_seq"):
             getattr(L, f).restype = ctypes.c_int64
             getattr(L, f).argtypes = [ctypes.c_void_p]
         L.oracle_num_states.argtypes = [ctypes.c_void_p]
@@ -86,6 +87,10 @@ class OracleEngine:
 
     def dropped_returns(self):
         return lib().oracle_dropped_returns(self.h)
+
+    def oldest_live_seq(self):
+        """The oldest event any open partial holds (oracle_oldest_live_seq)."""
+        return lib().oracle_oldest_live_seq(self.h)
 
     def fetch(self):
         L = lib()

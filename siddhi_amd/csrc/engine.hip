@@ -371,6 +371,10 @@ struct shp_engine {
         throw CompileError(-2, "force_general 4: the query is not `every (x=X and y=Y) -> not Z for T` in playback");
       fast = 4;
     }
+    if (cfg.match_layout == SHP_LAYOUT_COMPACT)  // the path's own compact form (a host that decodes all)
+      cfg.match_layout = fast == 2 ? SHP_LAYOUT_PAIRS32
+                                   : (fast == 3 && !cseq_v1 && cfg.max_batch <= (int64_t)CH32_G ? SHP_LAYOUT_CHAIN32
+                                                                                                 : SHP_LAYOUT_FULL);
     if ((cfg.match_layout == SHP_LAYOUT_PAIRS || cfg.match_layout == SHP_LAYOUT_PAIRS32) && fast != 2)
       throw CompileError(-2, "match_layout PAIRS / PAIRS32 needs the sweep path");
     if (cfg.match_layout == SHP_LAYOUT_CHAIN32) {
@@ -848,7 +852,9 @@ struct shp_engine {
     int32_t maybe_null, pad;
   };
 
-  void snapshot(void** buf, size_t* len) {
+  void snapshot(void** buf, size_t* len) { snapshot_into(snap, buf, len); }
+
+  void snapshot_into(std::vector<char>& snap, void** buf, size_t* len) {
     HIP_OK(hipStreamSynchronize(stream));
     auto secs = state_sections();
     size_t payload = 0;
@@ -1003,6 +1009,7 @@ struct shp_engine {
     o += "},\"keys\":{";
     bool firstKey = true;
     auto ev = [&](std::string& s, int64_t seqv, int64_t tsv) {
+      if (live_min && seqv >= 0 && seqv < *live_min) *live_min = seqv;
       s += "{\"seq\":";
       jnum(s, seqv);
       s += ",\"ts\":";
@@ -1064,7 +1071,10 @@ struct shp_engine {
           ev(o, hseq[cs_hslot(i, k, C.M)], hts[cs_hslot(i, k, C.M)]);
         }
         o += "],[]]}]},\"LastEvent\":";
+        int64_t* const keep = live_min;  // the key's last event: history, not a partial's event
+        live_min = nullptr;
         ev(o, last, hts[cs_hslot(C.M - 1, k, C.M)]);
+        live_min = keep;
         o += "}";
       }
     } else if (fast == 2 || fast == 1) {
@@ -1232,6 +1242,30 @@ struct shp_engine {
     return o;
   }
 
+  // ---- the oldest event sequence number the committed state still names (shp_engine_oldest_live_seq):
+  // every event of an open partial -- a pending / new-and-every list entry of any state, a count
+  // chain, a logical slot, a pair waiting on an absent timer, a sweep carry or spill-pool entry.  A
+  // later push's matches name only these events and the later pushes' own, so a host that rebuilds
+  // match events from its own rows (ColumnarBatch) may drop every row below it.  The walk is the
+  // snapshot decoder's (describe), so it covers exactly what a snapshot would restore.
+  int64_t* live_min = nullptr;
+  std::vector<char> live_snap;
+  int64_t oldest_live_seq() {
+    void* b = nullptr;
+    size_t n = 0;
+    snapshot_into(live_snap, &b, &n);
+    int64_t m = seq;  // nothing open: every later match names only later events
+    live_min = &m;
+    try {
+      (void)describe(b, n);
+    } catch (...) {
+      live_min = nullptr;
+      throw;
+    }
+    live_min = nullptr;
+    return m;
+  }
+
   // sweep path, PAIRS layout: materialise the full records of the last push on demand
   void ensure_expanded() {
     if (expanded || cfg.match_layout == SHP_LAYOUT_AGG || (fast != 2 && fast != 3)) return;
@@ -1373,6 +1407,33 @@ struct shp_engine {
     out->refs = h_refs.data();
     out->agg = nullptr;
   }
+
+  // shp_push_batch_compact: the last push's records in the compact layout the engine produced them in
+  // (PAIRS32 / PAIRS on the sweep path, CHAIN32 on the count-sequence path, AGG rows), copied to
+  // the host as they are -- no expansion.  On a path that emits full records this is
+  // shp_fetch_matches: the caller reads out->layout.  The compact words keep the engine's per-key emission order; across
+  // keys they are in owner order, so a host that needs the reference's global order sorts them by
+  // e2's batch index (stable).
+  std::vector<uint32_t> h_words;
+  int fetch_compact(shp_matches* out) {
+    const int lay = cfg.match_layout;
+    const bool compact = !expanded && ((fast == 2 && (lay == SHP_LAYOUT_PAIRS32 || lay == SHP_LAYOUT_PAIRS)) ||
+                                       (fast == 3 && lay == SHP_LAYOUT_CHAIN32));
+    if (!compact) {
+      fetch(out);
+      return SHP_OK;
+    }
+    const int64_t m = last_m;
+    const int64_t words = lay == SHP_LAYOUT_PAIRS ? 4 * m : (lay == SHP_LAYOUT_PAIRS32 ? 2 * m : m);
+    h_words.resize((size_t)std::max<int64_t>(words, 1));
+    if (m) HIP_OK(hipMemcpy(h_words.data(), d_refs, (size_t)words * 4, hipMemcpyDeviceToHost));
+    *out = shp_matches{};
+    out->layout = lay;
+    out->m = m;
+    out->num_states = comp.P.nstates;
+    out->refs = (int64_t*)h_words.data();
+    return SHP_OK;
+  }
 };
 
 // ---------------------------------------------------------------- C-ABI
@@ -1504,6 +1565,25 @@ extern "C" int shp_engine_device_records(shp_engine* e, shp_matches* out, int64_
   });
 }
 
+int shp_engine_oldest_live_seq(shp_engine* e, int64_t* out) {
+  if (!e || !out) return SHP_ERR_ARG;
+  return guarded(e, [&]() {
+    *out = e->oldest_live_seq();
+    return SHP_OK;
+  });
+}
+
+int shp_push_batch_compact(shp_engine* e, const shp_batch* in, shp_matches* out) {
+  if (!e || !in || !out) return SHP_ERR_ARG;
+  return guarded(e, [&]() {
+    if (in->n > e->cfg.max_batch) return e->fail(SHP_ERR_ARG, "batch larger than max_batch");
+    e->stage(in, hipMemcpyHostToDevice);
+    int rc = e->run(in->n, false, nullptr, in->clock != nullptr, in->seq != nullptr);
+    if (rc != SHP_OK) return rc;
+    return e->fetch_compact(out);
+  });
+}
+
 int shp_fetch_matches(shp_engine* e, shp_matches* out) {
   if (!e || !out) return SHP_ERR_ARG;
   return guarded(e, [&]() {
@@ -1568,6 +1648,7 @@ int64_t shp_engine_stat(const shp_engine* e, const char* which) {
   if (w == "cseq_wide_reruns") return e->cseq_wide_reruns;
   if (w == "cseq_owner") return e->fast == 3 && e->cs.own ? 1 : 0;  // CHAIN32 pushes on the owner kernels
   if (w == "labs_fallbacks") return e->labs_fallbacks;
+  if (w == "match_layout") return e->cfg.match_layout;  // as resolved at create (SHP_LAYOUT_COMPACT)
   if (w == "spill_reruns") return e->spill_reruns;
   if (w == "spilled_owners") return e->fast == 2 ? e->sw.count_spilled() : 0;
   return -1;

@@ -22,7 +22,7 @@ _lib = None
 SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACITY",
               -4: "SHP_ERR_OUTPUT", -5: "SHP_ERR_DEVICE", -6: "SHP_ERR_KEYS"}
 
-SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches",
+SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches", "shp_push_batch_compact", "shp_engine_oldest_live_seq",
            "shp_advance_clock", "shp_engine_num_states", "shp_engine_state_stream", "shp_engine_path", "shp_last_kernel_ms", "shp_engine_stat",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
            "shp_dev_to_host", "shp_host_alloc", "shp_host_free", "shp_host_register",
@@ -41,7 +41,7 @@ class ShpConfig(ctypes.Structure):
                 ("force_general", ctypes.c_int32), ("profile_kernels", ctypes.c_int32),
                 ("match_layout", ctypes.c_int32)]
 
-LAYOUT_FULL, LAYOUT_PAIRS, LAYOUT_AGG, LAYOUT_PAIRS32, LAYOUT_CHAIN32 = 0, 1, 2, 3, 4
+LAYOUT_FULL, LAYOUT_PAIRS, LAYOUT_AGG, LAYOUT_PAIRS32, LAYOUT_CHAIN32, LAYOUT_COMPACT = 0, 1, 2, 3, 4, 5
 
 
 class ShpBatch(ctypes.Structure):
@@ -79,6 +79,8 @@ def lib():
         for f in ("shp_push_batch", "shp_push_batch_device"):
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpBatch), ctypes.POINTER(ShpMatches)]
         L.shp_fetch_matches.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpMatches)]
+        L.shp_push_batch_compact.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpBatch), ctypes.POINTER(ShpMatches)]
+        L.shp_engine_oldest_live_seq.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
         L.shp_advance_clock.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ShpMatches)]
         L.shp_engine_num_states.argtypes = [ctypes.c_void_p]
         L.shp_engine_state_stream.argtypes = [ctypes.c_void_p, ctypes.c_int32]
@@ -307,6 +309,45 @@ class HipEngine:
             self._check(L.shp_push_batch(self.h, ctypes.byref(b), ctypes.byref(mt)))
             out_all.append(matches_to_numpy(mt))
         self._pending = _concat(out_all, self._pending, self.S, self.layout)
+
+    def push_compact(self, ts, key, stream, cols, nulls, clock=None, seq=None):
+        """One push of host arrays through shp_push_batch_compact (the Java binding's push): the
+        records come back in the layout the engine produced them in, without expansion.  Returns
+        {"layout": L, "m": m, "words": uint32 array} for PAIRS32 (2 words per match) / CHAIN32 (1)
+        / PAIRS (4), or the FULL / AGG dict of fetch() with its "layout"."""
+        L = lib()
+        n = len(ts)
+        if n > self.max_batch:
+            raise ValueError("push_compact: batch larger than max_batch")
+        t = np.ascontiguousarray(ts, np.int64)
+        k = np.ascontiguousarray(key, np.int32)
+        s = np.ascontiguousarray(stream, np.int32)
+        cs = [np.ascontiguousarray(c) for c in cols]
+        ns = [None if m is None else np.ascontiguousarray(m, np.uint8) for m in nulls]
+        _check_columns(cs, ns, self.col_bytes, n)
+        colp = (ctypes.c_void_p * max(1, len(cs)))(*[c.ctypes.data for c in cs])
+        nulp = (ctypes.c_void_p * max(1, len(ns)))(*[0 if m is None else m.ctypes.data for m in ns])
+        ck = None if clock is None else np.ascontiguousarray(clock, np.int64)
+        sq = None if seq is None else np.ascontiguousarray(seq, np.int64)
+        b = ShpBatch(n, t.ctypes.data, k.ctypes.data, s.ctypes.data, ctypes.cast(colp, ctypes.c_void_p),
+                     ctypes.cast(nulp, ctypes.c_void_p), None if ck is None else ck.ctypes.data,
+                     None if sq is None else sq.ctypes.data)
+        mt = ShpMatches()
+        self._check(L.shp_push_batch_compact(self.h, ctypes.byref(b), ctypes.byref(mt)))
+        lay = int(mt.layout)
+        if lay in (LAYOUT_PAIRS32, LAYOUT_CHAIN32, LAYOUT_PAIRS):
+            per = {LAYOUT_PAIRS32: 2, LAYOUT_CHAIN32: 1, LAYOUT_PAIRS: 4}[lay]
+            return {"layout": lay, "m": int(mt.m), "words": _arr(mt.refs, int(mt.m) * per, np.uint32)}
+        out = matches_to_numpy(mt)
+        out["layout"] = lay
+        out["m"] = int(mt.m)
+        return out
+
+    def oldest_live_seq(self) -> int:
+        """shp_engine_oldest_live_seq: the oldest event an open partial of the committed state holds."""
+        v = ctypes.c_int64()
+        self._check(lib().shp_engine_oldest_live_seq(self.h, ctypes.byref(v)))
+        return int(v.value)
 
     def advance(self, now):
         mt = ShpMatches()

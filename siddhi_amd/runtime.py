@@ -23,6 +23,7 @@ from typing import Callable, Dict, List, Optional
 import numpy as np
 
 from .query.compiler import Dictionary, compile_app
+from .history import ChainRings, RowHistory, decode_pairs32
 from .query.selector import Selector
 
 _NP = {"int": np.int32, "long": np.int64, "float": np.float32, "double": np.float64,
@@ -81,25 +82,50 @@ class InputHandler:
             self.rt._enqueue(self.stream, self.rt._now_ms(), list(a))
 
 
+def _count_max(tree) -> int:
+    """The largest count bound <min:max> of the program's state tree (CHAIN32's chain length)."""
+    if not isinstance(tree, dict):
+        return 0
+    m = int(tree.get("max", 0)) if tree.get("t") == "count" else 0
+    return max([m] + [_count_max(tree[c]) for c in ("a", "b", "x") if c in tree])
+
+
 class _QueryRun:
-    def __init__(self, rt, cq, engine):
+    """One query's engine and what GpuStateStreamRuntime holds beside it: the pushed rows by
+    sequence number (RowHistory = ColumnarBatch's history, trimmed by the engine's oldest live
+    sequence number) and, for CHAIN32, the per-key rings of the last M events."""
+
+    def __init__(self, rt, cq, engine, min_trim):
         self.cq = cq
         self.engine = engine
-        self.selector = Selector(cq, rt._events, rt.strings)
+        self.history = RowHistory(min_trim)
+        self.selector = Selector(cq, self.history, rt.strings)
         self.callbacks: List[Callable] = []
-        self.local_to_app: List[int] = []
         self.streams = set(cq.partition_keys.keys()) if cq.partition_keys else \
             {lf.stream for lf in cq.leaves}
         self.stream_idx = cq.stream_index
         self.rows: List[tuple] = []
+        self.compact = hasattr(engine, "push_compact") and rt.compact
+        self.layout = engine.stat("match_layout") if self.compact else 0
+        self.rings = ChainRings(_count_max(cq.program["tree"])) if self.layout == 4 else None
+        self.retain = rt.retain and hasattr(engine, "oldest_live_seq")
 
 
 class SiddhiAppRuntime:
     def __init__(self, text: str, engine_factory: Callable, start_clock: Optional[int] = None,
-                 batch_size: int = 1 << 20, native_lowering: bool = False):
+                 batch_size: int = 1 << 20, native_lowering: bool = False, compact: bool = False,
+                 retain: bool = True, min_trim: int = 4096):
         """native_lowering: engines are created from the SiddhiQL text by the library
         (shp_engine_create_siddhiql), as the Java host does; string values then use the library's
-        dictionary, shared with the lowering's filter constants."""
+        dictionary, shared with the lowering's filter constants.
+        batch_size: events per push (1 = GpuStateStreamRuntime's FlushPolicy.SYNC with single sends).
+        compact: engines made with SHP_LAYOUT_COMPACT and pushed with shp_push_batch_compact, the
+        records decoded on the host (PAIRS32 / CHAIN32), as the Java binding does.
+        retain / min_trim: keep the pushed rows only from the engine's oldest live sequence number on
+        (history.RowHistory), asking the engine once the kept rows reach min_trim and have doubled."""
+        self.compact = compact
+        self.retain = retain
+        self.min_trim = min_trim
         self.text = text
         self.native_lowering = native_lowering
         if native_lowering:
@@ -109,7 +135,7 @@ class SiddhiAppRuntime:
             self.strings = Dictionary()
         self.keydict = Dictionary()
         self.app, self.compiled, _ = compile_app(text, self.strings)
-        self._events: List[tuple] = []  # app event id -> (stream idx, ts, data)
+        self._events: List[tuple] = []  # events not yet pushed: (stream idx, ts, data)
         self._pending: List[int] = []
         self._start_clock = start_clock
         self._engine_factory = engine_factory
@@ -150,14 +176,15 @@ class SiddhiAppRuntime:
         if self.queries:
             return
         start = self._start_clock if self._start_clock is not None else (0 if self.app.playback else self._t0)
+        kw = {"match_layout": 5} if self.compact else {}  # SHP_LAYOUT_COMPACT
         for cq in self.compiled:
             if self.native_lowering:
-                eng = self._engine_factory(cq.program_json(), start, siddhiql=(self.text, cq.name, self.strings))
+                eng = self._engine_factory(cq.program_json(), start, siddhiql=(self.text, cq.name, self.strings), **kw)
                 if eng.program_json != cq.program_json():
                     raise AssertionError(f"native lowering of {cq.name} differs from query.compiler")
             else:
-                eng = self._engine_factory(cq.program_json(), start)
-            self.queries[cq.name] = _QueryRun(self, cq, eng)
+                eng = self._engine_factory(cq.program_json(), start, **kw)
+            self.queries[cq.name] = _QueryRun(self, cq, eng, self.min_trim)
 
     def _enqueue(self, stream: str, ts: int, data: list):
         self._ensure_queries()
@@ -180,6 +207,9 @@ class SiddhiAppRuntime:
             return
         ids = self._pending
         self._pending = []
+        events = self._events
+        self._events = []  # the queries' histories keep what their engines may still name
+        ids = [i - ids[0] for i in ids]
         stream_names = list(self.app.streams.keys())
         for qr in self.queries.values():
             if self.app.playback:
@@ -188,14 +218,13 @@ class SiddhiAppRuntime:
                 # fires its timers -- pushed as clock-only events (stream -1)
                 sel = list(ids)
             else:
-                sel = [i for i in ids if stream_names[self._events[i][0]] in qr.streams]
+                sel = [i for i in ids if stream_names[events[i][0]] in qr.streams]
             if not sel:
                 continue
-            self._push(qr, sel, stream_names)
-            self._drain(qr)
+            self._push(qr, [events[i] for i in sel], stream_names)
 
-    def _push(self, qr: _QueryRun, sel: List[int], stream_names):
-        n = len(sel)
+    def _push(self, qr: _QueryRun, evs: List[tuple], stream_names):
+        n = len(evs)
         ts = np.empty(n, np.int64)
         key = np.zeros(n, np.int32)
         stream = np.empty(n, np.int32)
@@ -205,8 +234,8 @@ class SiddhiAppRuntime:
             cols.append(np.zeros(n, _NP[t]))
             nulls.append(np.zeros(n, np.uint8))
         pk = qr.cq.partition_keys
-        for j, i in enumerate(sel):
-            s, t, data = self._events[i]
+        for j, ev in enumerate(evs):
+            s, t, data = ev
             ts[j] = t
             stream[j] = s
             sname = stream_names[s]
@@ -229,32 +258,49 @@ class SiddhiAppRuntime:
                 else:
                     cols[c][j] = v
         null_ptrs = [m if m.any() else None for m in nulls]
-        qr.engine.push(ts, key, stream, cols, null_ptrs)
-        qr.local_to_app.extend(sel)
+        if qr.compact:
+            res = qr.engine.push_compact(ts, key, stream, cols, null_ptrs)
+        else:
+            qr.engine.push(ts, key, stream, cols, null_ptrs)
+            res = None
+        # the engine took the push (its sequence counter moved by n): the rows join the history
+        seq0 = qr.history.add_block(list(evs))
+        if res is not None and res["layout"] == 3:  # PAIRS32
+            for i, slots in decode_pairs32(res["words"], seq0):
+                self._deliver(qr, int(key[i]), int(ts[i]), 0, slots)
+        elif res is not None and res["layout"] == 4:  # CHAIN32
+            for i, slots in qr.rings.decode(res["words"], key, stream >= 0, seq0):
+                self._deliver(qr, int(key[i]), int(ts[i]), 0, slots)
+        else:
+            self._drain(qr, res)
+        if qr.retain:
+            qr.history.maybe_trim(qr.engine.oldest_live_seq)
 
-    def _drain(self, qr: _QueryRun):
-        mb = qr.engine.fetch()
+    def _deliver(self, qr: _QueryRun, key: int, ts: int, etype: int, slots):
+        row = qr.selector.select(key, ts, etype, slots)
+        if row is None:
+            return
+        qr.rows.append((ts, row))
+        for cb in qr.callbacks:
+            cb(ts, [Event(ts, row)], None)
+
+    def _drain(self, qr: _QueryRun, mb=None):
+        """FULL records (slots name events by the engine's sequence numbers = history positions)."""
+        if mb is None:
+            mb = qr.engine.fetch()
         m = len(mb["key"])
         if m == 0:
             return
         S = mb["slot_len"].shape[1] if m else 0
         refs = mb["refs"]
         off = 0
-        l2a = qr.local_to_app
         for i in range(m):
             slots = []
             for s in range(S):
                 ln = int(mb["slot_len"][i, s])
-                chain = [l2a[int(x)] if x >= 0 else -1 for x in refs[off:off + ln]]
+                slots.append([int(x) for x in refs[off:off + ln]])
                 off += ln
-                slots.append(chain)
-            row = qr.selector.select(int(mb["key"][i]), int(mb["ts"][i]), int(mb["type"][i]), slots)
-            if row is None:
-                continue
-            t = int(mb["ts"][i])
-            qr.rows.append((t, row))
-            for cb in qr.callbacks:
-                cb(t, [Event(t, row)], None)
+            self._deliver(qr, int(mb["key"][i]), int(mb["ts"][i]), int(mb["type"][i]), slots)
 
 
 class SiddhiManager:

@@ -241,7 +241,127 @@ def test_layout_constants_match_the_header():
     """SHP_LAYOUT_* of include/siddhi_hip.h, ShpNative.LAYOUT_* and siddhi_amd.native.LAYOUT_* agree."""
     hdr = open(os.path.join(ROOT, "include", "siddhi_hip.h")).read()
     want = {k: int(v) for k, v in re.findall(r"#define SHP_LAYOUT_(\w+) (\d+)", hdr)}
-    assert set(want) == {"FULL", "PAIRS", "AGG", "PAIRS32", "CHAIN32"}
+    assert set(want) == {"FULL", "PAIRS", "AGG", "PAIRS32", "CHAIN32", "COMPACT"}
     java = {k: int(v) for k, v in re.findall(r"static final int LAYOUT_(\w+) = (\d+);", _java("ShpNative.java"))}
     assert java == want
     assert {k: getattr(native, "LAYOUT_" + k) for k in want} == want
+
+
+# ------------------------------------------------------------------ partition wiring (8f-2)
+REF_CORE = "/root/reference/modules/siddhi-core/src/main/java/io/siddhi/core"
+# the supertypes the reference declares for the stream runtimes PartitionRuntimeImpl dispatches on
+REF_SUPERS = {"StateStreamRuntime": ["StreamRuntime"], "SingleStreamRuntime": ["StreamRuntime"],
+              "JoinStreamRuntime": ["StreamRuntime"]}
+
+
+def _type_chain(src, cls):
+    m = re.search(r"public (?:final )?class " + cls + r" (?:extends (\w+))?\s*(?:implements ([\w, ]+))?\{", src)
+    assert m, f"no class declaration for {cls}"
+    chain, todo = [cls], [t.strip() for t in (m.group(1) or "").split(",") + (m.group(2) or "").split(",") if t.strip()]
+    while todo:
+        t = todo.pop(0)
+        chain.append(t)
+        todo += REF_SUPERS.get(t, [])
+    return chain
+
+
+def _partition_branch(chain):
+    """PartitionRuntimeImpl.addPartitionReceiver (core/partition/PartitionRuntimeImpl.java:243-258):
+    the instanceof dispatch that decides whether a query's outer streams get PartitionStreamReceivers."""
+    for t, branch in (("SingleStreamRuntime", "single"), ("JoinStreamRuntime", "join"), ("StateStreamRuntime", "state")):
+        if t in chain:
+            return branch
+    return None  # no receiver: the query would never see a partitioned stream's events
+
+
+def _wired_streams(tree, states, streams):
+    """addPartitionReceiverForStateElement (:262-288): Every -> inner, Next -> current then next,
+    Count -> inner, Logical -> element 1 then 2, stream -> one receiver with the next executor index."""
+    out = []
+
+    def walk(n):
+        t = n["t"]
+        if t == "every":
+            walk(n["x"])
+        elif t == "next":
+            walk(n["a"])
+            walk(n["b"])
+        elif t == "logical":
+            walk(n["s1"])
+            walk(n["s2"])
+        else:  # stream, count, absent: one StreamStateElement
+            out.append(streams[states[n["state"]]["stream"]]["name"])
+    walk(tree)
+    return out
+
+
+@pytest.mark.parametrize("cfg", [2, 3, "3b", 4, 5])
+def test_partitioned_queries_reach_the_state_branch_and_subscribe_every_stream(cfg):
+    """C2-C5 are partitioned: the runtime's type takes PartitionRuntimeImpl's StateStreamRuntime
+    branch, every stream the query reads gets its PartitionStreamReceiver, and
+    PartitionStreamReceiver.addStreamJunction (:291-310: for i < getInputStreamId().size(), subscribe
+    runtime i's receiver when its stream is the junction's) subscribes one of our runtimes to each."""
+    rt = _java("GpuStateStreamRuntime.java")
+    chain = _type_chain(rt, "GpuStateStreamRuntime")
+    assert _partition_branch(chain) == "state", chain
+    app, qs, _ = parse_app_and_compile(cfg)
+    prog = qs[0].program
+    assert prog["partitioned"]
+    wired = _wired_streams(prog["tree"], prog["states"], prog["streams"])
+    read = {prog["streams"][s["stream"]]["name"] for s in prog["states"]}
+    assert set(wired) == read and len(wired) == len(prog["states"])
+    # getInputStreamId() = StateInputStream.getAllStreamIds (collectStreamIds: the same walk), and the
+    # runtimes are ProgramInfo.stateStream in state order (one SingleStreamRuntime per state)
+    runtime_stream = [prog["streams"][s["stream"]]["name"] for s in sorted(prog["states"], key=lambda s: s["id"])]
+    for stream in set(wired):
+        assert any(runtime_stream[i] == stream for i in range(len(wired))), (stream, runtime_stream)
+
+
+def parse_app_and_compile(cfg):
+    from siddhi_amd.query.compiler import compile_app
+    return compile_app(synth.QUERIES[cfg])
+
+
+def test_runtime_extends_state_stream_runtime_and_overrides_its_inner_runtime_calls():
+    rt = _java("GpuStateStreamRuntime.java")
+    assert "import io.siddhi.core.query.input.stream.state.StateStreamRuntime;" in rt
+    ctor = rt[rt.index("GpuStateStreamRuntime(String appText, String queryName, ProgramInfo info"):]
+    body = ctor[ctor.index("{") + 1:]
+    # StateStreamRuntime(SiddhiQueryContext, MetaStateEvent) (StateStreamRuntime.java:44): first statement
+    assert body.lstrip().startswith("super(queryContext, metaStateEvent);")
+    # every StateStreamRuntime method that reads its innerStateRuntime (null here) is overridden
+    for m in ("getSingleStreamRuntimes()", "setCommonProcessor(Processor", "resetAndUpdate()", "initPartition()",
+              "getMetaComplexEvent()", "getProcessingMode()", "getQuerySelector()"):
+        assert re.search(r"@Override\s+public [\w<>]+ " + re.escape(m), rt), m
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CORE), reason="reference sources not present")
+def test_reference_dispatch_is_the_one_restated():
+    """The restated dispatch and walk are the reference's (read as text where the sources exist)."""
+    src = open(os.path.join(REF_CORE, "partition", "PartitionRuntimeImpl.java")).read()
+    assert "instanceof SingleStreamRuntime" in src and "instanceof JoinStreamRuntime" in src
+    assert "} else if (queryRuntime.getStreamRuntime() instanceof StateStreamRuntime) {" in src
+    st = open(os.path.join(REF_CORE, "query", "input", "stream", "state", "StateStreamRuntime.java")).read()
+    assert "public class StateStreamRuntime implements StreamRuntime" in st
+    for m in ("public void resetAndUpdate()", "public void initPartition()",
+              "public StateStreamRuntime(SiddhiQueryContext siddhiQueryContext, MetaStateEvent metaStateEvent)"):
+        assert m in st, m
+
+
+def test_runtime_pushes_compact_and_trims_by_oldest_live_seq():
+    """The Java flush follows the mirror's rules (siddhi_amd/runtime.py, tests/test_retention.py):
+    SHP_LAYOUT_COMPACT, shp_push_batch_compact, commit then decode, trim by the engine's report;
+    no fixed push-count history is left."""
+    rt = _java("GpuStateStreamRuntime.java")
+    cb = _java("ColumnarBatch.java")
+    assert "ShpNative.CFG_MATCH_LAYOUT, ShpNative.LAYOUT_COMPACT" in rt
+    assert "ShpNative.PUSH_BATCH_COMPACT.invokeExact(engine, batch.descriptor(), matches)" in rt
+    flush = rt[rt.index("void flush()"):rt.index("private long oldestLiveSeq()")]
+    assert flush.index("batch.commit()") < flush.index("deliver(seq0, pushed)") < flush.index("batch.maybeTrim(")
+    assert "ShpNative.OLDEST_LIVE_SEQ.invokeExact(engine, out)" in rt
+    for dec in ("deliverPairs32", "deliverChain32", "deliverFull"):
+        assert f"private void {dec}(" in rt
+    assert "historyBatches" not in cb and "history.size() >" not in cb
+    assert "void maybeTrim(LongSupplier oldestLive)" in cb and "void trim(long lo)" in cb
+    src = _java("ShpNative.java")
+    assert re.search(r"LAYOUT_COMPACT = 5;", src)
