@@ -1712,5 +1712,21 @@ int64_t oracle_oldest_live_seq(void* hp) {
   return ne > 0 ? e.ev_gseq[ne - 1] + 1 : 0;
 }
 
+// Debugging aid (tests only): key `key`'s timer queue of scheduler 0 into out[0..cap), then the
+// absent processor's lastScheduledTime; returns the queue length (or -1: no such key)
+int64_t oracle_debug_queue(void* hp, int32_t key, int64_t* out, int64_t cap) {
+  Engine& e = ((OracleHandle*)hp)->e;
+  auto it = e.keyIndex.find(key);
+  if (it == e.keyIndex.end() || e.schedulers.empty()) return -1;
+  oracle::KeyCtx* k = e.keys[it->second].get();
+  int64_t n = 0;
+  for (int64_t t : k->sched[0].queue) {
+    if (n < cap) out[n] = t;
+    n++;
+  }
+  if (n < cap) out[n] = k->pre[e.schedulers[0]->id].lastScheduledTime;
+  return n;
+}
+
 void oracle_destroy(void* hp) { delete (OracleHandle*)hp; }
 }

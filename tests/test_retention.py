@@ -124,13 +124,15 @@ def _hip_factory(max_keys):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,n,keys,ms,layout", [(2, 100_000, 10_000, 0.05, 3), ("3b", 100_000, 1_000, 1, 4),
-                                                  (5, 30_000, 10_000, 0.05, 3), (3, 20_000, 1_000, 1, 0),
+@pytest.mark.parametrize("cfg,n,keys,ms,layout", [(2, 200_000, 10_000, 0.05, 3), ("3b", 100_000, 1_000, 1, 4),
+                                                  (5, 60_000, 2_000, 0.2, 3), (3, 20_000, 1_000, 1, 0),
                                                   (4, 20_000, 100, 5, 0)])
 def test_sync_pushes_compact_with_engine_retention(cfg, n, keys, ms, layout):
-    """C2 and C3' for 10^5 single-event pushes (C5, C3 and C4 shorter): the HIP engine's compact
-    records decoded on the host, rows kept from shp_engine_oldest_live_seq on, the output equal to the
-    oracle's.  On the sequences the engine's report equals the oracle's oldest live event."""
+    """C2 (10k keys, 2*10^5 pushes) and C3' (10^5 pushes) one event per push (C5, C3 and C4 shorter):
+    the HIP engine's compact records decoded on the host, rows kept from shp_engine_oldest_live_seq on,
+    the output equal to the oracle's.  A candidate the reference leaves on a pending list stays there
+    until its key's next event, so at 10k keys the live rows span ~10^5 events (the least recently
+    seen key's): the C2 run is long enough for the history to be trimmed well below what it pushed."""
     evs = _events(cfg, n, keys, ms)
     want = _rows(_run(_oracle_factory, cfg, evs, retain=False))
     rt = _run(_hip_factory(max(keys, 256)), cfg, evs, batch_size=1, compact=True, min_trim=256)
