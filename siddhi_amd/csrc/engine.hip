@@ -365,12 +365,12 @@ struct shp_engine {
         SweepState::build_map(cfg.max_keys, nown, kmap))
       fast = 2;
     if (!fast && cfg.force_general != 1 && CseqState::shape_ok(comp.P, comp.cseq)) fast = 3;
-    // the logical-absent kernel is opt-in: it needs per-key ordered timestamps (labs.h)
-    if (!fast && cfg.force_general == 4) {
-      if (!LabsState::shape_ok(comp.P, comp.labs))
-        throw CompileError(-2, "force_general 4: the query is not `every (x=X and y=Y) -> not Z for T` in playback");
+    // the logical-absent automaton (labs.h): exact for any timestamp order, the default for its shape
+    if (!fast && cfg.force_general == 4 && !LabsState::shape_ok(comp.P, comp.labs))
+      throw CompileError(-2, "force_general 4: the query is not `every (x=X and y=Y) -> not Z for T` in playback");
+    if (!fast && (cfg.force_general == 0 || cfg.force_general == 4) && LabsState::shape_ok(comp.P, comp.labs) &&
+        !getenv("SHP_NO_LABS"))
       fast = 4;
-    }
     if (cfg.match_layout == SHP_LAYOUT_COMPACT)  // the path's own compact form (a host that decodes all)
       cfg.match_layout = fast == 2 ? SHP_LAYOUT_PAIRS32
                                    : (fast == 3 && !cseq_v1 && cfg.max_batch <= (int64_t)CH32_G ? SHP_LAYOUT_CHAIN32
@@ -741,9 +741,6 @@ struct shp_engine {
       if (herr & SWE_KEYS) return fail(SHP_ERR_KEYS, "partition key id >= max_keys");
       if (herr & SWE_BOUND) return fail(SHP_ERR_DEVICE, "internal: a match pair names an event outside its push (SWE_BOUND)");
       if (fast == 4 && (herr & LA_BOUND)) return fail(SHP_ERR_DEVICE, "logical-absent path: a key's records overflowed its region");
-      if (fast == 4 && (herr & LA_UNORDERED))
-        return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the logical-absent path (force_general 4); "
-                                         "the general lanes (force_general 1) replay such streams");
       if (herr & E_OUT) return fail(SHP_ERR_OUTPUT, "match buffer too small for this batch (max_matches)");
       if (herr & SWE_MONO) return fail(SHP_ERR_UNSUPPORTED, "timestamps decrease within a key on the 2-state scan kernels");
       if (herr & SWE_RANGE)
@@ -819,7 +816,8 @@ struct shp_engine {
       v.push_back({D.p_null[c], pc});
     } else if (fast == 4) {
       const LabsDev& L = la.D;
-      v = {{L.pend[L.cur], (size_t)nk * sizeof(LaPend)}, {L.wq[L.cur], (size_t)nk * L.wcap * sizeof(LaWait)}};
+      v = {{L.pend[L.cur], (size_t)nk * sizeof(LaPend)}, {L.wq[L.cur], (size_t)nk * L.wcap * sizeof(LaWait)},
+           {L.fq[L.cur], (size_t)nk * L.wcap * sizeof(LaEnt)}};
     } else if (fast == 3) {
       const CseqDev& C = cs.D;
       const int c = C.cur;
@@ -895,8 +893,8 @@ struct shp_engine {
     if (fast == 0 && (h.pad < 0 || h.pad >= LANE_TIERS)) return fail(SHP_ERR_ARG, "snapshot capacity tier unknown");
     if (fast == 4 && h.pad != la.tier) {  // the waits rings of the snapshot's tier
       if (h.pad < 0 || h.pad >= LA_TIERS) return fail(SHP_ERR_ARG, "snapshot capacity tier unknown");
-      const size_t need = sizeof h + 16 + (size_t)cfg.max_keys * sizeof(LaPend) +
-                          (size_t)cfg.max_keys * LA_CAPS[h.pad] * sizeof(LaWait);
+      const size_t need = sizeof h + 24 + (size_t)cfg.max_keys * sizeof(LaPend) +
+                          (size_t)cfg.max_keys * LA_CAPS[h.pad] * (sizeof(LaWait) + sizeof(LaEnt));
       if (need != len) return fail(SHP_ERR_ARG, "snapshot layout mismatch");
       if (!la.set_tier(h.pad, false, stream)) return fail(SHP_ERR_CAPACITY, "no device memory for the snapshot's tier");
     }
@@ -983,6 +981,7 @@ struct shp_engine {
     if (fast == 4) {
       if (h.pad < 0 || h.pad >= LA_TIERS) throw std::runtime_error("snapshot capacity tier unknown");
       secs[1].bytes = (size_t)cfg.max_keys * LA_CAPS[h.pad] * sizeof(LaWait);
+      secs[2].bytes = (size_t)cfg.max_keys * LA_CAPS[h.pad] * sizeof(LaEnt);
     }
     std::vector<const char*> sp(secs.size());
     const char* q = (const char*)buf + sizeof h;
@@ -1017,9 +1016,11 @@ struct shp_engine {
       s += "}";
     };
     if (fast == 4) {
-      // logical-absent: the logical partial (x / y slots) and the pairs waiting on the absent state
+      // logical-absent: the logical partial (x / y slots), the pairs on the absent state's pending and
+      // new-and-every lists, its lastScheduledTime and the key's Scheduler queue
       const LaPend* pd = (const LaPend*)sp[0];
       const LaWait* wq = (const LaWait*)sp[1];
+      const LaEnt* fq = (const LaEnt*)sp[2];
       const LabsDev& L = la.D;
       const int64_t wcap = LA_CAPS[h.pad >= 0 && h.pad < LA_TIERS ? h.pad : 0];
       for (int32_t k = 0; k < cfg.max_keys; k++) {
@@ -1036,14 +1037,25 @@ struct shp_engine {
         o += "]}}]},\"absent\":{\"PendingStateEventList\":[";
         for (int i = 0; i < s.nw; i++) {
           const LaWait& w = wq[(int64_t)k * wcap + ((s.wh + i) & (wcap - 1))];
-          if (i) o += ",";
-          o += "{\"due\":";
+          if (i == s.nw - s.nae) o += "],\"NewAndEveryStateEventList\":[";
+          else if (i) o += ",";
+          o += "{\"ts\":";
+          jnum(o, w.due - L.wait);
+          o += ",\"due\":";
           jnum(o, w.due);
           o += ",\"slots\":[";
           ev(o, w.xseq, w.xts);
           o += ",";
           ev(o, w.yseq, w.yts);
           o += "]}";
+        }
+        if (s.nae == 0) o += "],\"NewAndEveryStateEventList\":[";
+        o += "],\"LastScheduledTime\":";
+        jnum(o, s.lst);
+        o += "},\"scheduler0\":{\"ToNotifyQueue\":[";
+        for (int i = 0; i < s.ne; i++) {
+          if (i) o += ",";
+          jnum(o, fq[(int64_t)k * wcap + ((s.eh + i) & (wcap - 1))].t);
         }
         o += "]}}";
       }

@@ -1,38 +1,30 @@
 // siddhi-hip: the logical-absent path, the playback pattern
 //   every (x=X[fx] and y=Y[fy]) -> not Z[fz] for T [within W]        
-// over three distinct streams (engine path 4, opt-in: shp_config.force_general = 4).
+// over three distinct streams (engine path 4, the default for this shape).
 //
 // For this shape the LogicalPre/PostStateProcessor pair (LogicalPreStateProcessor.java
 // processAndReturn :128-167, addEveryState :65-84), the AbsentStreamPre/PostStateProcessor
 // (AbsentStreamPreStateProcessor.java addState :80-103, processAndReturn :257-274, the timer
-// process(ComplexEventChunk) :151-227) and the playback Scheduler (Scheduler.java :71-103, 171-209)
-// reduce, per partition key whose timestamps do not decrease, to:
+// process(ComplexEventChunk) :151-227) and the playback Scheduler (Scheduler.java :71-103, 113-127,
+// 171-209) reduce, per partition key, to:
 //   pend    the one logical partial: an x slot and a y slot (StateEvent with e1 / e2);
-//   waits   completed (x, y) pairs waiting on the absent state, in completion order, each due at
-//           completion ts + T.
-// On each event of the key, after the timers the clock reached have fired:
-//   a filled pend slot older than W (|slot ts - ts| > W, StreamPreStateProcessor.expireEvents
-//   :326-361) resets pend (the every re-arms it);
-//   X event with fx: fills x if empty; with y filled the pair completes: waits += (x, y, due), pend
-//   re-arms (LogicalPostStateProcessor.process :59-87 -> addState on the absent state).  Y alike;
-//   Z event: every wait with fz(z, x, y) is dropped (AbsentStreamPostStateProcessor.process :36-56).
-// A wait fires at the first event (any key) whose playback clock reaches its due time: the match
-// (ts = due, per-state slots x, y, -) is emitted if both x and y are within W of due
-// (isExpired at the timer, AbsentStreamPreStateProcessor :198-213).  The rule was derived from and
-// is checked against the oracle's restatement of those processors (tests/test_labs.py, CPU and
-// GPU).  Cross-key ties of the playback scheduler's TreeMultimap (one state per due time) are not
-// modelled, as on the general lanes (parity-unpinned).  A key whose timestamps
-// decrease fails the push with SHP_ERR_UNSUPPORTED (the general lanes, force_general = 1, replay
-// such streams exactly).  The waiting pairs of a key form a ring of wcap entries: 16 in LDS at
-// first, growing x16 per tier in HBM (256, 4096, 65536, ... capacity tiers, as the general lanes
-// have) when a push overflows it; the push then re-runs from the committed state.
+//   pairs   completed (x, y) pairs on the absent state's lists, in list order, the last `nae` of
+//           them on its new-and-every list;
+//   queue   the key's Scheduler queue, a FIFO of notify times, and lastScheduledTime.
+// k_labs runs that state event by event for ANY timestamp order (the rule is stated and checked
+// against the oracle in tests/labs_exact.py): a queue entry fires at the first send whose clock
+// reaches it and sets the clock, behind the entries ahead of it; its timer emits the pending pairs
+// at least T old (ts = the entry), drops the expired ones, and re-arms when it emitted nothing.
+// k_labs_w runs the ordered special case (a key's events do not go back in time, no event lags the
+// clock by T, no clock step beyond T: then the queue stays sorted and a pair fires at its due time)
+// a wave per key, 64 events a step, and leaves the same state; anything else raises LA_SLOW and
+// k_labs re-runs the push from the committed state.  Cross-key ties of the playback scheduler's
+// TreeMultimap (one state per due time per onTimeChange) are not modelled, as on the general lanes
+// (parity-unpinned).  The rings (pairs, queue) start at 8 per key and grow x16 per
+// tier in HBM when a push overflows them (the push then re-runs from the committed state).
 //
-// Kernels: the batch is partitioned by key with the engine's stable radix sort; k_labs runs one
-// thread per key over its events in arrival order (pend in registers, waits in LDS), twice: a
-// count pass, an exclusive scan over the keys, and the pass that writes each key's records
-// contiguously and the state.  Which event fired a timer is fixed afterwards by k_labs_pos: a
-// binary search of the running clock over the events between the key's previous event and the
-// one that reached the due time.
+// Batch order: the events are packed into 16-byte records and sorted with their keys (k_labs_pack2
+// + one rocPRIM radix sort), so each key's events are contiguous.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -59,7 +51,6 @@ struct __attribute__((aligned(16))) LaEv {  // one event: packed (32 B, one sect
   int32_t st;
   uint32_t n;
 };
-constexpr int LA_UNORDERED = 1 << 27;  // a key's timestamps decrease (this path needs them ordered)
 constexpr int LA_WIDE = 1 << 26;       // a push's ts / clock leave base +- 2^31 ms or its batch index 2^27:
                                         // the push re-runs with the 32-byte records (not an error)
 
@@ -96,14 +87,26 @@ struct __attribute__((aligned(8))) LaRec {
   uint32_t flo, fhi;  // the fire event is the first batch index in [flo, fhi] whose clock reaches due
 };
 
+// one timer entry of the key's Scheduler queue (ToNotifyQueue, a FIFO: Scheduler.java:113-127, 332)
+struct __attribute__((aligned(8))) LaEnt {
+  int64_t t;    // notify time
+  int32_t i0;   // the first batch index of the current push it may fire at (0 for carried entries)
+  int32_t pad;
+};
+
 struct LaPend {
   int64_t xseq, xts, yseq, yts;  // seq -1: slot empty
   uint32_t xv, yv;
   uint32_t fl;    // 1 x null, 2 y null
-  int32_t nw;     // waits held
-  int32_t wh;     // ring head of the waits
-  int32_t pad;
+  int32_t nw;     // pairs held on the absent state's lists
+  int32_t wh;     // ring head of the pairs
+  int32_t nae;    // the last nae of them are on its new-and-every list (the rest pending)
   int64_t last;   // ts of the key's latest event (INT64_MIN: none)
+  int64_t lst;    // AbsentStreamPreStateProcessor's lastScheduledTime
+  int32_t ne;     // timer entries queued
+  int32_t eh;     // ring head of the entries
+  int32_t reg;    // 1: regular -- k_labs_w may run from this state (la_regular)
+  int32_t pad;
 };
 
 struct LabsDev {
@@ -117,9 +120,11 @@ struct LabsDev {
   int32_t nk, cur;
   int32_t wcap, pad1;  // waits ring per key (LA_CAPS[tier])
   LaPend* pend[2];   // nk
-  LaWait* wq[2];     // nk * wcap
-  LaWait* wtmp;      // nk * wcap: the count pass's working rings (tiers >= 1)
-  int64_t* aux;      // per record of the push: last batch index the timer can have fired at
+  LaWait* wq[2];     // nk * wcap: the pairs on the absent state's lists
+  LaWait* wtmp;      // nk * wcap: the count pass's working rings
+  LaEnt* fq[2];      // nk * wcap: the timer entries (Scheduler queue)
+  LaEnt* ftmp;       // nk * wcap: the count pass's working entry rings
+  unsigned long long* maxstep;  // the push's largest clock step after its first event (k_labs_steps)
   uint32_t *cm, *om; // nk: records per key (count pass), their exclusive scan
   // the batch in key order (k_labs_gather): one thread per key then reads its events
   // contiguously; random gathers from 16 waves were bound by address translation (5 us an event)
@@ -250,25 +255,95 @@ __device__ __forceinline__ bool la_pred(const LaPredD& p, const LaVals& V) {
   return p.combine ? (a || b) : (a && b);
 }
 
-// HBMQ: the waits ring is worked on in HBM (tiers >= 1: the committed ring is copied to the
-// pass's own ring first); otherwise in LDS (tier 0)
+// ------------------------------------------------------------------ k_labs: the exact rule
+// One thread per key over its events in arrival order, with the state of the reference's
+// processors for this shape (tests/labs_exact.py states it and checks it against the oracle for any
+// timestamp order):
+//   the logical partial (x / y slots);
+//   the pairs on the absent state's lists in list order, the last `nae` of them on new-and-every
+//     (AbsentStreamPreStateProcessor.addState :80-103 appends there; updateState moves them, stably
+//     sorted by ts, StreamPreStateProcessor.java:308-323);
+//   the key's Scheduler queue (a FIFO of notify times, Scheduler.java:113-127, 332) and
+//     lastScheduledTime.
+// A queue entry fires at the first send at or after it was queued whose clock reaches it and that
+// sets the clock (TimestampGeneratorImpl.setCurrentTimestamp :105-121: a send below the clock fires
+// no timer), behind the entries ahead of it; the timer then runs AbsentStreamPreStateProcessor.process
+// (:151-227): new-and-every -> pending, expired pairs dropped, due pairs emitted with ts = the entry,
+// lastScheduledTime = clock + T when the clock passed entry + T, and with nothing emitted and
+// lastScheduledTime below the entry a re-arm entry + T.  Each key event: the timers its send fires,
+// then expireEvents (the partial; the pending list's expired head, every expired new-and-every pair),
+// then Z: new-and-every -> pending and each pending pair fz matches is dropped with a queue entry
+// ts + T (AbsentStreamPostStateProcessor.process :36-56 -> updateLastArrivalTime :68-78); X / Y: a
+// slot fill, and with both slots the pair joins new-and-every with an entry ts + T.
+// Two passes: EMIT = false counts each key's records (working rings: wtmp / ftmp), EMIT = true
+// writes them at the key's offset (an exclusive scan of the counts) and the state into copy wr.
+// The rings grow by capacity tier (E_LIST: the push re-runs at the next one).
+__device__ __forceinline__ bool la_expired(int64_t xts, int64_t yts, int64_t t, int64_t W) {
+  return W >= 0 && (llabs(xts - t) > W || llabs(yts - t) > W);
+}
+
+// the batch index at which a queue entry for time t fires, queued so that it may fire from batch
+// index i0 on: the first send at or after i0 whose clock reaches t and sets the clock; B.n: not in
+// this push (the playback clock B.rmax is non-decreasing; a send sets it iff tclk == rmax)
+__device__ int64_t la_fire_at(const BatchView& B, int64_t t, int64_t i0) {
+  const int64_t n = B.n;
+  if (i0 >= n) return n;
+  int64_t a = i0, b = n;
+  while (a < b) {
+    const int64_t m = a + ((b - a) >> 1);
+    if (B.rmax[m] >= t) b = m;
+    else a = m + 1;
+  }
+  if (a < n && a == i0 && (i0 == 0 ? B.clock0 : B.rmax[i0 - 1]) >= t)
+    while (a < n && B.tclk[a] != B.rmax[a]) a++;  // the clock was already there: the next send that sets it
+  return a;
+}
+
+// the state k_labs_w may run from (its ordered formulation holds for events that do not go back in
+// time): queue sorted, its last entry <= last ts + T and <= lastScheduledTime (no re-arm), pairs in
+// ts order at or before the last event, the pending pairs' expiry bounds in list order, the partial's
+// slots between the pairs' slots and the last event
+__device__ __forceinline__ int la_regular(const LaPend& s, const LaWait* wq, const LaEnt* fq, int msk, int64_t W,
+                                          int64_t T) {
+  const int64_t Wn = W >= 0 ? W : (1ll << 60);
+  for (int i = 1; i < s.ne; i++)
+    if (fq[(s.eh + i) & msk].t < fq[(s.eh + i - 1) & msk].t) return 0;
+  if (s.ne > 0) {
+    const int64_t tmax = fq[(s.eh + s.ne - 1) & msk].t;
+    if (s.last == INT64_MIN || tmax > s.last + T || s.lst < tmax) return 0;
+  }
+  int64_t pdue = INT64_MIN, pd = INT64_MIN, slots = INT64_MIN;
+  for (int i = 0; i < s.nw; i++) {
+    const LaWait& w = wq[(s.wh + i) & msk];
+    if (w.due < pdue || w.due - T > s.last) return 0;
+    pdue = w.due;
+    const int64_t d = min(w.xts, w.yts) + Wn;
+    if (i < s.nw - s.nae && d < pd) return 0;
+    pd = max(pd, d);
+    slots = max(slots, max(w.xts, w.yts));
+  }
+  if (s.xseq >= 0 && (s.xts > s.last || s.xts < slots)) return 0;
+  if (s.yseq >= 0 && (s.yts > s.last || s.yts < slots)) return 0;
+  return 1;
+}
+
 // KPB keys per 64-thread block: 64 (a lane per key), or 1 for few keys (a wave per key: the lanes
 // of a wave would otherwise run the three streams' branches one after another, and the SIMDs
 // beyond 1 / 64 of the keys sit idle)
-template <bool EMIT, bool HBMQ, int KPB>
+template <bool EMIT, int KPB>
 __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ perm,
                                              const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                              int* err) {
-  __shared__ LaWait W[HBMQ ? 1 : KPB][HBMQ ? 1 : LA_WCAP];
   __shared__ LaEv SB[KPB][LA_SB];
   if (threadIdx.x >= KPB) return;
   const int k = blockIdx.x * KPB + threadIdx.x;
   const uint32_t lane = threadIdx.x;
   const bool live = k < D.nk;
   const int rd = D.cur, wr = D.cur ^ 1;
-  const int cap = HBMQ ? D.wcap : LA_WCAP;
+  const int cap = D.wcap;
   const int msk = cap - 1;
-  LaWait* wq = HBMQ ? (EMIT ? D.wq[wr] : D.wtmp) + (int64_t)(live ? k : 0) * cap : W[lane];
+  LaWait* wq = (EMIT ? D.wq[wr] : D.wtmp) + (int64_t)(live ? k : 0) * cap;
+  LaEnt* fq = (EMIT ? D.fq[wr] : D.ftmp) + (int64_t)(live ? k : 0) * cap;
   LaPend s{};
   s.xseq = s.yseq = -1;
   s.last = INT64_MIN;
@@ -279,12 +354,17 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
       const int r = (s.wh + i) & msk;
       wq[r] = D.wq[rd][(int64_t)k * cap + r];
     }
+    for (int i = 0; i < s.ne; i++) {
+      const int r = (s.eh + i) & msk;
+      LaEnt x = D.fq[rd][(int64_t)k * cap + r];
+      x.i0 = 0;  // queued in an earlier push
+      fq[r] = x;
+    }
     beg = kbeg[k];
     cnt = kcnt[k];
   }
-  const bool useW = D.within >= 0;
+  const int64_t Wn = D.within, Tw = D.wait;
   int e = 0;
-  int64_t lo = 0;  // first batch index a timer of this key can fire at (after the key's previous event)
   uint32_t nm = 0;
   int64_t mi = 0;
   if (EMIT && live) {
@@ -294,151 +374,205 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
       O.count[1] = 2ull * (unsigned long long)(mi + D.cm[k]);
     }
   }
-  // one step per event of the key, plus a final step for the timers the batch's last clock reaches
-  auto step = [&](bool act, int64_t g, int64_t clk, int64_t ts, int stm, uint32_t ev0, uint32_t ev1, uint32_t ev2,
-                  bool en0, bool en1, bool en2) {
-    const int64_t hi = g;
-    // 1. timers the clock reached (FIFO: due times follow completion order)
-    int nf = 0, ne = 0;
-    while (nf < s.nw && wq[(s.wh + nf) & msk].due <= clk) {
-      const LaWait& w = wq[(s.wh + nf) & msk];
-      if (!useW || (llabs(w.xts - w.due) <= D.within && llabs(w.yts - w.due) <= D.within)) ne++;
-      nf++;
+  int64_t gfired = 0;  // batch index of this push's latest firing of the key's queue (a FIFO)
+  auto pair_at = [&](int i) -> LaWait& { return wq[(s.wh + i) & msk]; };
+  auto push_entry = [&](int64_t t, int64_t i0) {
+    if (s.ne >= cap) {
+      e |= E_LIST;
+      return;
     }
-    nm += (uint32_t)ne;
-    if (EMIT) {
-      for (int i = 0; i < nf; i++) {
-        const LaWait& w = wq[(s.wh + i) & msk];
-        if (useW && !(llabs(w.xts - w.due) <= D.within && llabs(w.yts - w.due) <= D.within)) continue;
-        if (mi >= O.cap || 2 * mi + 2 > O.refcap) {
-          e |= E_OUT;
-        } else {
-          O.key[mi] = B.partitioned ? k : 0;
-          O.ts[mi] = w.due;  // the timer's time (AbsentStreamPreStateProcessor: ev.ts = currentTime)
-          O.type[mi] = 0;
-          O.pos[mi] = lo;    // k_labs_pos: the event in [lo, aux] whose clock reached the due time
-          D.aux[mi] = hi;
-          O.ref_off[mi] = 2 * mi;
-          int64_t r = 2 * mi;
-          for (int q = 0; q < 3; q++) {
-            const bool isx = q == D.sid[0], isy = q == D.sid[1];
-            O.slot_len[mi * MAXS + q] = (int16_t)((isx || isy) ? 1 : 0);
-            if (isx) O.refs[r++] = w.xseq;
-            if (isy) O.refs[r++] = w.yseq;
-          }
-        }
-        mi++;
+    LaEnt x;
+    x.t = t;
+    x.i0 = (int32_t)i0;
+    x.pad = 0;
+    fq[(s.eh + s.ne) & msk] = x;
+    s.ne++;
+  };
+  // updateState: the new-and-every pairs, stably sorted by ts, join the pending list
+  auto move_nae = [&]() {
+    const int b0 = s.nw - s.nae;
+    for (int i = b0 + 1; i < s.nw; i++) {
+      const LaWait x = pair_at(i);
+      int j = i;
+      while (j > b0 && pair_at(j - 1).due > x.due) {
+        pair_at(j) = pair_at(j - 1);
+        j--;
+      }
+      pair_at(j) = x;
+    }
+    s.nae = 0;
+  };
+  auto emit = [&](const LaWait& w, int64_t et, int64_t g) {
+    nm++;
+    if (!EMIT) return;
+    if (mi >= O.cap || 2 * mi + 2 > O.refcap) {
+      e |= E_OUT;
+    } else {
+      O.key[mi] = B.partitioned ? k : 0;
+      O.ts[mi] = et;  // the timer's time (AbsentStreamPreStateProcessor: ev.ts = currentTime)
+      O.type[mi] = 0;
+      O.pos[mi] = bseq(B, g);
+      O.ref_off[mi] = 2 * mi;
+      int64_t r = 2 * mi;
+      for (int q = 0; q < 3; q++) {
+        const bool isx = q == D.sid[0], isy = q == D.sid[1];
+        O.slot_len[mi * MAXS + q] = (int16_t)((isx || isy) ? 1 : 0);
+        if (isx) O.refs[r++] = w.xseq;
+        if (isy) O.refs[r++] = w.yseq;
       }
     }
-    if (nf) {  // drop the fired waits
-      s.wh = (s.wh + nf) & msk;
-      s.nw -= nf;
+    mi++;
+  };
+  // the timer of entry et, fired at batch index g (AbsentStreamPreStateProcessor.process)
+  auto process = [&](int64_t et, int64_t g) {
+    move_nae();
+    int o = 0;
+    bool sent = false;
+    for (int i = 0; i < s.nw; i++) {
+      const LaWait w = pair_at(i);
+      if (la_expired(w.xts, w.yts, et, Wn)) continue;
+      if (et >= w.due) {
+        sent = true;
+        emit(w, et, g);
+        continue;
+      }
+      pair_at(o++) = w;
     }
-    if (!act) return;
-    // 2. the event
-    if (s.last != INT64_MIN && ts < s.last) e |= LA_UNORDERED;
-    s.last = ts;
-    lo = g + 1;
-    // expireEvents over every pre of the key: a half-filled logical partial older than W re-arms
-    if (useW && ((s.xseq >= 0 && llabs(s.xts - ts) > D.within) || (s.yseq >= 0 && llabs(s.yts - ts) > D.within))) {
-      s.xseq = s.yseq = -1;
+    s.nw = o;
+    const int64_t actual = B.rmax[g];
+    if (actual > Tw + et) s.lst = actual + Tw;
+    if (!sent && s.lst < et) {  // the re-arm
+      s.lst = et + Tw;
+      push_entry(et + Tw, g);
+    }
+  };
+  auto fire = [&](int64_t upto) {
+    while (s.ne > 0) {
+      const LaEnt x = fq[s.eh & msk];
+      const int64_t g = la_fire_at(B, x.t, max((int64_t)x.i0, gfired));
+      if (g > upto) break;
+      s.eh = (s.eh + 1) & msk;
+      s.ne--;
+      gfired = g;
+      process(x.t, g);
+    }
+  };
+  auto step = [&](const LaEv& x) {
+    fire((int64_t)x.g);
+    const int64_t t = x.ts;
+    s.last = t;
+    // expireEvents over every pre of the key (StreamPreStateProcessor.expireEvents :326-361)
+    if (Wn >= 0 && ((s.xseq >= 0 && llabs(s.xts - t) > Wn) || (s.yseq >= 0 && llabs(s.yts - t) > Wn))) {
+      s.xseq = s.yseq = -1;  // the logical partial expired: `every` re-arms a fresh one
       s.fl = 0;
     }
-    const int role = stm == D.st[0] ? 0 : (stm == D.st[1] ? 1 : (stm == D.st[2] ? 2 : -1));
-    if (role < 0) return;
-    LaVals V{s.xv, s.yv, 0u, (s.fl & 1u) != 0, (s.fl & 2u) != 0, true, D.tag[0], D.tag[1], D.tag[2]};
-    const uint32_t ev = role == 0 ? ev0 : (role == 1 ? ev1 : ev2);
-    const bool en = role == 0 ? en0 : (role == 1 ? en1 : en2);
-    if (role < 2) {
-      if (role == 0) {
-        V.v0 = ev;
-        V.n0 = en;
-        if (!la_pred(D.fx, V)) return;
-      } else {
-        V.v1 = ev;
-        V.n1 = en;
-        if (!la_pred(D.fy, V)) return;
+    if (Wn >= 0) {
+      while (s.nw - s.nae > 0 && la_expired(pair_at(0).xts, pair_at(0).yts, t, Wn)) {  // pending: from the head
+        s.wh = (s.wh + 1) & msk;
+        s.nw--;
       }
-      const int64_t seqg = bseq(B, g);
-      if (role == 0 && s.xseq < 0) {
-        s.xseq = seqg;
-        s.xts = ts;
-        s.xv = ev;
-        s.fl = (s.fl & ~1u) | (en ? 1u : 0u);
-      } else if (role == 1 && s.yseq < 0) {
-        s.yseq = seqg;
-        s.yts = ts;
-        s.yv = ev;
-        s.fl = (s.fl & ~2u) | (en ? 2u : 0u);
-      } else {
-        return;  // the slot is taken: the partial waits for its partner
-      }
-      if (s.xseq >= 0 && s.yseq >= 0) {  // the pair completes: it waits on the absent state
-        if (s.nw >= cap) {
-          e |= E_LIST;
-        } else {
-          LaWait& w = wq[(s.wh + s.nw++) & msk];
-          w.due = ts + D.wait;
-          w.xseq = s.xseq;
-          w.xts = s.xts;
-          w.yseq = s.yseq;
-          w.yts = s.yts;
-          w.xv = s.xv;
-          w.yv = s.yv;
-          w.fl = s.fl;
+      if (s.nae > 0) {  // new-and-every: every expired pair
+        const int b0 = s.nw - s.nae;
+        int o = b0;
+        for (int i = b0; i < s.nw; i++) {
+          const LaWait w = pair_at(i);
+          if (!la_expired(w.xts, w.yts, t, Wn)) pair_at(o++) = w;
         }
-        s.xseq = s.yseq = -1;  // every: a fresh partial
-        s.fl = 0;
+        s.nae = o - b0;
+        s.nw = o;
       }
-    } else {  // a Z event drops every waiting pair its filter matches
-      V.v2 = ev;
+    }
+    const int role = x.st == D.st[0] ? 0 : (x.st == D.st[1] ? 1 : (x.st == D.st[2] ? 2 : -1));
+    if (role < 0) return;
+    const bool en = x.n != 0;
+    LaVals V{s.xv, s.yv, 0u, (s.fl & 1u) != 0, (s.fl & 2u) != 0, true, D.tag[0], D.tag[1], D.tag[2]};
+    if (role == 2) {  // Z: new-and-every -> pending, then each pending pair fz matches is dropped
+      move_nae();
+      V.v2 = x.v;
       V.n2 = en;
       int o = 0;
       for (int i = 0; i < s.nw; i++) {
-        const LaWait w = wq[(s.wh + i) & msk];
+        const LaWait w = pair_at(i);
         V.v0 = w.xv;
         V.v1 = w.yv;
         V.n0 = (w.fl & 1u) != 0;
         V.n1 = (w.fl & 2u) != 0;
-        if (!la_pred(D.fz, V)) {
-          if (o != i) wq[(s.wh + o) & msk] = w;
-          o++;
+        if (la_pred(D.fz, V)) {
+          s.lst = t + Tw;
+          push_entry(t + Tw, (int64_t)x.g + 1);
+        } else {
+          pair_at(o++) = w;
         }
       }
       s.nw = o;
+      return;
+    }
+    if (role == 0) {
+      V.v0 = x.v;
+      V.n0 = en;
+      if (!la_pred(D.fx, V)) return;
+    } else {
+      V.v1 = x.v;
+      V.n1 = en;
+      if (!la_pred(D.fy, V)) return;
+    }
+    const int64_t seqg = bseq(B, (int64_t)x.g);
+    if (role == 0 && s.xseq < 0) {
+      s.xseq = seqg;
+      s.xts = t;
+      s.xv = x.v;
+      s.fl = (s.fl & ~1u) | (en ? 1u : 0u);
+    } else if (role == 1 && s.yseq < 0) {
+      s.yseq = seqg;
+      s.yts = t;
+      s.yv = x.v;
+      s.fl = (s.fl & ~2u) | (en ? 2u : 0u);
+    } else {
+      return;  // the slot is taken: the partial waits for its partner
+    }
+    if (s.xseq >= 0 && s.yseq >= 0) {  // the pair completes: new-and-every of the absent state
+      if (s.nw >= cap) {
+        e |= E_LIST;
+      } else {
+        LaWait& w = pair_at(s.nw++);
+        w.due = t + Tw;
+        w.xseq = s.xseq;
+        w.xts = s.xts;
+        w.yseq = s.yseq;
+        w.yts = s.yts;
+        w.xv = s.xv;
+        w.yv = s.yv;
+        w.fl = s.fl;
+        w.pad = 0;
+        s.nae++;
+      }
+      s.lst = t + Tw;
+      push_entry(t + Tw, (int64_t)x.g + 1);
+      s.xseq = s.yseq = -1;  // every: a fresh partial
+      s.fl = 0;
     }
   };
-  // the key's run (contiguous in the gathered columns) is staged in LDS LA_SB events at a time:
-  // the refill's loads are independent and in flight together (16 waves in all leave HBM latency
-  // exposed otherwise: ~4 us a step), and the step body is not unrolled (copies of it overflowed
-  // the instruction cache)
+  // the key's run (contiguous in key order) is staged in LDS LA_SB events at a time; the step body
+  // is not unrolled (copies of it overflowed the instruction cache)
   LaEv* sb = SB[lane];
   for (uint32_t j0 = 0; live && j0 < cnt; j0 += LA_SB) {
 #pragma unroll
     for (int q = 0; q < LA_SB; q++) {
-      if (j0 + q < cnt) {
-        sb[q] = la_ev_at(D, B, (int64_t)beg + j0 + q);
-      }
+      if (j0 + q < cnt) sb[q] = la_ev_at(D, B, (int64_t)beg + j0 + q);
     }
     const uint32_t nq = min((uint32_t)LA_SB, cnt - j0);
 #pragma unroll 1
-    for (uint32_t q = 0; q < nq; q++) {
-      const LaEv x = sb[q];
-      step(true, (int64_t)x.g, x.clk, x.ts, x.st, x.v, x.v, x.v, x.n != 0, x.n != 0, x.n != 0);
-    }
+    for (uint32_t q = 0; q < nq; q++) step(sb[q]);
   }
-  if (live) step(false, B.n - 1, B.n > 0 ? B.rmax[B.n - 1] : INT64_MIN, 0, -1, 0u, 0u, 0u, true, true, true);
+  if (live) fire(B.n - 1);  // the timers the push's last clock reaches
   if (!EMIT) {
     if (live) D.cm[k] = nm;
     return;
   }
   if (live) {
+    for (int i = 0; i < s.ne; i++) fq[(s.eh + i) & msk].i0 = 0;
+    s.reg = la_regular(s, wq, fq, msk, Wn, Tw);
     D.pend[wr][k] = s;
-    if (!HBMQ)
-      for (int i = 0; i < s.nw; i++) {
-        const int r = (s.wh + i) & msk;
-        D.wq[wr][(int64_t)k * cap + r] = wq[r];
-      }
   }
   if (e) atomicOr(err, e);
 }
@@ -504,12 +638,32 @@ __device__ __forceinline__ bool la_kill(const LaPredD& p, const LaKill& K, doubl
 }
 
 // one pass: records into the key's region of D.rec, the key's count into D.cm, the state into
-// copy wr; k_labs_out then writes the push's records contiguously
+// copy wr; k_labs_out then writes the push's records contiguously.
+// The state it leaves is the exact rule's (k_labs, tests/labs_exact.py FastC4 states the formulas):
+// when the key's events do not go back in time, no event lags the clock by T or more and the clock
+// never steps by more than T, the Scheduler queue stays sorted and every entry the clock reached has
+// fired, so per pair P (completed at c, slots' earliest ts m, due = c + T, D = m + W):
+//   E_D   = min(due, the first queued entry > max(D, clock(c)) at c): P leaves the pending list --
+//           emitted when due <= D, else expired -- at the first key event q > c with clock(q) >= E_D
+//           or ts(q) > D (or when the push's last clock reaches E_D);
+//   kill  = the first Z event in (c, that q) whose fz holds; it queues an entry ts + T;
+//   H     = the queue's head at c: P is still on new-and-every at the end iff no Z event of the key
+//           came after c and H > the last clock;
+// lastScheduledTime = ts + T of the key's last completion or kill; the queue keeps every entry past
+// the last clock.  A push or state outside that raises LA_SLOW (k_labs re-runs it exactly).
+constexpr int LA_WF = 64;  // queue entries k_labs_w holds (LDS)
+
 static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
                                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                                int* err) {
-  __shared__ LaWait A[64];  // waiting pairs, completion order
+  __shared__ LaWait A[64];   // the pairs on the absent state's lists, list (= completion) order
   __shared__ int32_t Ac[64];  // completing lane in the current block (-1: an earlier block)
+  __shared__ int64_t Aed[64];  // E_D of each pair
+  __shared__ int64_t Ah[64];   // H of each pair
+  __shared__ uint8_t Anae[64];  // on new-and-every (no Z event of the key since its completion)
+  __shared__ int64_t Ef[2 * LA_WF];  // the queue: entries queued before this block, sorted
+  __shared__ int64_t BE[64];  // entries queued in this block (completions, then kills) and their lanes
+  __shared__ int32_t BEl[64];
   const int k = blockIdx.x;
   if (k >= D.nk) return;
   const int lane = (int)threadIdx.x;
@@ -517,23 +671,44 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   const int rd = D.cur, wr = rd ^ 1;
   const int cap = D.wcap, msk = cap - 1;
   const LaPend s0 = D.pend[rd][k];
+  const bool useW = D.within >= 0;
+  const int64_t Wn = D.within, Tw = D.wait;
+  const int64_t Wb = useW ? Wn : (1ll << 60);  // D = min slot ts + Wb
   int nal = s0.nw;
-  if (nal > 64) {
-    if (lane == 0) {
-      D.cm[k] = 0;  // k_labs_out runs before the host sees LA_SLOW
-      atomicOr(err, LA_SLOW);
+  int nef = s0.ne;
+  {  // the ordered formulation must hold from this state and for this push (else k_labs)
+    bool slow = nal > 64 || nef > LA_WF || !s0.reg;
+    if (!slow && nef > 0 && B.n > 0 && B.rmax[0] - B.clock0 > Tw) slow = true;  // a step at the first send
+    if (!slow && *D.maxstep > (unsigned long long)Tw) slow = true;             // a step at a later send
+    if (slow) {
+      if (lane == 0) {
+        D.cm[k] = 0;  // k_labs_out runs before the host sees LA_SLOW
+        atomicOr(err, LA_SLOW);
+      }
+      return;
     }
-    return;
   }
+  if (lane < nef) Ef[lane] = D.fq[rd][(int64_t)k * cap + ((s0.eh + lane) & msk)].t;
+  __syncthreads();
   if (lane < nal) {
-    A[lane] = D.wq[rd][(int64_t)k * cap + ((s0.wh + lane) & msk)];
+    const LaWait w = D.wq[rd][(int64_t)k * cap + ((s0.wh + lane) & msk)];
+    A[lane] = w;
     Ac[lane] = -1;
+    Anae[lane] = lane >= nal - s0.nae ? 1 : 0;
+    // a carried pair: E_D from the queue as it stands (every entry > the clock; its own due among them)
+    const int64_t dd = min(w.xts, w.yts) + Wb;
+    int64_t ed = w.due, h = w.due;
+    for (int i = 0; i < nef; i++) {
+      const int64_t t = Ef[i];
+      h = min(h, t);
+      if (t > dd) ed = min(ed, t);
+    }
+    Aed[lane] = ed;
+    Ah[lane] = h;
   }
   const uint32_t beg = kbeg[k], cnt = kcnt[k];
   LaRec* rec = D.rec + la_region(beg, k);
   const uint32_t rcap = (cnt + 1u) / 2u + 64u;  // the region's records (la_region)
-  const bool useW = D.within >= 0;
-  const int64_t Wn = D.within, Tw = D.wait;
   const int8_t t0g = D.tag[0], t1g = D.tag[1], t2g = D.tag[2];
   int e = 0;
   uint32_t nm = 0;
@@ -542,11 +717,14 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   int64_t xseq = s0.xseq, xts = s0.xts, yseq = s0.yseq, yts = s0.yts;
   uint32_t xv = s0.xv, yv = s0.yv, fl = s0.fl;
   int64_t last = s0.last;
+  int64_t lsched = s0.lst;  // lastScheduledTime
   int64_t lo = 0;  // first batch index a timer can fire at (after the key's previous event)
-  // the waiting pairs (one per lane) fire (fired: in [flo, fhi]) unless killed; the survivors
-  // are compacted in order
-  auto settle = [&](bool fired, bool killed, int64_t flo, int64_t fhi, LaWait w) {
-    const bool ok = lane < nal && fired && !killed &&
+  int nbe = 0;     // entries queued in the current block
+  int lsl = -1;    // the block's last lane that queued an entry (a completion or a kill)
+  // the pairs (one per lane) leave (left: in [flo, fhi]) -- emitted when within W of their due
+  // time -- or are killed; the survivors are compacted in order
+  auto settle = [&](bool left, bool killed, bool tonae, int64_t flo, int64_t fhi, LaWait w, int64_t ed, int64_t h) {
+    const bool ok = lane < nal && left && !killed &&
                     (!useW || (llabs(w.xts - w.due) <= Wn && llabs(w.yts - w.due) <= Wn));
     const uint64_t em = __ballot(ok);
     if (nm + (uint32_t)__popcll(em) > rcap) e |= LA_BOUND;
@@ -560,13 +738,16 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       rec[nm + (uint32_t)__popcll(em & lt)] = r;
     }
     nm += (uint32_t)__popcll(em);
-    const bool surv = lane < nal && !fired && !killed;
+    const bool surv = lane < nal && !left && !killed;
     const uint64_t sm = __ballot(surv);
     __syncthreads();  // every lane holds its pair before the compaction writes
     if (surv) {
       const int d = __popcll(sm & lt);
       A[d] = w;
       Ac[d] = -1;
+      Aed[d] = ed;
+      Ah[d] = h;
+      Anae[d] = tonae ? 1 : 0;
     }
     nal = __popcll(sm);
     __syncthreads();
@@ -614,10 +795,17 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     const bool en = n_n != 0;
     if (j0 + 64 < cnt) fetch(j0 + 64);
     const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
-    {  // timestamps must not decrease within the key
+    {  // the ordered formulation: timestamps do not decrease within the key, and no event lags the
+       // clock by T or more (an entry queued then could fire at a send far past it)
       const int64_t tp = __shfl_up(ts, 1, 64);
       const int64_t prev = lane == 0 ? last : tp;
-      if (valid && prev != INT64_MIN && ts < prev) e |= LA_UNORDERED;
+      if (__ballot(valid && ((prev != INT64_MIN && ts < prev) || clk - ts >= Tw))) {
+        if (lane == 0) {
+          D.cm[k] = 0;
+          atomicOr(err, LA_SLOW);
+        }
+        return;
+      }
     }
     const int64_t seqg = bseq(B, g);
     const LaVals V0{v, v, 0u, en, en, true, t0g, t1g, t2g};
@@ -639,7 +827,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       const uint64_t Om = hx ? QY : QX;
       const int z = Em ? __builtin_ctzll(Em) : 64, b = Om ? __builtin_ctzll(Om) : 64;
       if (b < z) {  // the partner: the pair completes and waits on the absent state
-        if (nal >= 64) {
+        if (nal >= 64 || nbe >= 64) {
           if (lane == 0) {
             D.cm[k] = 0;
             atomicOr(err, LA_SLOW);
@@ -673,8 +861,13 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
           w.pad = 0;
           A[nal] = w;
           Ac[nal] = b;
+          Anae[nal] = 1;
+          BE[nbe] = w.due;
+          BEl[nbe] = b;
         }
         nal++;
+        nbe++;
+        lsl = max(lsl, b);
         hx = hy = false;
         xseq = yseq = -1;
         fl = 0;
@@ -747,9 +940,9 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
         break;
       }
     }
-    if (PM) {  // the completed pairs, in completion order, join the waits
+    if (PM) {  // the completed pairs, in completion order, join the absent state's new-and-every list
       const int npm = __popcll(PM);
-      if (nal + npm > 64) {
+      if (nal + npm > 64 || nbe + npm > 64) {
         if (lane == 0) {
           D.cm[k] = 0;
           atomicOr(err, LA_SLOW);
@@ -775,8 +968,13 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
         w.pad = 0;
         A[d] = w;
         Ac[d] = b;
+        Anae[d] = 1;
+        BE[nbe + __popcll(PM & lt)] = w.due;
+        BEl[nbe + __popcll(PM & lt)] = b;
       }
       nal += npm;
+      nbe += npm;
+      lsl = max(lsl, __builtin_amdgcn_readlane(b, 63 - __builtin_clzll(PM)));
     }
     if (hk >= 0) {  // the slot event a of the chain's last step
       const int ha = __builtin_amdgcn_readlane(a, hk);
@@ -799,72 +997,213 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     __syncthreads();
     LA_STAMP(1);
     LA_COUNT(6, nal);
-    // 2. the waiting pairs against this block's events
+    const uint64_t zm = __ballot(valid && role == 2);
+    const int lastz = zm ? 63 - __builtin_clzll(zm) : -1;  // the block's last Z event (new-and-every -> pending)
+    const int64_t clkl = la_rl64(clk, nv - 1);            // the clock at the block's last event
+    // 2. the pairs against this block's events
     if (nal > 0) {
       LaWait w{};
       int c = 64;
+      int64_t ed = 0, h = 0;
       if (lane < nal) {
         w = A[lane];
         c = Ac[lane];
+        ed = Aed[lane];
+        h = Ah[lane];
       }
-      // fire event: the first event after c whose clock reaches the due time.  Due times and
-      // completions follow the pair order, so the fire events do too: the first pair that does
-      // not fire in this block ends the search.
-      int f = 64;
-      {  // per pair, a search over the block's clocks (ascending) after c
+      const int64_t dd = min(w.xts, w.yts) + Wb;
+      const int64_t cc = __shfl(clk, c >= 0 && c < 64 ? c : 0, 64);  // (lanes with c < 0 ignore it)
+      const int ncb = nbe;  // the block's completion entries (BE[0, ncb))
+      // E_D and H of a pair completed in this block: the entries queued before c and not fired at c
+      auto at_c = [&](int nk) {
+        if (lane < nal && c >= 0) {
+          int64_t e2 = w.due, h2 = w.due;
+          for (int i = 0; i < nef; i++) {
+            const int64_t t = Ef[i];
+            if (t > cc) {
+              h2 = min(h2, t);
+              if (t > dd) e2 = min(e2, t);
+            }
+          }
+          for (int i = 0; i < nk; i++) {
+            const int64_t t = BE[i];
+            if (BEl[i] < c && t > cc) {
+              h2 = min(h2, t);
+              if (t > dd) e2 = min(e2, t);
+            }
+          }
+          ed = e2;
+          h = h2;
+        }
+      };
+      at_c(ncb);
+      int f = 64, kq = 64;
+      bool killed = false;
+      // the leave event: the first event after c whose clock reaches E_D or whose ts passes D (both
+      // ascend in the block); the kill: the first Z event before it whose filter holds.  A kill queues
+      // an entry that may lower a later pair's E_D: repeat until no E_D changes
+      for (int it = 0; it < 65; it++) {
         int l2 = c + 1, h2 = nv;  // the answer lies in [l2, h2]; h2 = nv: not in this block
 #pragma unroll
-        for (int it = 0; it < 7; it++) {
+        for (int st7 = 0; st7 < 7; st7++) {
           const int mid = (l2 + h2) >> 1;
-          const int64_t cm = __shfl(clk, mid < 64 ? mid : 0, 64);
+          const int64_t cm = __shfl(clk, mid < 64 ? mid : 0, 64), tm = __shfl(ts, mid < 64 ? mid : 0, 64);
           if (l2 < h2) {
-            if (mid < nv && cm >= w.due) h2 = mid;
+            if (mid < nv && (cm >= ed || tm > dd)) h2 = mid;
             else l2 = mid + 1;
           }
         }
-        if (lane < nal && l2 < nv) f = l2;
-      }
-      LA_STAMP(2);
-      // killed: a Z event between completion and firing whose filter holds.  Each pair walks the
-      // Z events of its window (c, f) with first-set-bit jumps; the walk ends at the first kill.
-      bool killed = false;
-      const uint64_t zm = __ballot(valid && role == 2);
-      if (zm) {
-        const LaKill K = la_kill_pre(D.fz, w, t0g, t1g, t2g);
-        auto nextz = [&](int x) -> int {
-          if (x >= 64) return 64;
-          const uint64_t r = zm >> x;
-          return r ? x + __builtin_ctzll(r) : 64;
-        };
-        int q = nextz(c + 1);
-        bool act = lane < nal && q < f;
-        while (__ballot(act)) {
-          const int qs = q < 64 ? q : 0;
-          const uint32_t zv = (uint32_t)__shfl((int)v, qs, 64);
-          const bool zn = __shfl((int)en, qs, 64) != 0;
-          if (act) {
-            killed = la_kill(D.fz, K, la_val(zv, t2g, false), la_val(zv, t2g, true), zn);
-            q = nextz(q + 1);
-            act = !killed && q < f;
+        f = lane < nal && l2 < nv ? l2 : 64;
+        LA_STAMP(2);
+        killed = false;
+        kq = 64;
+        if (zm) {
+          const LaKill K = la_kill_pre(D.fz, w, t0g, t1g, t2g);
+          auto nextz = [&](int x) -> int {
+            if (x >= 64) return 64;
+            const uint64_t r = zm >> x;
+            return r ? x + __builtin_ctzll(r) : 64;
+          };
+          int q = nextz(c + 1);
+          bool act = lane < nal && q < f;
+          while (__ballot(act)) {
+            const int qs = q < 64 ? q : 0;
+            const uint32_t zv = (uint32_t)__shfl((int)v, qs, 64);
+            const bool zn = __shfl((int)en, qs, 64) != 0;
+            if (act) {
+              killed = la_kill(D.fz, K, la_val(zv, t2g, false), la_val(zv, t2g, true), zn);
+              if (killed) kq = q;
+              q = nextz(q + 1);
+              act = !killed && q < f;
+            }
           }
         }
+        // the kills' entries, in pair order after the completions'
+        const uint64_t km = __ballot(killed);
+        const int64_t tkq = __shfl(ts, kq < 64 ? kq : 0, 64);
+        if (ncb + __popcll(km) > 64) {
+          if (lane == 0) {
+            D.cm[k] = 0;
+            atomicOr(err, LA_SLOW);
+          }
+          return;
+        }
+        __syncthreads();
+        if (killed) {
+          const int d = ncb + __popcll(km & lt);
+          BE[d] = tkq + Tw;
+          BEl[d] = kq;
+        }
+        nbe = ncb + __popcll(km);
+        __syncthreads();
+        const int64_t ed0 = ed;
+        at_c(nbe);
+        if (!__ballot(lane < nal && c >= 0 && ed != ed0)) break;
       }
       LA_STAMP(3);
-      const bool fired = f < 64;
+      {  // the last completion or kill sets lastScheduledTime
+        const uint64_t km = __ballot(killed);
+        int kl = -1;
+        if (km) {
+          int kmax = killed ? kq : -1;
+          for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
+          kl = kmax;
+        }
+        lsl = max(lsl, kl);
+      }
+      const bool left = f < 64;
       const int64_t gp = (int64_t)(uint32_t)__shfl(g, f > 0 ? f - 1 : 0, 64);
       const int64_t gf = (int64_t)(uint32_t)__shfl(g, f < 64 ? f : 0, 64);
-      settle(fired, killed, f == 0 ? lo : gp + 1, gf, w);
+      const bool tonae = lane < nal && Anae[lane] && c >= lastz;  // no Z event after its completion
+      settle(left, killed, tonae, f == 0 ? lo : gp + 1, gf, w, ed, h);
       LA_STAMP(4);
     }
+    // the queue: this block's entries join in lane order (= time order); the entries its clock
+    // reached have fired
+    if (nbe > 0) {
+      __syncthreads();
+      int64_t t = 0;
+      int l = 0;
+      if (lane < nbe) {
+        t = BE[lane];
+        l = BEl[lane];
+      }
+      // rank by (lane, index): completions before kills at one lane cannot happen (different events)
+      int r = 0;
+      for (int i = 0; i < nbe; i++) {
+        const int li = BEl[i];
+        r += (li < l || (li == l && i < lane)) ? 1 : 0;
+      }
+      __syncthreads();
+      if (lane < nbe) BE[r] = t;
+      __syncthreads();
+    }
+    {
+      // drop the fired (t <= clkl), append the block's entries
+      int keep0 = 0;
+      for (int i = 0; i < nef; i++) keep0 += Ef[i] <= clkl ? 1 : 0;  // a sorted prefix
+      int keep1 = 0;
+      for (int i = 0; i < nbe; i++) keep1 += BE[i] <= clkl ? 1 : 0;
+      const int n0 = nef - keep0, n1 = nbe - keep1;
+      if (n0 + n1 > LA_WF) {
+        if (lane == 0) {
+          D.cm[k] = 0;
+          atomicOr(err, LA_SLOW);
+        }
+        return;
+      }
+      int64_t a0 = 0, a1 = 0;
+      if (lane < n0) a0 = Ef[keep0 + lane];
+      if (lane < n1) a1 = BE[keep1 + lane];
+      __syncthreads();
+      if (lane < n0) Ef[lane] = a0;
+      if (lane < n1) Ef[n0 + lane] = a1;
+      nef = n0 + n1;
+      __syncthreads();
+    }
+    if (lsl >= 0) lsched = la_rl64(ts, lsl) + Tw;
+    lsl = -1;
+    nbe = 0;
     lo = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)g, nv - 1) + 1;
     last = la_rl64(ts, nv - 1);
   }
   // the timers the push's last clock reaches
+  const int64_t lastclk = B.n > 0 ? B.rmax[B.n - 1] : B.clock0;
   if (nal > 0) {
     LaWait w{};
-    if (lane < nal) w = A[lane];
-    const int64_t lastclk = B.n > 0 ? B.rmax[B.n - 1] : INT64_MIN;
-    settle(lane < nal && w.due <= lastclk, false, lo, B.n - 1, w);
+    int64_t ed = 0, h = 0;
+    bool nae = false;
+    if (lane < nal) {
+      w = A[lane];
+      ed = Aed[lane];
+      h = Ah[lane];
+      nae = Anae[lane] != 0;
+    }
+    settle(lane < nal && ed <= lastclk, false, nae, lo, B.n - 1, w, ed, h);
+  }
+  {  // the queue keeps the entries past the last clock
+    int drop = 0;
+    for (int i = 0; i < nef; i++) drop += Ef[i] <= lastclk ? 1 : 0;
+    int64_t a0 = 0;
+    if (lane < nef - drop) a0 = Ef[drop + lane];
+    __syncthreads();
+    nef -= drop;
+    if (nef <= cap && lane < nef) {
+      LaEnt x;
+      x.t = a0;
+      x.i0 = 0;
+      x.pad = 0;
+      D.fq[wr][(int64_t)k * cap + lane] = x;
+    }
+  }
+  // new-and-every: the trailing pairs with no Z event since their completion and no timer since
+  int nae = 0;
+  {
+    const bool q = lane < nal && Anae[lane] && Ah[lane] > lastclk;
+    const uint64_t m = __ballot(q);
+    const uint64_t all = nal >= 64 ? ~0ull : ((1ull << nal) - 1ull);
+    const uint64_t notq = all & ~m;
+    nae = notq ? nal - 1 - (63 - __builtin_clzll(notq)) : nal;
   }
 #ifdef SHP_SW_STAMPS
   LA_COUNT(7, cnt);
@@ -873,7 +1212,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
 #endif
 #undef LA_STAMP
 #undef LA_COUNT
-  if (nal > cap) e |= E_LIST;
+  if (nal > cap || nef > cap) e |= E_LIST;
   else if (lane < nal) D.wq[wr][(int64_t)k * cap + lane] = A[lane];
   if (lane == 0) {
     D.cm[k] = min(nm, rcap);
@@ -887,7 +1226,12 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     s.fl = fl;
     s.nw = nal;
     s.wh = 0;
+    s.nae = nae;
     s.last = last;
+    s.lst = lsched;
+    s.ne = nef;
+    s.eh = 0;
+    s.reg = 1;
     D.pend[wr][k] = s;
   }
   if (e) atomicOr(err, e);
@@ -938,23 +1282,7 @@ static __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B,
   if (e) atomicOr(err, e);
 }
 
-// the event that fired each timer record of the push: the first batch index in [pos, aux] whose
-// running clock reaches the record's due time (the playback clock is non-decreasing)
-static __global__ void k_labs_pos(LabsDev D, BatchView B, MatchOut O) {
-  const int64_t m = min((int64_t)O.count[0], O.cap);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t a = O.pos[i], b = D.aux[i];
-    const int64_t due = O.ts[i];
-    while (a < b) {
-      const int64_t mid = a + ((b - a) >> 1);
-      if (B.rmax[mid] >= due) b = mid;
-      else a = mid + 1;
-    }
-    O.pos[i] = bseq(B, a);
-  }
-}
-
-// a key's waiting pairs into a ring of another capacity (tier change), head reset to 0
+// a key's pairs and queue entries into rings of another capacity (tier change), heads reset to 0
 static __global__ void k_labs_migrate(LabsDev Dn, LabsDev Do) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= Do.nk) return;
@@ -962,7 +1290,10 @@ static __global__ void k_labs_migrate(LabsDev Dn, LabsDev Do) {
   LaPend s = Do.pend[c][k];
   for (int i = 0; i < s.nw && i < Dn.wcap; i++)
     Dn.wq[c][k * Dn.wcap + i] = Do.wq[c][k * Do.wcap + ((s.wh + i) & (Do.wcap - 1))];
+  for (int i = 0; i < s.ne && i < Dn.wcap; i++)
+    Dn.fq[c][k * Dn.wcap + i] = Do.fq[c][k * Do.wcap + ((s.eh + i) & (Do.wcap - 1))];
   s.wh = 0;
+  s.eh = 0;
   Dn.pend[c][k] = s;
 }
 
@@ -972,9 +1303,21 @@ static __global__ void k_labs_init(LabsDev D) {
     LaPend s{};
     s.xseq = s.yseq = -1;
     s.last = INT64_MIN;
+    s.reg = 1;
     D.pend[0][i] = s;
     D.pend[1][i] = s;
   }
+}
+
+// the push's largest step of the playback clock after its first send (k_labs_w's formulation needs
+// every step <= T: then an entry fires at most T past its time, and lastScheduledTime never moves
+// to the clock); the first send's step is checked per key (it matters only where entries are queued)
+static __global__ void k_labs_steps(const int64_t* __restrict__ rmax, int64_t n, unsigned long long* out) {
+  unsigned long long m = 0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; g < n; g += (int64_t)gridDim.x * blockDim.x)
+    m = max(m, (unsigned long long)(rmax[g] - rmax[g - 1]));
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor((long long)m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
 }
 
 struct LabsState {
@@ -1043,8 +1386,11 @@ struct LabsState {
     for (int c = 0; c < 2; c++) {
       al(D.pend[c], max_keys);
       al(D.wq[c], (int64_t)max_keys * LA_WCAP);
+      al(D.fq[c], (int64_t)max_keys * LA_WCAP);
     }
-    al(D.aux, mcap);
+    al(D.wtmp, (int64_t)max_keys * LA_WCAP);
+    al(D.ftmp, (int64_t)max_keys * LA_WCAP);
+    al(D.maxstep, 1);
     al(D.cm, max_keys);
     al(D.om, max_keys);
     al(D.p_ev, cap);
@@ -1068,13 +1414,8 @@ struct LabsState {
   template <bool EMIT>
   void launch(unsigned gk, bool few, const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg,
               const uint32_t* kcnt, int* err, hipStream_t s) {
-    if (few) {
-      if (tier == 0) k_labs<EMIT, false, 1><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
-      else k_labs<EMIT, true, 1><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
-    } else {
-      if (tier == 0) k_labs<EMIT, false, 64><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
-      else k_labs<EMIT, true, 64><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
-    }
+    if (few) k_labs<EMIT, 1><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
+    else k_labs<EMIT, 64><<<gk, 64, 0, s>>>(D, B, O, perm, kbeg, kcnt, err);
   }
 
   void run(const BatchView& B, const MatchOut& O, const uint32_t* perm, const uint32_t* kbeg, const uint32_t* kcnt,
@@ -1088,6 +1429,9 @@ struct LabsState {
       k_labs_gather<<<4096, 256, 0, s>>>(D, perm, B.n);
     }
     if (wave_ok && !slow) {  // one pass, then the records to their offsets
+      kt.mark("labs_steps", s);
+      (void)hipMemsetAsync(D.maxstep, 0, sizeof(unsigned long long), s);
+      if (B.n > 1) k_labs_steps<<<1024, 256, 0, s>>>(B.rmax, B.n, D.maxstep);
       kt.mark("labs", s);
       k_labs_w<<<(unsigned)D.nk, 64, 0, s>>>(D, B, perm, kbeg, kcnt, err);
       kt.mark("labs_scan", s);
@@ -1104,9 +1448,7 @@ struct LabsState {
     size_t tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
     kt.mark("labs", s);
-    launch<true>(gk, few, B, O, perm, kbeg, kcnt, err, s);
-    kt.mark("labs_pos", s);
-    k_labs_pos<<<1024, 256, 0, s>>>(D, B, O);
+    launch<true>(gk, few, B, O, perm, kbeg, kcnt, err, s);  // (k_labs writes each record's fire event)
     kt.mark(nullptr, s);
   }
 
@@ -1143,18 +1485,27 @@ struct LabsState {
     Dn.wcap = LA_CAPS[t];
     const int64_t n = (int64_t)D.nk * Dn.wcap;
     LaWait* q[3] = {nullptr, nullptr, nullptr};
-    for (int i = 0; i < 3; i++)
-      if (hipMalloc((void**)&q[i], (size_t)n * sizeof(LaWait)) != hipSuccess) {
-        for (LaWait* p : q)
-          if (p) (void)hipFree(p);
-        return false;
+    LaEnt* f[3] = {nullptr, nullptr, nullptr};
+    bool ok = true;
+    for (int i = 0; i < 3 && ok; i++)
+      ok = hipMalloc((void**)&q[i], (size_t)n * sizeof(LaWait)) == hipSuccess &&
+           hipMalloc((void**)&f[i], (size_t)n * sizeof(LaEnt)) == hipSuccess;
+    if (!ok) {
+      for (int i = 0; i < 3; i++) {
+        if (q[i]) (void)hipFree(q[i]);
+        if (f[i]) (void)hipFree(f[i]);
       }
+      return false;
+    }
     Dn.wq[0] = q[0];
     Dn.wq[1] = q[1];
     Dn.wtmp = q[2];
+    Dn.fq[0] = f[0];
+    Dn.fq[1] = f[1];
+    Dn.ftmp = f[2];
     if (migrate) k_labs_migrate<<<(unsigned)((D.nk + 255) / 256), 256, 0, s>>>(Dn, D);
     if (hipStreamSynchronize(s) != hipSuccess) return false;
-    for (LaWait* p : {D.wq[0], D.wq[1], D.wtmp})
+    for (void* p : {(void*)D.wq[0], (void*)D.wq[1], (void*)D.wtmp, (void*)D.fq[0], (void*)D.fq[1], (void*)D.ftmp})
       if (p) (void)hipFree(p);
     D = Dn;
     tier = t;
@@ -1165,9 +1516,11 @@ struct LabsState {
     for (int c = 0; c < 2; c++) {
       if (D.pend[c]) (void)hipFree(D.pend[c]);
       if (D.wq[c]) (void)hipFree(D.wq[c]);
+      if (D.fq[c]) (void)hipFree(D.fq[c]);
     }
     if (D.wtmp) (void)hipFree(D.wtmp);
-    void* qs[] = {D.aux, D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp};
+    if (D.ftmp) (void)hipFree(D.ftmp);
+    void* qs[] = {D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp, D.maxstep};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = LabsDev{};

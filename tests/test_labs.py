@@ -1,15 +1,17 @@
-"""The logical-absent path (siddhi_amd/csrc/labs.h, opt-in force_general = 4), C4's shape:
+"""The logical-absent path (siddhi_amd/csrc/labs.h, the default for its shape), C4's shape:
 `every (e1=S1[f] and e2=S2[f]) -> not S3[price > e1.price] for T within W` in playback.
 
-CPU: the per-key rule labs.h implements, restated in Python (pend = the logical partial, waits =
-completed pairs in completion order, each firing at the first event whose playback clock reaches
-completion ts + T), against the oracle's object-level restatement of the Logical / AbsentStream
-processors and the playback Scheduler (oracle/oracle.cpp) -- the C4 stream at several key counts,
-and dense random streams with ties in no due time (cross-key scheduler ties are parity-unpinned,
-SURVEY.md §8c), and k_labs_w's block-at-a-time formulation against that rule.  GPU (`-m gpu`):
-k_labs_w / k_labs + k_labs_pos against the oracle, split pushes, a clock advanced with no event,
-snapshot/restore, the hand-back of keys with more than 64 waiting pairs, and the refusal of
-out-of-order timestamps.
+CPU: the exact per-key rule for ANY timestamp order (tests/labs_exact.py ExactC4: the logical
+partial, the absent state's pending / new-and-every lists, the key's Scheduler FIFO and
+lastScheduledTime) against the oracle's object-level restatement of the Logical / AbsentStream
+processors and the playback Scheduler (oracle/oracle.cpp) -- ordered C4 streams and streams whose
+timestamps go back within keys and globally, keys lagging the clock, clock jumps -- on streams
+with no cross-key scheduler tie (those are parity-unpinned); k_labs_w's ordered
+formulation as formulas per pair (FastC4) against ExactC4, outputs AND state after every push; the
+older ordered rule (`model`) and its block-at-a-time form (`wave_model`).  GPU (`-m gpu`): k_labs_w /
+k_labs against the oracle, unordered streams through the default path (k_labs_w hands them to
+k_labs), the two kernels' states equal after every push, split pushes, a clock advanced with no
+event, snapshot/restore, the hand-back of keys with more than 64 waiting pairs.
 """
 from collections import deque
 
@@ -17,6 +19,7 @@ import numpy as np
 import pytest
 
 from diff_util import compare, per_key, program_for, run, small_stream
+from labs_exact import ExactC4, FastC4
 from oracle.oracle import OracleEngine
 
 W, WAIT = 10_000, 5_000
@@ -307,22 +310,20 @@ def test_labs_snapshot_restore_continues():
 
 
 @pytest.mark.gpu
-def test_labs_refuses_unordered_timestamps_and_keeps_state():
-    from siddhi_amd.native import ShpError
-    cq = program_for(4)
-    g = small_stream(4, 20_000, 50)
+def test_labs_unordered_push_runs_exact_and_keeps_going():
+    """A push with a key going back in time: k_labs_w hands it to k_labs (exact), and the ordered
+    pushes after it run on k_labs_w again from the state k_labs left; all against the oracle."""
     from siddhi_amd.native import _concat
+    cq = program_for(4)
+    g = small_stream(4, 30_000, 50)
+    g["ts"] = g["ts"].copy()
+    g["ts"][10_100] -= 5_000
     want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
     eng = _hip(cq, 50, 1 << 15)
-    first = run(eng, cq, {k: v[:10_000] for k, v in g.items()})
-    bad = {k: v[10_000:].copy() for k, v in g.items()}
-    bad["ts"][100] -= 5_000
-    with pytest.raises(ShpError):
-        run(eng, cq, bad)
-    # the refused push left the engine as it was: the ordered remainder continues exactly
-    second = run(eng, cq, {k: v[10_000:] for k, v in g.items()})
-    got = per_key(_concat([first, second], None, eng.S))
+    outs = [run(eng, cq, {k: v[lo:lo + 10_000] for k, v in g.items()}) for lo in (0, 10_000, 20_000)]
+    got = per_key(_concat(outs, None, eng.S))
     assert compare(want, got) is None, compare(want, got)
+    assert eng.stat("labs_fallbacks") == 1
 
 
 @pytest.mark.gpu
@@ -383,3 +384,145 @@ def test_labs_more_than_4096_waiting_pairs():
     assert compare(want, got) is None, compare(want, got)
     assert sum(len(x) for x in want.values()) > 10_000
     assert eng.describe(eng.snapshot())["engine"]["tier"] >= 3
+
+
+# ------------------------------------------------------------------ the exact rule (any order)
+
+def unordered_c4(seed, n=30_000):
+    """A C4-shaped playback stream whose timestamps misbehave in one of five ways."""
+    rng = np.random.default_rng(seed)
+    keys = [3, 10, 40, 5, 20, 8, 2, 60, 30, 12][seed % 10]
+    ts = (np.arange(n) * int(rng.integers(1, 40))).astype(np.int64) + 100_000
+    mode = seed % 5
+    if mode == 0:
+        ts = ts + rng.integers(-8000, 8000, n)                                 # local disorder
+    elif mode == 1:
+        ts = ts - (rng.random(n) < 0.05) * rng.integers(0, 30_000, n)          # occasional big decreases
+    elif mode == 2:
+        ts = ts + np.cumsum(rng.random(n) < 0.001) * 20_000                    # clock jumps beyond T
+    elif mode == 3:
+        ts = ts + (rng.integers(0, keys, n) % 3) * 7_000                       # keys lagging the clock
+    else:
+        ts = np.sort(ts - rng.integers(0, 3, n))                               # ordered, with ties
+    key = rng.integers(0, keys, n).astype(np.int32)
+    st = rng.integers(0, 3, n).astype(np.int32)
+    pr = (rng.integers(0, 10000, n) / 100.0).astype(np.float32)
+    return ts.astype(np.int64), key, st, pr
+
+
+def _exact(ts, key, st, pr, batch):
+    m = ExactC4()
+    for lo in range(0, len(ts), batch):
+        hi = min(len(ts), lo + batch)
+        m.push(ts[lo:hi], key[lo:hi], st[lo:hi], pr[lo:hi])
+    return m.fetch(), m
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_exact_rule_matches_oracle_any_order(seed):
+    ts, key, st, pr = unordered_c4(seed)
+    o = OracleEngine(program_for(4).program_json(), 0)
+    for lo in range(0, len(ts), 7919):
+        hi = min(len(ts), lo + 7919)
+        o.push(ts[lo:hi], key[lo:hi], st[lo:hi], [pr[lo:hi]] * 3, [None] * 3)
+    if o.timer_ties():
+        pytest.skip("cross-key scheduler ties (TreeMultimap): parity-unpinned")
+    want = per_key(o.fetch())
+    got, m = _exact(ts, key, st, pr, 7919)
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 10
+
+
+def test_exact_rule_re_arms_and_jumps_occur():
+    """The unordered streams exercise the re-arm entries and lastScheduledTime jumps that the
+    ordered fast path never sees (the reason the state carries them)."""
+    rearms = jumps = 0
+    for seed in (0, 3, 5, 8):
+        _, m = _exact(*unordered_c4(seed, 12_000), 4001)
+        rearms += m.rearms
+        jumps += m.jumps
+    assert rearms > 0 and jumps > 0
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fast_formulas_equal_exact_rule_state_and_output(seed):
+    """FastC4 (k_labs_w's per-pair formulas) against ExactC4 on ordered streams: every key's state
+    (partial, pending and new-and-every pairs, queue, lastScheduledTime) after every push, and the
+    records; W / T / key counts / event spacing varied (T >= W included)."""
+    rng = np.random.default_rng(100 + seed)
+    n = 6000
+    keys = int(rng.integers(1, 30))
+    step = int(rng.integers(1, 600))
+    Wv = int(rng.choice([3000, 6000, 10000, 20000]))
+    Tv = int(rng.choice([2000, 5000, 8000]))
+    ts = np.sort((np.arange(n) * step).astype(np.int64) + 10_000 - rng.integers(0, 3, n))
+    key = rng.integers(0, keys, n).astype(np.int32)
+    st = rng.integers(0, 3, n).astype(np.int32)
+    pr = (rng.integers(0, 10000, n) / 100.0).astype(np.float32)
+    a, b = ExactC4(W=Wv, T=Tv), FastC4(W=Wv, T=Tv)
+    batch = int(rng.integers(100, 3000))
+    for lo in range(0, n, batch):
+        hi = min(n, lo + batch)
+        a.push(ts[lo:hi], key[lo:hi], st[lo:hi], pr[lo:hi])
+        b.push(ts[lo:hi], key[lo:hi], st[lo:hi], pr[lo:hi])
+        for k in a.keys:
+            assert a.keys[k].snapshot() == b.state(k), (lo, k)
+    oa, ob = a.fetch(), b.fetch()
+    assert compare(oa, ob) is None, compare(oa, ob)
+    assert a.rearms == 0 and a.jumps == 0
+
+
+# ---------------------------------------------------------------- GPU: any order, both kernels
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(10))
+def test_labs_default_path_any_order_vs_oracle(seed):
+    """The default path of C4's shape (force_general = 0) is the logical-absent automaton; on the
+    misbehaving streams k_labs_w hands the pushes to k_labs, and the records equal the oracle's."""
+    from siddhi_amd.native import HipEngine
+    ts, key, st, pr = unordered_c4(seed)
+    cq = program_for(4)
+    o = OracleEngine(cq.program_json(), 0)
+    e = HipEngine(cq.program_json(), 0, max_keys=64, max_batch=1 << 13)
+    assert e.path == 4
+    for lo in range(0, len(ts), 7919):
+        hi = min(len(ts), lo + 7919)
+        args = (ts[lo:hi], key[lo:hi], st[lo:hi], [pr[lo:hi]] * 3, [None] * 3)
+        o.push(*args)
+        e.push(*args)
+    if o.timer_ties():
+        pytest.skip("cross-key scheduler ties (TreeMultimap): parity-unpinned")
+    want, got = per_key(o.fetch()), per_key(e.fetch())
+    assert compare(want, got) is None, compare(want, got)
+    if seed % 5 != 4:
+        assert e.stat("labs_fallbacks") > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("keys,step", [(50, 1), (7, 300), (1, 900)])
+def test_labs_wave_and_thread_kernels_leave_the_same_state(monkeypatch, keys, step):
+    """k_labs_w's state (pairs and their list, the Scheduler queue, lastScheduledTime) equals
+    k_labs's after every push of an ordered stream (SHP_NO_LABS_W: k_labs only)."""
+    from siddhi_amd.native import HipEngine
+    cq = program_for(4)
+    g = small_stream(4, 60_000, keys)
+    g["ts"] = (synth_t0() + np.arange(len(g["ts"])) * step).astype(np.int64)
+    a = HipEngine(cq.program_json(), 0, max_keys=keys, max_batch=1 << 14)
+    monkeypatch.setenv("SHP_NO_LABS_W", "1")
+    b = HipEngine(cq.program_json(), 0, max_keys=keys, max_batch=1 << 14)
+    cols = [g["price"].astype(np.float32)] * 3
+    n = len(g["ts"])
+    for lo in range(0, n, 9_001):
+        hi = min(n, lo + 9_001)
+        args = (g["ts"][lo:hi], g["key"][lo:hi], g["stream"][lo:hi], [c[lo:hi] for c in cols], [None] * 3)
+        a.push(*args)
+        b.push(*args)
+        da, db = a.describe(a.snapshot()), b.describe(b.snapshot())
+        assert da["keys"] == db["keys"], lo
+    assert compare(per_key(a.fetch()), per_key(b.fetch())) is None
+    assert a.stat("labs_fallbacks") == 0
+
+
+def synth_t0():
+    from siddhi_amd import synth
+    return synth.T0
