@@ -308,7 +308,7 @@ class FastC4:
             K["pairs"] = [{k2: p[k2] for k2 in ("x", "y", "ts", "H", "ED")} for p in alive]
             nae = 0
             for p in reversed(alive):
-                if (p["was_nae"] and p["c"] > lastZ) and p["H"] > clk_end:
+                if (p["was_nae"] and p["c"] >= lastZ) and p["H"] > clk_end:
                     nae += 1
                 else:
                     break
