@@ -140,7 +140,8 @@ def test_sync_pushes_compact_with_engine_retention(cfg, n, keys, ms, layout):
     assert q.layout == layout
     assert _rows(rt) == want
     assert len(want) > 100 or cfg == 3
-    assert q.history.trims > 0 and q.history.dropped > n // 3, (q.history.trims, q.history.dropped)
+    # kept <= 2x the live span (trims when the rows double): at 10k keys C2's live span is ~8*10^4 events
+    assert q.history.trims > 0 and q.history.dropped > n // 6, (q.history.trims, q.history.dropped)
 
 
 @pytest.mark.gpu
