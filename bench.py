@@ -53,7 +53,7 @@ WORKLOADS = {
 }
 PATHS = {2: "sweep (owner partition + LDS sweep)", 1: "scan kernels over a key-sorted batch", 0: "general NFA lanes",
          3: "count-sequence automaton over a key-sorted batch (cseq)",
-         4: "logical-absent automaton over a key-sorted batch (labs, opt-in --path labs)"}
+         4: "logical-absent automaton over a key-sorted batch (labs: k_labs_w, ordered pushes; k_labs, any order)"}
 
 
 def parse():
@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=["auto", "general", "scan", "labs"], default="auto",
                     help="auto = the engine's default path; scan = round-1 scan kernels; general = NFA lanes; "
-                         "labs = the opt-in logical-absent kernel (C4, force_general 4)")
+                         "labs = the logical-absent automaton (C4, force_general 4; the auto path for C4 too)")
     ap.add_argument("--same-device", action="store_true",
                     help="N>1 rehearsal on a one-GPU box without torchrun: one process, an in-process group of "
                          "--gpus ranks all on cuda:0 (device copies stand in for RCCL)")

@@ -639,31 +639,32 @@ __device__ __forceinline__ bool la_kill(const LaPredD& p, const LaKill& K, doubl
 
 // one pass: records into the key's region of D.rec, the key's count into D.cm, the state into
 // copy wr; k_labs_out then writes the push's records contiguously.
-// The state it leaves is the exact rule's (k_labs, tests/labs_exact.py FastC4 states the formulas):
-// when the key's events do not go back in time, no event lags the clock by T or more and the clock
-// never steps by more than T, the Scheduler queue stays sorted and every entry the clock reached has
-// fired, so per pair P (completed at c, slots' earliest ts m, due = c + T, D = m + W):
+// The state it leaves is the exact rule's (k_labs; tests/labs_exact.py FastC4 states the formulas
+// and checks them against the exact rule, state included): when the key's events do not go back in
+// time, no event lags the clock by T or more and the clock never steps by more than T, the
+// Scheduler queue stays sorted and every entry the clock reached has fired, so per pair P
+// (completed at c, slots' earliest ts m, due = c + T, D = m + W):
 //   E_D   = min(due, the first queued entry > max(D, clock(c)) at c): P leaves the pending list --
 //           emitted when due <= D, else expired -- at the first key event q > c with clock(q) >= E_D
 //           or ts(q) > D (or when the push's last clock reaches E_D);
 //   kill  = the first Z event in (c, that q) whose fz holds; it queues an entry ts + T;
-//   H     = the queue's head at c: P is still on new-and-every at the end iff no Z event of the key
-//           came after c and H > the last clock;
+//   P is still on new-and-every at the end iff no Z event of the key and no firing of its queue
+//   came after c;
 // lastScheduledTime = ts + T of the key's last completion or kill; the queue keeps every entry past
 // the last clock.  A push or state outside that raises LA_SLOW (k_labs re-runs it exactly).
-constexpr int LA_WF = 64;  // queue entries k_labs_w holds (LDS)
+// The queue lives in registers, entry i in lane i (sorted); the entries a block queues are counted
+// per event lane (a completion, or the pairs a Z event kills), all at that event's ts + T.
+constexpr int LA_WF = 64;  // queue entries k_labs_w holds (one per lane)
 
 static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
                                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                                int* err) {
-  __shared__ LaWait A[64];   // the pairs on the absent state's lists, list (= completion) order
-  __shared__ int32_t Ac[64];  // completing lane in the current block (-1: an earlier block)
-  __shared__ int64_t Aed[64];  // E_D of each pair
-  __shared__ int64_t Ah[64];   // H of each pair
-  __shared__ uint8_t Anae[64];  // on new-and-every (no Z event of the key since its completion)
-  __shared__ int64_t Ef[2 * LA_WF];  // the queue: entries queued before this block, sorted
-  __shared__ int64_t BE[64];  // entries queued in this block (completions, then kills) and their lanes
-  __shared__ int32_t BEl[64];
+  __shared__ LaWait A[64];      // the pairs on the absent state's lists, list (= completion) order
+  __shared__ int32_t Ac[64];    // completing lane in the current block (-1: an earlier block)
+  __shared__ int64_t Aed[64];   // E_D of each pair
+  __shared__ uint8_t Anae[64];  // on new-and-every (no Z event and no firing since its completion)
+  __shared__ int32_t Ec[64];    // per event lane of the block: entries it queued (completion + kills)
+  __shared__ int64_t Es[64];    // staging of the queue's new order
   const int k = blockIdx.x;
   if (k >= D.nk) return;
   const int lane = (int)threadIdx.x;
@@ -688,24 +689,29 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       return;
     }
   }
-  if (lane < nef) Ef[lane] = D.fq[rd][(int64_t)k * cap + ((s0.eh + lane) & msk)].t;
-  __syncthreads();
+  int64_t qe = lane < nef ? D.fq[rd][(int64_t)k * cap + ((s0.eh + lane) & msk)].t : INT64_MAX;  // the queue
+  Ec[lane] = 0;
   if (lane < nal) {
     const LaWait w = D.wq[rd][(int64_t)k * cap + ((s0.wh + lane) & msk)];
     A[lane] = w;
     Ac[lane] = -1;
     Anae[lane] = lane >= nal - s0.nae ? 1 : 0;
-    // a carried pair: E_D from the queue as it stands (every entry > the clock; its own due among them)
-    const int64_t dd = min(w.xts, w.yts) + Wb;
-    int64_t ed = w.due, h = w.due;
+  }
+  {  // a carried pair's E_D: the first queued entry past D (every entry is past the clock; its own due is one)
+    int64_t dd = INT64_MAX, due = INT64_MAX;
+    if (lane < nal) {
+      const LaWait& w = A[lane];
+      dd = min(w.xts, w.yts) + Wb;
+      due = w.due;
+    }
+    int64_t ed = due;
     for (int i = 0; i < nef; i++) {
-      const int64_t t = Ef[i];
-      h = min(h, t);
+      const int64_t t = la_rl64(qe, i);
       if (t > dd) ed = min(ed, t);
     }
-    Aed[lane] = ed;
-    Ah[lane] = h;
+    if (lane < nal) Aed[lane] = ed;
   }
+  __syncthreads();
   const uint32_t beg = kbeg[k], cnt = kcnt[k];
   LaRec* rec = D.rec + la_region(beg, k);
   const uint32_t rcap = (cnt + 1u) / 2u + 64u;  // the region's records (la_region)
@@ -719,11 +725,10 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   int64_t last = s0.last;
   int64_t lsched = s0.lst;  // lastScheduledTime
   int64_t lo = 0;  // first batch index a timer can fire at (after the key's previous event)
-  int nbe = 0;     // entries queued in the current block
-  int lsl = -1;    // the block's last lane that queued an entry (a completion or a kill)
   // the pairs (one per lane) leave (left: in [flo, fhi]) -- emitted when within W of their due
   // time -- or are killed; the survivors are compacted in order
-  auto settle = [&](bool left, bool killed, bool tonae, int64_t flo, int64_t fhi, LaWait w, int64_t ed, int64_t h) {
+  auto settle = [&](bool left, bool killed, bool tonae, int64_t flo, int64_t fhi, LaWait w, int64_t ed)
+                    __attribute__((always_inline)) {
     const bool ok = lane < nal && left && !killed &&
                     (!useW || (llabs(w.xts - w.due) <= Wn && llabs(w.yts - w.due) <= Wn));
     const uint64_t em = __ballot(ok);
@@ -746,7 +751,6 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       A[d] = w;
       Ac[d] = -1;
       Aed[d] = ed;
-      Ah[d] = h;
       Anae[d] = tonae ? 1 : 0;
     }
     nal = __popcll(sm);
@@ -774,7 +778,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   int64_t n_ts = 0, n_clk = 0;
   uint32_t n_g = 0, n_v = 0, n_n = 1;
   int32_t n_st = -1;
-  auto fetch = [&](uint32_t j0) {
+  auto fetch = [&](uint32_t j0) __attribute__((always_inline)) {
     if (j0 + (uint32_t)lane < cnt) {
       const LaEv x = la_ev_at(D, B, (int64_t)beg + j0 + lane);
       n_ts = x.ts;
@@ -821,13 +825,12 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     //    position is walked with one readlane per step.
     int p0 = 0;
     if (hx || hy) {
-      LA_COUNT(5, 1);
       const int64_t tf = hx ? xts : yts;
       const uint64_t Em = useW ? __ballot(valid && ts - tf > Wn) : 0ull;
       const uint64_t Om = hx ? QY : QX;
       const int z = Em ? __builtin_ctzll(Em) : 64, b = Om ? __builtin_ctzll(Om) : 64;
       if (b < z) {  // the partner: the pair completes and waits on the absent state
-        if (nal >= 64 || nbe >= 64) {
+        if (nal >= 64) {
           if (lane == 0) {
             D.cm[k] = 0;
             atomicOr(err, LA_SLOW);
@@ -862,12 +865,10 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
           A[nal] = w;
           Ac[nal] = b;
           Anae[nal] = 1;
-          BE[nbe] = w.due;
-          BEl[nbe] = b;
+          Aed[nal] = w.due;
+          Ec[b] = 1;
         }
         nal++;
-        nbe++;
-        lsl = max(lsl, b);
         hx = hy = false;
         xseq = yseq = -1;
         fl = 0;
@@ -927,7 +928,6 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     uint64_t PM = 0;  // chain positions whose step completes a pair
     int hk = -1;      // chain position that leaves a half partial
     for (int p = p0; p < nv;) {
-      LA_COUNT(5, 1);
       const int kj = __builtin_amdgcn_readlane(KJ, p);
       const int kd = kj >> 8;
       if (kd == 1) {
@@ -942,7 +942,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     }
     if (PM) {  // the completed pairs, in completion order, join the absent state's new-and-every list
       const int npm = __popcll(PM);
-      if (nal + npm > 64 || nbe + npm > 64) {
+      if (nal + npm > 64) {
         if (lane == 0) {
           D.cm[k] = 0;
           atomicOr(err, LA_SLOW);
@@ -969,12 +969,10 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
         A[d] = w;
         Ac[d] = b;
         Anae[d] = 1;
-        BE[nbe + __popcll(PM & lt)] = w.due;
-        BEl[nbe + __popcll(PM & lt)] = b;
+        Aed[d] = w.due;
+        Ec[b] = 1;
       }
       nal += npm;
-      nbe += npm;
-      lsl = max(lsl, __builtin_amdgcn_readlane(b, 63 - __builtin_clzll(PM)));
     }
     if (hk >= 0) {  // the slot event a of the chain's last step
       const int ha = __builtin_amdgcn_readlane(a, hk);
@@ -1000,66 +998,62 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     const uint64_t zm = __ballot(valid && role == 2);
     const int lastz = zm ? 63 - __builtin_clzll(zm) : -1;  // the block's last Z event (new-and-every -> pending)
     const int64_t clkl = la_rl64(clk, nv - 1);            // the clock at the block's last event
+    const uint64_t cmask = __ballot(valid && Ec[lane] != 0);  // lanes that completed a pair
+    const int64_t qt = ts + Tw;                            // the time of an entry this event queues
     // 2. the pairs against this block's events
     if (nal > 0) {
       LaWait w{};
       int c = 64;
-      int64_t ed = 0, h = 0;
+      int64_t ed = 0;
       if (lane < nal) {
         w = A[lane];
         c = Ac[lane];
         ed = Aed[lane];
-        h = Ah[lane];
       }
       const int64_t dd = min(w.xts, w.yts) + Wb;
-      const int64_t cc = __shfl(clk, c >= 0 && c < 64 ? c : 0, 64);  // (lanes with c < 0 ignore it)
-      const int ncb = nbe;  // the block's completion entries (BE[0, ncb))
-      // E_D and H of a pair completed in this block: the entries queued before c and not fired at c
-      auto at_c = [&](int nk) {
-        if (lane < nal && c >= 0) {
-          int64_t e2 = w.due, h2 = w.due;
-          for (int i = 0; i < nef; i++) {
-            const int64_t t = Ef[i];
-            if (t > cc) {
-              h2 = min(h2, t);
-              if (t > dd) e2 = min(e2, t);
-            }
-          }
-          for (int i = 0; i < nk; i++) {
-            const int64_t t = BE[i];
-            if (BEl[i] < c && t > cc) {
-              h2 = min(h2, t);
-              if (t > dd) e2 = min(e2, t);
-            }
-          }
-          ed = e2;
-          h = h2;
-        }
+      // pairs completed in this block and past their D before their due: their E_D looks at the queue
+      uint64_t doom = __ballot(lane < nal && c >= 0 && w.due > dd);
+      // E_D of pair j (completed at cj): the first entry past max(D, clock(cj)) among the queue and
+      // the block's entries queued before cj (em: the event lanes that queued some)
+      auto edj = [&](int j, uint64_t em) __attribute__((always_inline)) -> int64_t {
+        const int cj = __builtin_amdgcn_readlane(c, j);
+        const int64_t thr = max(la_rl64(dd, j), la_rl64(clk, cj));
+        int64_t r = la_rl64(w.due, j);
+        const uint64_t qm = __ballot(lane < nef && qe > thr);
+        if (qm) r = min(r, la_rl64(qe, __builtin_ctzll(qm)));
+        const uint64_t bm = em & __ballot(lane < cj && qt > thr);
+        if (bm) r = min(r, la_rl64(qt, __builtin_ctzll(bm)));
+        return r;
       };
-      at_c(ncb);
+      for (uint64_t m = doom; m; m &= m - 1) {
+        const int j = __builtin_ctzll(m);
+        const int64_t r = edj(j, cmask);
+        if (lane == j) ed = r;
+      }
+      LA_STAMP(2);
       int f = 64, kq = 64;
       bool killed = false;
       // the leave event: the first event after c whose clock reaches E_D or whose ts passes D (both
       // ascend in the block); the kill: the first Z event before it whose filter holds.  A kill queues
-      // an entry that may lower a later pair's E_D: repeat until no E_D changes
+      // an entry that may lower a later doomed pair's E_D: repeat until none changes
       for (int it = 0; it < 65; it++) {
         int l2 = c + 1, h2 = nv;  // the answer lies in [l2, h2]; h2 = nv: not in this block
 #pragma unroll
         for (int st7 = 0; st7 < 7; st7++) {
           const int mid = (l2 + h2) >> 1;
-          const int64_t cm = __shfl(clk, mid < 64 ? mid : 0, 64), tm = __shfl(ts, mid < 64 ? mid : 0, 64);
+          const int ms = mid < 64 ? mid : 0;
+          const int64_t cm = __shfl(clk, ms, 64), tm = __shfl(ts, ms, 64);
           if (l2 < h2) {
             if (mid < nv && (cm >= ed || tm > dd)) h2 = mid;
             else l2 = mid + 1;
           }
         }
         f = lane < nal && l2 < nv ? l2 : 64;
-        LA_STAMP(2);
         killed = false;
         kq = 64;
         if (zm) {
           const LaKill K = la_kill_pre(D.fz, w, t0g, t1g, t2g);
-          auto nextz = [&](int x) -> int {
+          auto nextz = [&](int x) __attribute__((always_inline)) -> int {
             if (x >= 64) return 64;
             const uint64_t r = zm >> x;
             return r ? x + __builtin_ctzll(r) : 64;
@@ -1078,129 +1072,130 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
             }
           }
         }
-        // the kills' entries, in pair order after the completions'
         const uint64_t km = __ballot(killed);
-        const int64_t tkq = __shfl(ts, kq < 64 ? kq : 0, 64);
-        if (ncb + __popcll(km) > 64) {
+        if (!km || !doom) break;
+        // the kills' lanes: do they come before a doomed pair's completion?
+        int kmin = killed ? kq : 64;
+        for (int o = 32; o > 0; o >>= 1) kmin = min(kmin, __shfl_xor(kmin, o, 64));
+        uint64_t redo = 0;
+        for (uint64_t m = doom; m; m &= m - 1) {
+          const int j = __builtin_ctzll(m);
+          if (__builtin_amdgcn_readlane(c, j) <= kmin) continue;
+          uint64_t kl = 0;  // event lanes with a kill
+          for (uint64_t mm = km; mm; mm &= mm - 1) kl |= 1ull << __builtin_amdgcn_readlane(kq, __builtin_ctzll(mm));
+          const int64_t r = edj(j, cmask | kl);
+          const int64_t cur = la_rl64(ed, j);
+          if (r != cur) {
+            redo |= 1ull << j;
+            if (lane == j) ed = r;
+          }
+        }
+        if (!redo) break;
+      }
+      LA_STAMP(3);
+      // the kills, counted per event lane (each queues an entry at the event's ts + T)
+      if (killed) atomicAdd(&Ec[kq], 1);
+      __syncthreads();
+      const uint64_t emk = __ballot(valid && Ec[lane] != 0);  // event lanes that queued entries
+      const bool left = f < 64;
+      const int64_t gp = (int64_t)(uint32_t)__shfl(g, f > 0 ? f - 1 : 0, 64);
+      const int64_t gf = (int64_t)(uint32_t)__shfl(g, f < 64 ? f : 0, 64);
+      // the block's last firing of the queue (before which event lane): of its latest fired entry,
+      // an old one (queued before the block) or one the block queued
+      int lastf = -1;
+      {
+        const uint64_t fo = __ballot(lane < nef && qe <= clkl);
+        if (fo) {
+          const int64_t t = la_rl64(qe, 63 - __builtin_clzll(fo));
+          const uint64_t r = __ballot(valid && clk >= t);
+          lastf = max(lastf, __builtin_ctzll(r));
+        }
+        const uint64_t fb = emk & __ballot(valid && qt <= clkl);
+        if (fb) {
+          const int p = 63 - __builtin_clzll(fb);
+          const int64_t t = la_rl64(qt, p);
+          const uint64_t r = __ballot(valid && lane > p && clk >= t);
+          lastf = max(lastf, __builtin_ctzll(r));
+        }
+      }
+      const bool tonae = lane < nal && Anae[lane] && c >= lastf && c >= lastz;  // no Z / firing after it
+      settle(left, killed, tonae, f == 0 ? lo : gp + 1, gf, w, ed);
+      LA_STAMP(4);
+    }
+    LA_STAMP(0);
+    // the queue: the entries the block's clock reached have fired; the block's own join in lane
+    // (= time) order; lastScheduledTime from the block's last completion or kill
+    {
+      const int ecl = valid ? Ec[lane] : 0;
+      const uint64_t qm = __ballot(ecl != 0);
+      if (qm || nef) {
+        const uint64_t keep = __ballot(lane < nef && qe > clkl);  // a suffix (sorted)
+        const int n0 = __popcll(keep);
+        const int drop = nef - n0;
+        int64_t x = __shfl(qe, lane + drop < 64 ? lane + drop : 63, 64);
+        // the block's entries still queued, expanded (a Z event that kills several pairs queues several)
+        const int ec2 = qt > clkl ? ecl : 0;
+        int pos = ec2;
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive scan of the counts
+          const int y = __shfl_up(pos, o, 64);
+          if (lane >= o) pos += y;
+        }
+        const int n1 = __shfl(pos, 63, 64);
+        if (n0 + n1 > LA_WF) {
           if (lane == 0) {
             D.cm[k] = 0;
             atomicOr(err, LA_SLOW);
           }
           return;
         }
+        for (int i = pos - ec2; i < pos; i++) Es[n0 + i] = qt;
         __syncthreads();
-        if (killed) {
-          const int d = ncb + __popcll(km & lt);
-          BE[d] = tkq + Tw;
-          BEl[d] = kq;
-        }
-        nbe = ncb + __popcll(km);
+        if (lane < n0) Es[lane] = x;
         __syncthreads();
-        const int64_t ed0 = ed;
-        at_c(nbe);
-        if (!__ballot(lane < nal && c >= 0 && ed != ed0)) break;
+        nef = n0 + n1;
+        qe = lane < nef ? Es[lane] : INT64_MAX;
+        if (qm) lsched = la_rl64(qt, 63 - __builtin_clzll(qm));
+        __syncthreads();
       }
-      LA_STAMP(3);
-      {  // the last completion or kill sets lastScheduledTime
-        const uint64_t km = __ballot(killed);
-        int kl = -1;
-        if (km) {
-          int kmax = killed ? kq : -1;
-          for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
-          kl = kmax;
-        }
-        lsl = max(lsl, kl);
-      }
-      const bool left = f < 64;
-      const int64_t gp = (int64_t)(uint32_t)__shfl(g, f > 0 ? f - 1 : 0, 64);
-      const int64_t gf = (int64_t)(uint32_t)__shfl(g, f < 64 ? f : 0, 64);
-      const bool tonae = lane < nal && Anae[lane] && c >= lastz;  // no Z event after its completion
-      settle(left, killed, tonae, f == 0 ? lo : gp + 1, gf, w, ed, h);
-      LA_STAMP(4);
+      Ec[lane] = 0;
     }
-    // the queue: this block's entries join in lane order (= time order); the entries its clock
-    // reached have fired
-    if (nbe > 0) {
-      __syncthreads();
-      int64_t t = 0;
-      int l = 0;
-      if (lane < nbe) {
-        t = BE[lane];
-        l = BEl[lane];
-      }
-      // rank by (lane, index): completions before kills at one lane cannot happen (different events)
-      int r = 0;
-      for (int i = 0; i < nbe; i++) {
-        const int li = BEl[i];
-        r += (li < l || (li == l && i < lane)) ? 1 : 0;
-      }
-      __syncthreads();
-      if (lane < nbe) BE[r] = t;
-      __syncthreads();
-    }
-    {
-      // drop the fired (t <= clkl), append the block's entries
-      int keep0 = 0;
-      for (int i = 0; i < nef; i++) keep0 += Ef[i] <= clkl ? 1 : 0;  // a sorted prefix
-      int keep1 = 0;
-      for (int i = 0; i < nbe; i++) keep1 += BE[i] <= clkl ? 1 : 0;
-      const int n0 = nef - keep0, n1 = nbe - keep1;
-      if (n0 + n1 > LA_WF) {
-        if (lane == 0) {
-          D.cm[k] = 0;
-          atomicOr(err, LA_SLOW);
-        }
-        return;
-      }
-      int64_t a0 = 0, a1 = 0;
-      if (lane < n0) a0 = Ef[keep0 + lane];
-      if (lane < n1) a1 = BE[keep1 + lane];
-      __syncthreads();
-      if (lane < n0) Ef[lane] = a0;
-      if (lane < n1) Ef[n0 + lane] = a1;
-      nef = n0 + n1;
-      __syncthreads();
-    }
-    if (lsl >= 0) lsched = la_rl64(ts, lsl) + Tw;
-    lsl = -1;
-    nbe = 0;
+    LA_STAMP(5);
     lo = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)g, nv - 1) + 1;
     last = la_rl64(ts, nv - 1);
+    __syncthreads();
   }
   // the timers the push's last clock reaches
   const int64_t lastclk = B.n > 0 ? B.rmax[B.n - 1] : B.clock0;
+  const bool flushed = __ballot(lane < nef && qe <= lastclk) != 0;  // a firing after every event of the key
   if (nal > 0) {
     LaWait w{};
-    int64_t ed = 0, h = 0;
+    int64_t ed = 0;
     bool nae = false;
     if (lane < nal) {
       w = A[lane];
       ed = Aed[lane];
-      h = Ah[lane];
-      nae = Anae[lane] != 0;
+      nae = Anae[lane] != 0 && !flushed;
     }
-    settle(lane < nal && ed <= lastclk, false, nae, lo, B.n - 1, w, ed, h);
+    settle(lane < nal && ed <= lastclk, false, nae, lo, B.n - 1, w, ed);
   }
   {  // the queue keeps the entries past the last clock
-    int drop = 0;
-    for (int i = 0; i < nef; i++) drop += Ef[i] <= lastclk ? 1 : 0;
-    int64_t a0 = 0;
-    if (lane < nef - drop) a0 = Ef[drop + lane];
-    __syncthreads();
-    nef -= drop;
+    const uint64_t keep = __ballot(lane < nef && qe > lastclk);
+    const int n0 = __popcll(keep);
+    const int drop = nef - n0;
+    const int64_t x = __shfl(qe, lane + drop < 64 ? lane + drop : 63, 64);
+    nef = n0;
     if (nef <= cap && lane < nef) {
-      LaEnt x;
-      x.t = a0;
-      x.i0 = 0;
-      x.pad = 0;
-      D.fq[wr][(int64_t)k * cap + lane] = x;
+      LaEnt y;
+      y.t = x;
+      y.i0 = 0;
+      y.pad = 0;
+      D.fq[wr][(int64_t)k * cap + lane] = y;
     }
   }
-  // new-and-every: the trailing pairs with no Z event since their completion and no timer since
+  // new-and-every: the trailing pairs with no Z event and no firing since their completion
   int nae = 0;
   {
-    const bool q = lane < nal && Anae[lane] && Ah[lane] > lastclk;
-    const uint64_t m = __ballot(q);
+    const uint64_t m = __ballot(lane < nal && Anae[lane]);
     const uint64_t all = nal >= 64 ? ~0ull : ((1ull << nal) - 1ull);
     const uint64_t notq = all & ~m;
     nae = notq ? nal - 1 - (63 - __builtin_clzll(notq)) : nal;

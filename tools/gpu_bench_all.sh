@@ -1,6 +1,6 @@
 #!/bin/bash
-# GPU box: bench lines (with CPU baselines) for every SURVEY §8d config on its default path, plus
-# the opt-in labs path for C4 and C3 as specified.  CONFIGS overrides the list; each line lands in
+# GPU box: bench lines (with CPU baselines) for every SURVEY §8d config on its default path
+# (C4's is the logical-absent automaton since round 5), and C3 as specified.  CONFIGS overrides the list; each line lands in
 # gpurun_out/bench_<name>.json.  Stops at the first failing run.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -10,13 +10,13 @@ run() {  # name, timeout, args...
   grep '^{' gpurun_out/bench_$name.log > gpurun_out/bench_$name.json
   python3 -c "import json; d=json.load(open('gpurun_out/bench_$name.json')); c=d['cpu_baseline'] or {}; print('$name', round(d['value']/1e9,3), 'G/s', round(d['ms_per_step'],3), 'ms', d['config']['engine_path'][:60], 'frac', round(d['roofline']['frac'],3), 'cpu', c.get('value'))"
 }
-for c in ${CONFIGS:-c3b c5 c4labs c4 c3 c1}; do
+for c in ${CONFIGS:-c3b c5 c4 c3 c1}; do
   case $c in
     c2) run c2 400 ;;
     c3b) run c3b 400 --config 3b ;;
     c5) run c5 400 --config 5 ;;
-    c4labs) run c4labs 500 --config 4 --path labs ;;
-    c4) run c4 700 --config 4 --steps 2 --warmup 1 --latency-batches 0 ;;
+    c4) run c4 500 --config 4 ;;
+    c4lanes) run c4lanes 700 --config 4 --path general --steps 2 --warmup 1 --latency-batches 0 ;;
     c3) run c3 600 --config 3 --steps 3 --warmup 1 --latency-batches 0 ;;
     c1) run c1 500 --config 1 --steps 3 --warmup 1 ;;
   esac || exit 1

@@ -53,12 +53,12 @@ def main():
             L.shp_debug_la_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
             nk = L.shp_debug_la_stamps(eng.h, buf, K * 8)
             st = np.frombuffer(buf, dtype=np.uint64, count=nk * 8).reshape(nk, 8).astype(np.float64)
-            names = ["load+filters", "partial", "fire", "kill", "settle"]
-            tot = st[:, :5].sum()
+            names = ["load+filters", "partial", "fire", "kill", "settle", "queue"]
+            tot = st[:, :6].sum()
             blocks = st[:, 7].sum() / 64
-            for x in range(5):
+            for x in range(6):
                 print(f"    {names[x]:<14} {100 * st[:, x].sum() / tot:5.1f}%  cycles/block {st[:, x].sum() / blocks:8.0f}")
-            print(f"    partial trips/block {st[:, 5].sum() / blocks:.1f}  waiting pairs/block {st[:, 6].sum() / blocks:.1f}"
+            print(f"    waiting pairs/block {st[:, 6].sum() / blocks:.1f}"
                   f"  events/key {st[:, 7].mean():.0f}  cycles/key {st[:, :5].sum(1).mean():.3e}")
 
 
