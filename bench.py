@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--latency-events", type=int, default=16_000_000)
     ap.add_argument("--pairs-layout", choices=["pairs32", "pairs"], default="pairs32",
                     help="match payload of the 2-state sweep: 8-byte PAIRS32 (default) or 16-byte PAIRS")
+    ap.add_argument("--disorder", type=float, default=0.0,
+                    help="fraction of events whose ts is moved back by up to 8 s (C4: the exact kernel, k_labs, "
+                         "takes such pushes; a measurement of that path, not the headline)")
     ap.add_argument("--cseq-layout", choices=["chain32", "full"], default="chain32",
                     help="match payload of the count-sequence path (C3'): 4-byte CHAIN32 words (default) or FULL")
     return ap.parse_args()
@@ -163,6 +166,10 @@ def main():
                               key.data_ptr(), price.data_ptr(), None,
                               stream.data_ptr() if stream is not None else None, None)
         assert rc == 0
+        if a.disorder > 0:  # events going back in time (seeded by the step, so every run is the same stream)
+            gg = torch.Generator(device="cuda").manual_seed(1000 + start)
+            back = torch.rand(N, device="cuda", generator=gg) < a.disorder
+            ts -= back.to(torch.int64) * torch.randint(0, 8000, (N,), device="cuda", generator=gg)
         return ts, key, price, stream
 
     batches = [[gen(s, r) for r in my_ranks] for s in range(steps)]
@@ -306,7 +313,7 @@ def main():
             "dtype": "f32 compare / int64 ts",
             "data": "synthetic (PCG32 stream of SURVEY.md §8d, generated in HBM)",
             "config": {
-                "workload": WORKLOADS.get(str(cfg_id), f"C{cfg_id}") + f"; {K} keys",
+                "workload": WORKLOADS.get(str(cfg_id), f"C{cfg_id}") + f"; {K} keys" + (f"; {a.disorder:g} of events moved back by up to 8 s" if a.disorder else ""),
                 "events_per_gpu_per_step": N,
                 "keys": K,
                 "parallelism": par,

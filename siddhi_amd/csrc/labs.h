@@ -1012,7 +1012,8 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       }
       const int64_t dd = min(w.xts, w.yts) + Wb;
       // pairs completed in this block and past their D before their due: their E_D looks at the queue
-      uint64_t doom = __ballot(lane < nal && c >= 0 && w.due > dd);
+      const uint64_t doomall = __ballot(lane < nal && w.due > dd);  // past D before their due
+      const uint64_t doom = doomall & __ballot(c >= 0);              // ... and completed in this block
       // E_D of pair j (completed at cj): the first entry past max(D, clock(cj)) among the queue and
       // the block's entries queued before cj (em: the event lanes that queued some)
       auto edj = [&](int j, uint64_t em) __attribute__((always_inline)) -> int64_t {
@@ -1037,18 +1038,25 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       // ascend in the block); the kill: the first Z event before it whose filter holds.  A kill queues
       // an entry that may lower a later doomed pair's E_D: repeat until none changes
       for (int it = 0; it < 65; it++) {
+        // (a pair not past D before its due leaves at its due: ts > D implies clock > due there)
         int l2 = c + 1, h2 = nv;  // the answer lies in [l2, h2]; h2 = nv: not in this block
 #pragma unroll
         for (int st7 = 0; st7 < 7; st7++) {
           const int mid = (l2 + h2) >> 1;
-          const int ms = mid < 64 ? mid : 0;
-          const int64_t cm = __shfl(clk, ms, 64), tm = __shfl(ts, ms, 64);
+          const int64_t cm = __shfl(clk, mid < 64 ? mid : 0, 64);
           if (l2 < h2) {
-            if (mid < nv && (cm >= ed || tm > dd)) h2 = mid;
+            if (mid < nv && cm >= ed) h2 = mid;
             else l2 = mid + 1;
           }
         }
         f = lane < nal && l2 < nv ? l2 : 64;
+        for (uint64_t m = doomall; m; m &= m - 1) {  // a pair past D before its due: or the first event beyond D
+          const int j = __builtin_ctzll(m);
+          const int cj = __builtin_amdgcn_readlane(c, j);
+          const uint64_t xm = __ballot(valid && lane > cj && ts > la_rl64(dd, j));
+          const int fx = xm ? __builtin_ctzll(xm) : 64;
+          if (lane == j) f = min(f, fx);
+        }
         killed = false;
         kq = 64;
         if (zm) {
