@@ -878,6 +878,7 @@ struct CseqState {
   CoDev P{};
   bool own = false;
   uint32_t* ch = nullptr;  // CHAIN32 words staged for the expansion (mcap)
+  bool ch_saved = false;   // this push's words are in `ch` (set by the first expansion, reset per push)
   int64_t mcap = 0;
 
   // owners and local keys for nk keys with M history slots: false when they do not fit
@@ -1143,7 +1144,10 @@ struct CseqState {
     if (m > mcap) throw std::runtime_error("count-sequence expansion: more matches than the staging buffer");
     const int64_t n = B.n;
     kt.mark("cs_expand", s);
-    (void)hipMemcpyAsync(ch, O.refs, (size_t)m * 4, hipMemcpyDeviceToDevice, s);
+    // the words move to `ch` once per push: an expansion that failed (and overwrote part of O.refs
+    // with FULL refs) re-runs from `ch`
+    if (!ch_saved) (void)hipMemcpyAsync(ch, O.refs, (size_t)m * 4, hipMemcpyDeviceToDevice, s);
+    ch_saved = true;
     const unsigned gp = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     k_cs_pack<CsRec><<<gp, 256, 0, s>>>(B.ts, key, stream, (const uint32_t*)B.cols[0], B.nulls[0], n, B.partitioned,
                                         (uint32_t)D.nk, D.pk, D.pr, D.tsmax, err);

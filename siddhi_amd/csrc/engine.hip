@@ -420,6 +420,9 @@ struct shp_engine {
     HIP_OK(hipHostMalloc((void**)&h_status, 4 * sizeof(unsigned long long), hipHostMallocDefault));
     mcap = cfg.max_matches;
     rcap = mcap * comp.P.nstates * 2 + 64;
+    // CHAIN32: a committed push must always expand to FULL (shp_fetch_matches, the group gather come
+    // after the commit), so the refs hold the longest chains: L + 1 <= M + 1 per match
+    if (cfg.match_layout == SHP_LAYOUT_CHAIN32) rcap = std::max<int64_t>(rcap, mcap * (comp.cseq.M + 1) + 64);
     alloc(d_mkey, mcap);
     alloc(d_mts, mcap);
     alloc(d_mpos, mcap);
@@ -478,6 +481,7 @@ struct shp_engine {
   // the caller's HBM columns for shp_push_batch_device); leaves matches in HBM
   int run(int64_t n, bool clock_only = false, const shp_batch* in = nullptr, bool staged_clk = false,
           bool staged_seq = false) {
+    cs.ch_saved = false;  // a new push: its CHAIN32 words are in O.refs
     const DevProg& P = comp.P;
     const int64_t* x_ts = in ? in->ts : d_ts;
     const int64_t* x_clk = in ? in->clock : (staged_clk ? d_clk : nullptr);
@@ -1289,7 +1293,8 @@ struct shp_engine {
     HIP_OK(hipMemcpyAsync(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
     if (herr & SWE_BOUND) throw DevError("internal: a match pair names an event outside its push (SWE_BOUND)");
-    if (herr & E_OUT) throw DevError("match refs beyond the engine's ref capacity (CHAIN32 expansion)");
+    if (herr & E_OUT)  // (unreachable: rcap holds M + 1 refs per match for CHAIN32 engines)
+      throw std::runtime_error("SHP_ERR_OUTPUT: CHAIN32 expansion beyond the ref capacity (raise max_matches)");
     expanded = true;
   }
 

@@ -164,3 +164,25 @@ def test_chain32_rejected_off_the_count_sequence_path():
     from siddhi_amd.native import LAYOUT_CHAIN32, HipEngine, ShpError
     with pytest.raises(ShpError):
         HipEngine(program_for(2).program_json(), 0, max_keys=300, max_batch=1 << 16, match_layout=LAYOUT_CHAIN32)
+
+
+def test_chain32_long_chains_with_a_small_match_buffer(path):
+    """max_matches barely above the matches of a push, every match an M = 7 chain: the push commits
+    and its expansion always fits (a CHAIN32 engine's ref capacity holds M + 1 refs per match), so
+    shp_fetch_matches returns every record exactly (the expansion used to fail after the
+    commit and lose the matches)."""
+    from siddhi_amd.native import LAYOUT_CHAIN32, HipEngine
+    app = _app(7, "<", "float")
+    cq = _cq(app)
+    n = 20_000
+    # one key, values rising then one drop: chains of 7 close at every drop
+    v = np.tile(np.array([30, 31, 32, 33, 34, 35, 36, 10], np.float32), n // 8)
+    g = {"ts": np.arange(n, dtype=np.int64) + 1000, "key": np.zeros(n, np.int32), "stream": np.zeros(n, np.int32),
+         "price": v}
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g))
+    m = sum(len(x) for x in want.values())
+    assert m >= 2000 and all(len(r[3][0]) == 7 for x in want.values() for r in x)
+    e = HipEngine(cq.program_json(), 0, max_keys=1, max_batch=n, max_matches=m + 16, match_layout=LAYOUT_CHAIN32)
+    got = per_key(run(e, cq, g))
+    assert compare(want, got) is None, compare(want, got)
+    assert e.fetch()["key"].size == 0
