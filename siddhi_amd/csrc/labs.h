@@ -283,19 +283,18 @@ __device__ __forceinline__ bool la_expired(int64_t xts, int64_t yts, int64_t t, 
 }
 
 // the batch index at which a queue entry for time t fires, queued so that it may fire from batch
-// index i0 on: the first send at or after i0 whose clock reaches t and sets the clock; B.n: not in
-// this push (the playback clock B.rmax is non-decreasing; a send sets it iff tclk == rmax)
-__device__ int64_t la_fire_at(const BatchView& B, int64_t t, int64_t i0) {
-  const int64_t n = B.n;
-  if (i0 >= n) return n;
-  int64_t a = i0, b = n;
+// index i0 on: the first send in [i0, hi] whose clock reaches t and sets the clock, or hi + 1 (the
+// playback clock B.rmax is non-decreasing; a send sets it iff tclk == rmax).  The caller knows the
+// clock at hi reached t.
+__device__ int64_t la_fire_at(const BatchView& B, int64_t t, int64_t i0, int64_t hi) {
+  int64_t a = i0, b = hi;
   while (a < b) {
     const int64_t m = a + ((b - a) >> 1);
     if (B.rmax[m] >= t) b = m;
     else a = m + 1;
   }
-  if (a < n && a == i0 && (i0 == 0 ? B.clock0 : B.rmax[i0 - 1]) >= t)
-    while (a < n && B.tclk[a] != B.rmax[a]) a++;  // the clock was already there: the next send that sets it
+  if (a == i0 && (i0 == 0 ? B.clock0 : B.rmax[i0 - 1]) >= t)
+    while (a <= hi && B.tclk[a] != B.rmax[a]) a++;  // the clock was already there: the next send that sets it
   return a;
 }
 
@@ -446,10 +445,13 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
       push_entry(et + Tw, g);
     }
   };
-  auto fire = [&](int64_t upto) {
+  // the queue's heads that fire at a send at or before batch index upto (whose clock is clk_upto)
+  auto fire = [&](int64_t upto, int64_t clk_upto) {
     while (s.ne > 0) {
       const LaEnt x = fq[s.eh & msk];
-      const int64_t g = la_fire_at(B, x.t, max((int64_t)x.i0, gfired));
+      const int64_t i0 = max((int64_t)x.i0, gfired);
+      if (i0 > upto || clk_upto < x.t) break;  // (the clock is non-decreasing: not yet reached)
+      const int64_t g = la_fire_at(B, x.t, i0, upto);
       if (g > upto) break;
       s.eh = (s.eh + 1) & msk;
       s.ne--;
@@ -458,7 +460,7 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
     }
   };
   auto step = [&](const LaEv& x) {
-    fire((int64_t)x.g);
+    fire((int64_t)x.g, x.clk);
     const int64_t t = x.ts;
     s.last = t;
     // expireEvents over every pre of the key (StreamPreStateProcessor.expireEvents :326-361)
@@ -564,7 +566,7 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
 #pragma unroll 1
     for (uint32_t q = 0; q < nq; q++) step(sb[q]);
   }
-  if (live) fire(B.n - 1);  // the timers the push's last clock reaches
+  if (live && B.n > 0) fire(B.n - 1, B.rmax[B.n - 1]);  // the timers the push's last clock reaches
   if (!EMIT) {
     if (live) D.cm[k] = nm;
     return;
