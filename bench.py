@@ -69,6 +69,8 @@ def parse():
                     help="threads of the key-sharded CPU baseline (default: the box's CPU share, "
                          "OMP_NUM_THREADS, else os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-expanded", action="store_true",
+                    help="skip the second timed pass of a compact layout with its words expanded to FULL rows")
     ap.add_argument("--path", choices=["auto", "general", "scan", "labs"], default="auto",
                     help="auto = the engine's default path; scan = round-1 scan kernels; general = NFA lanes; "
                          "labs = the logical-absent automaton (C4, force_general 4; the auto path for C4 too)")
@@ -127,7 +129,7 @@ def main():
     force = {"auto": 0, "general": 1, "scan": 2, "labs": 4}[a.path]
     sweep = force == 0 and _sweep_shape(cq, local, K_local)
     layout = ("agg" if "aggregate" in cq.program else a.pairs_layout) if sweep else "full"
-    if cfg_id == "3b" and force == 0:  # the count-sequence path takes C3' by default
+    if cfg_id in ("3", "3b") and force == 0:  # the count-sequence path takes C3 and C3' by default
         layout = a.cseq_layout
     mlay = {"agg": native.LAYOUT_AGG, "pairs": native.LAYOUT_PAIRS, "pairs32": native.LAYOUT_PAIRS32,
             "chain32": native.LAYOUT_CHAIN32, "full": native.LAYOUT_FULL}[layout]
@@ -255,6 +257,10 @@ def main():
     else:
         ev_total, m_total = ev_local, m_local
 
+    expanded = None
+    if G == 1 and layout in ("chain32", "pairs32") and not a.no_expanded:
+        expanded = expanded_rate(eng, L, native, [gen(steps + s, 0) for s in range(1 + a.steps)], push, layout)
+
     latency = None
     if rank == 0 and G == 1 and a.latency_batches > 0 and layout != "full":
         latency = batch_latency(eng, L, native, spec, K, layout, a.latency_events, a.latency_batches,
@@ -324,6 +330,10 @@ def main():
                 "p99_batch_ms": float(np.percentile(lat, 99)),
                 "match_layout": layout,
                 "latency": latency,
+                # the compact words are not self-contained (a CHAIN32 word names its e2 event; the
+                # chain needs the batch's key column and the engine's pre-push history): the same
+                # path with each push's words expanded to FULL rows in HBM, timed the same way
+                "expanded": expanded,
             },
             "roofline": {
                 "bound": "hbm",
@@ -382,6 +392,34 @@ def _path_desc(eng, layout):
 def native_stat(eng, which):
     from siddhi_amd import native
     return native.lib().shp_engine_stat(eng.h, which.encode())
+
+
+def expanded_rate(eng, L, native, bats, push, layout):
+    """Pushes of fresh batches, each followed by the engine's expansion of its compact words into
+    FULL match rows in HBM (shp_engine_device_records: k_cs_expand / the sweep's pair expansion),
+    synchronously: events/s and ms per step of the self-contained form."""
+    import torch
+    out = native.ShpMatches()
+    nrefs = ctypes.c_int64(0)
+    L.shp_engine_device_records.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.shp_engine_device_records.restype = ctypes.c_int
+
+    def one(b):
+        n, m = push(*b)
+        rc = L.shp_engine_device_records(eng.h, ctypes.byref(out), ctypes.byref(nrefs))
+        if rc != 0:
+            raise native.ShpError(rc, L.shp_last_error(eng.h).decode())
+        return n, m
+    one(bats[0])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev = 0
+    for b in bats[1:]:
+        ev += one(b)[0]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k = len(bats) - 1
+    return {"value": ev / el, "ms_per_step": el / k * 1e3, "layout": f"{layout} + expansion to FULL rows"}
 
 
 def batch_latency(eng, L, native, spec, K, layout, n, batches, start):

@@ -174,7 +174,9 @@ int shp_push_batch(shp_engine* e, const shp_batch* in, shp_matches* out);
 /* HBM-resident batch (device pointers); matches stay in HBM (out holds device pointers).  With a
  * compact layout (PAIRS, PAIRS32, CHAIN32) the batch's device columns (ts, key, stream, seq) must stay
  * valid until the matches are fetched: shp_fetch_matches / shp_group_gather_matches expand the
- * compact records from them. */
+ * compact records from them.  Key ids are the caller's here: keep them dense in [0, max_keys) (as
+ * shp_dict issues them) -- the sweep spreads keys over its owners by the low bits of the id, so
+ * strided ids run on a few owners (exact, but slow). */
 int shp_push_batch_device(shp_engine* e, const shp_batch* in, shp_matches* out);
 /* Host-memory batch with compact match records: as shp_push_batch, but the records come back in the
  * layout the engine produced them in, copied to host memory without expansion -- out->layout says

@@ -667,11 +667,12 @@ class ProgramCompiler {
     if (t.get("t").sv != "next") return;
     const JV& a = t.get("a");
     const JV& b = t.get("b");
-    if (a.get("t").sv != "every" || b.get("t").sv != "stream" || b.get("state").i() != 1) return;
-    const JV& c = a.get("x");
-    if (c.get("t").sv != "count" || c.get("state").i() != 0 || c.get("min").i() != 1) return;
-    const int64_t mx = c.get("max").i();
-    if (mx < 1 || mx > CSEQ_MAXM) return;
+    if (b.get("t").sv != "stream" || b.get("state").i() != 1) return;
+    const bool every = a.get("t").sv == "every";  // (without it the start is armed once: cseq.h cs_tables)
+    const JV& c = every ? a.get("x") : a;
+    if (c.get("t").sv != "count" || c.get("state").i() != 0) return;
+    const int64_t mn = c.get("min").i(), mx = c.get("max").i();
+    if (mx < 1 || mx > CSEQ_MAXM || mn < 1 || mn > mx) return;
     if (P.pre[0].stream != P.pre[1].stream || P.ncol > 1) return;
     const JV& st = root.get("states");
     const JV& f1 = st[0].get("filter");
@@ -680,6 +681,8 @@ class ProgramCompiler {
     if (!varIndex(f1, 1, 0x7fff) || !varIndex(f1, 0, -1) || !varIndex(f2, 0, -1)) return;
     if (!fastPred(f1, cseq.f1) || !fastPred(f2, cseq.f2)) return;
     cseq.M = (int32_t)mx;
+    cseq.every = every ? 1 : 0;
+    cseq.minc = (int32_t)mn;
     cseq.ok = 1;
   }
 };

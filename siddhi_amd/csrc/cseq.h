@@ -77,7 +77,8 @@ __device__ __forceinline__ void cs_set_ts(CsRec12& r, int64_t t, int64_t base, b
 struct CseqDev {
   SwPred f1, f2;     // f1: e1 slot = the arriving event; f2: e1 slot = e1[last], e2 slot = the arriving event
   int32_t M, vtag, nk, cur;
-  int32_t ch32, pad0;  // SHP_LAYOUT_CHAIN32: k_cs3's emit writes one word per match (cseq_own.h)
+  int32_t ch32;       // SHP_LAYOUT_CHAIN32: k_cs3's emit writes one word per match (cseq_own.h)
+  int32_t mode;       // CS_EVERY1 .. CS_ONCEN (cs_tables)
   uint8_t* len[2];   // nk: L
   uint32_t* prev[2]; // nk: the previous event's value bits
   uint8_t* pnull[2]; // nk: ... and whether it was null
@@ -158,11 +159,41 @@ __device__ __forceinline__ uint64_t cs_comp(uint64_t g, uint64_t f) {  // g afte
   for (int i = 0; i <= CSEQ_MAXM; i++) h |= (uint64_t)cs_at(g, cs_at(f, i)) << (4 * i);
   return h;
 }
-// T10: f1(x) without f2: 0 -> 1, L -> L + 1 (0 < L < M), M -> 1; T11: f1(x) and f2: 0 -> 1, M -> 1, else 0
-__device__ __forceinline__ void cs_tables(int M, uint64_t& t10, uint64_t& t11) {
-  t10 = 1ull | (1ull << (4 * M));
-  t11 = 1ull | (1ull << (4 * M));
-  for (int i = 1; i < M; i++) t10 |= (uint64_t)(i + 1) << (4 * i);
+// The shape's modes (CseqShape: `every` and min of e1's <min:M>), and per mode the tables T0
+// (not f1(x)), T10 (f1(x) without f2), T11 (f1(x) and f2) on L in 0..M+1 (tests/test_cseq.py checks
+// the rule against the oracle for every <min:M>, M <= 8, with and without `every`):
+//   0 every, min 1   T0: -> 0; T10: 0 -> 1, L -> L + 1 (0 < L < M), M -> 1; T11: 0 -> 1, M -> 1, else 0
+//   1 no every, min 1  (D = M + 1: the start state is armed once, CountPreStateProcessor.init
+//                    :178-194 / resetState :288-305) T0: -> D; T10: 0 -> 1, L -> L + 1, M -> D;
+//                    T11: 0 -> 1, L -> D; D -> D
+//   2 every, min >= 2 / 3 no every, min >= 2: a chain never passes 1 (it reaches e1's new-and-every
+//                    list only from min on, and the sequence's per-event reset clears the pending
+//                    one) -- nothing is ever emitted; T* -> 0 (every re-arms) / D
+// A match closes at an event with f2 when L before it is in 1..M (modes 0, 1).
+constexpr int CS_EVERY1 = 0, CS_ONCE1 = 1, CS_EVERYN = 2, CS_ONCEN = 3;
+__device__ __forceinline__ void cs_tables(int M, int mode, uint64_t& t0, uint64_t& t10, uint64_t& t11) {
+  const uint64_t D = (uint64_t)M + 1u;
+  t0 = t10 = t11 = 0;
+  for (int i = 0; i <= CSEQ_MAXM; i++) {
+    uint64_t a, b, z;
+    if (mode == CS_EVERY1) {
+      z = 0;
+      a = (i == 0 || i >= M) ? 1u : (uint64_t)(i + 1);
+      b = (i == 0 || i >= M) ? 1u : 0u;
+    } else if (mode == CS_ONCE1) {
+      z = D;
+      a = i == 0 ? 1u : (i < M ? (uint64_t)(i + 1) : D);
+      b = i == 0 ? 1u : D;
+    } else {
+      z = a = b = mode == CS_EVERYN ? 0u : D;
+    }
+    t0 |= z << (4 * i);
+    t10 |= a << (4 * i);
+    t11 |= b << (4 * i);
+  }
+}
+__device__ __forceinline__ bool cs_emits(int mode, uint32_t Lb, int M) {
+  return mode <= CS_ONCE1 && Lb >= 1u && Lb <= (uint32_t)M;
 }
 
 // the first key-run start at or after position j of the sorted keys (n if none): a 64-ary search
@@ -223,8 +254,8 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
   const int64_t S = ws[wv], E = ws[wv + 1];
   const bool vnull = C.vtag == T_NULL, vflt = C.vtag == T_FLOAT;
   const int64_t tbase = B.ts[0];  // the narrow records' ts base (k_cs_pack)
-  uint64_t t10, t11;
-  cs_tables(M, t10, t11);
+  uint64_t t0, t10, t11;
+  cs_tables(M, C.mode, t0, t10, t11);
   // carried from the previous 64 events (lane 63's): L after it, its value, its run's start
   uint32_t cL = 0, cpv = 0;
   bool cpn = true;
@@ -273,7 +304,7 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
     sw_conv(pv, vflt, pf, pi);
     const bool a = v && sw_pred<NT1>(C.f1, xf, xi, xn, 0.0, 0.0, true);
     const bool b = v && sw_pred<NT2>(C.f2, pf, pi, pn, xf, xi, xn);
-    const uint64_t F = a ? (b ? t11 : t10) : 0ull;
+    const uint64_t F = a ? (b ? t11 : t10) : t0;
     // seeded elements: a run start composes F with its stored L, lane 0 with the carried L
     const bool seeded = head || lane == 0;
     const uint32_t Lseed = head ? L0 : cL;
@@ -290,7 +321,7 @@ __global__ __launch_bounds__(256) void k_cs2(CseqDev C, BatchView B, MatchOut O,
     uint32_t Lb = __shfl_up(La, 1, 64);  // L before it
     if (lane == 0) Lb = cL;
     if (head) Lb = L0;
-    const bool em = v && Lb > 0 && b;
+    const bool em = v && cs_emits(C.mode, Lb, M) && b;
     const uint32_t rfs = em ? Lb + 1u : 0u;
     // this event's run start (for the chain refs and the history): the latest head at or before it
     int64_t rs = head ? j : -1;
@@ -415,8 +446,8 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
   const int64_t S = ws[wv], E = ws[wv + 1];
   const bool vnull = C.vtag == T_NULL, vflt = C.vtag == T_FLOAT;
   const int64_t tbase = B.ts[0];  // the narrow records' ts base (k_cs_pack)
-  uint64_t t10, t11;
-  cs_tables(M, t10, t11);
+  uint64_t t0, t10, t11;
+  cs_tables(M, C.mode, t0, t10, t11);
   uint64_t ident = 0;
 #pragma unroll
   for (int i = 0; i <= CSEQ_MAXM; i++) ident |= (uint64_t)i << (4 * i);
@@ -482,7 +513,7 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
       sw_conv(px, vflt, pf, pi);
       const bool a = v && sw_pred<NT1>(C.f1, xf, xi, xn, 0.0, 0.0, true);
       const bool b = v && sw_pred<NT2>(C.f2, pf, pi, pxn, xf, xi, xn);
-      const uint64_t F = a ? (b ? t11 : t10) : 0ull;
+      const uint64_t F = a ? (b ? t11 : t10) : t0;
       hb |= (head ? 1u : 0u) << q;
       ab |= (a ? 1u : 0u) << q;
       bb |= (b ? 1u : 0u) << q;
@@ -529,8 +560,8 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
       const bool head = (hb >> q) & 1u;
       const uint32_t Lb = head ? (uint32_t)(L0q >> (4 * q)) & 15u : L;
       const bool a = (ab >> q) & 1u, b = (bb >> q) & 1u, v = (vb >> q) & 1u;
-      L = cs_at(a ? (b ? t11 : t10) : 0ull, Lb);
-      const bool em = v && Lb > 0 && b;
+      L = cs_at(a ? (b ? t11 : t10) : t0, Lb);
+      const bool em = v && cs_emits(C.mode, Lb, M) && b;
       lm += em ? 1u : 0u;
       lr += em ? Lb + 1u : 0u;
       lbw |= (Cs3W)Lb << (4 * q);
@@ -581,7 +612,7 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
         const int64_t rs = hm ? p0 + (int64_t)src * CS3_Q + (31 - __clz(hm)) : S + RS;
         const uint32_t Lb = (uint32_t)(LbW >> (4 * q)) & 15u;
         const bool em = (emw >> q) & 1u, a = (FW >> (3 * CS3_Q + q)) & 1u;
-        const uint32_t La = cs_at(a ? (em ? t11 : t10) : 0ull, Lb);  // (Lb = 0: T11 and T10 agree)
+        const uint32_t La = cs_at(a ? (em ? t11 : t10) : t0, Lb);  // (no emission: T11 and T10 agree)
         const uint32_t k = kl;
         const R rj = sv[j];
         if (em && C.ch32) {  // CHAIN32: e2's batch index | L << 28 (the chain is implied)
@@ -882,8 +913,11 @@ struct CseqState {
   int64_t mcap = 0;
 
   // owners and local keys for nk keys with M history slots: false when they do not fit
-  bool own_plan(int M, int32_t nk) {
-    if (M > CO_MAXM) return false;  // (k_co_run's 8-byte transition tables)
+  static int mode_of(const CseqShape& s) {
+    return s.every ? (s.minc <= 1 ? CS_EVERY1 : CS_EVERYN) : (s.minc <= 1 ? CS_ONCE1 : CS_ONCEN);
+  }
+  bool own_plan(int M, int mode, int32_t nk) {
+    if (M > CO_MAXM || (mode == CS_ONCE1 && M + 1 > CO_MAXM)) return false;  // (k_co_run's 8-byte tables)
     const int per = 8 + 4 * M;  // value, L / null / ring head / ring fill, the ring
     int kmax = 1;
     while (kmax * 2 <= CO_KPO_MAX && kmax * 2 * per <= CO_KEY_LDS) kmax *= 2;
@@ -935,7 +969,7 @@ struct CseqState {
       (void)rocprim::exclusive_scan(nullptr, b4, rocprim::make_transform_iterator((const uint32_t*)ch, ChRefs{}),
                                     (int64_t*)nullptr, (int64_t)0, (size_t)mcap, rocprim::plus<int64_t>(), st);
       tmp_bytes = std::max(tmp_bytes, b4);
-      own = getenv("SHP_CO_OFF") == nullptr && own_plan(s.M, max_keys);
+      own = getenv("SHP_CO_OFF") == nullptr && own_plan(s.M, mode_of(s), max_keys);
       if (own) {
         const int64_t nst_max = (cap + CO_STLEN - 1) / CO_STLEN;
         const int64_t nc = (int64_t)P.nown * nst_max + 1;
@@ -961,6 +995,7 @@ struct CseqState {
     if (!SweepState::lower(s.f1, (int8_t)D.vtag, D.f1) || !SweepState::lower(s.f2, (int8_t)D.vtag, D.f2))
       throw std::runtime_error("count-sequence: predicate not lowerable");
     D.M = s.M;
+    D.mode = mode_of(s);
     D.nk = max_keys;
     D.cur = 0;
     for (int c = 0; c < 2; c++) {
@@ -982,6 +1017,7 @@ struct CseqState {
   // can the lowered predicates run here (f1 and f2 each at most two terms)?
   static bool shape_ok(const DevProg& P, const CseqShape& s) {
     if (!s.ok) return false;
+    if (!s.every && s.minc <= 1 && s.M + 1 > CSEQ_MAXM) return false;  // (the dead state: nibble tables 0..8)
     if (P.ncol == 1 && !(P.colTag[0] == T_INT || P.colTag[0] == T_FLOAT || P.colTag[0] == T_STR)) return false;
     SwPred a, b;
     const int8_t vt = P.ncol == 1 ? P.colTag[0] : T_NULL;

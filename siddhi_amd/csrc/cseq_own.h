@@ -227,9 +227,9 @@ __device__ __forceinline__ uint32_t co_block_scan(uint32_t v, uint32_t* sc, uint
 }
 
 // Transition tables as 8 bytes (byte i = L after, from L = i), composed with two byte permutes.
-// Every table the automaton makes maps L = 0 and L = M alike (T0, T10, T11 do, so their
-// compositions do), so inputs 0..7 cover M <= 7 and every output value (<= M) is a valid selector
-// of the next composition; the owner path takes M <= 7 (M = 8 runs on the sorted records).
+// The tables (cs_tables' modes) on L in 0..7: a state past M is either M (every: T* map it like 0)
+// or the dead state M + 1 (no every), so inputs 0..7 cover M <= 7 (M <= 6 without every) and every
+// output value is a valid selector of the next composition; larger M run on the sorted records.
 __device__ __forceinline__ uint64_t co_const(uint32_t c) { return 0x0101010101010101ull * (uint64_t)c; }
 __device__ __forceinline__ uint32_t co_at(uint64_t f, uint32_t i) { return (uint32_t)(f >> (8 * i)) & 0xffu; }
 __device__ __forceinline__ uint64_t co_comp(uint64_t g, uint64_t f) {  // g after f
@@ -238,13 +238,14 @@ __device__ __forceinline__ uint64_t co_comp(uint64_t g, uint64_t f) {  // g afte
   const uint32_t hi = __builtin_amdgcn_perm(gh, gl, (uint32_t)(f >> 32));
   return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ void co_tables(int M, uint64_t& t10, uint64_t& t11) {
-  t10 = t11 = 0;
+__device__ __forceinline__ void co_tables(int M, int mode, uint64_t& t0, uint64_t& t10, uint64_t& t11) {
+  uint64_t n0, n10, n11;  // cs_tables' nibbles, widened to bytes
+  cs_tables(M, mode, n0, n10, n11);
+  t0 = t10 = t11 = 0;
   for (int i = 0; i < 8; i++) {
-    const uint64_t a = (i == 0 || i >= M) ? 1u : (uint64_t)(i + 1);  // T10: 0 -> 1, L -> L + 1, M -> 1
-    const uint64_t b = (i == 0 || i == M) ? 1u : 0u;                   // T11: 0 -> 1, M -> 1, else 0
-    t10 |= a << (8 * i);
-    t11 |= b << (8 * i);
+    t0 |= ((n0 >> (4 * i)) & 15u) << (8 * i);
+    t10 |= ((n10 >> (4 * i)) & 15u) << (8 * i);
+    t11 |= ((n11 >> (4 * i)) & 15u) << (8 * i);
   }
 }
 constexpr uint64_t CO_IDENT = 0x0706050403020100ull;
@@ -288,8 +289,8 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   const int rd = C.cur, wr = C.cur ^ 1;
   const uint32_t nk = (uint32_t)C.nk;
   const bool vnull = C.vtag == T_NULL, vflt = C.vtag == T_FLOAT;
-  uint64_t t10, t11;
-  co_tables(M, t10, t11);
+  uint64_t t0, t10, t11;
+  co_tables(M, C.mode, t0, t10, t11);
   const uint64_t ident = CO_IDENT;
   // the owner's keys' state (the previous push)
   for (int lk = tid; lk < kpo; lk += CO_THREADS) {
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       sw_conv(px, vflt, pf, pi);
       const bool a = (cl & CO_F1) != 0;
       const bool b = sw_pred<NT2>(C.f2, pf, pi, pxn, xf, xi, xn);
-      const uint64_t F = a ? (b ? t11 : t10) : 0ull;
+      const uint64_t F = a ? (b ? t11 : t10) : t0;
       hb |= (head ? 1u : 0u) << q;
       ab |= (a ? 1u : 0u) << q;
       bb |= (b ? 1u : 0u) << q;
@@ -505,8 +506,8 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       const bool head = (hb >> q) & 1u;
       const uint32_t Lb = head ? (L0q >> (4 * q)) & 15u : L;
       const bool a = (ab >> q) & 1u, b = (bb >> q) & 1u;
-      L = co_at(a ? (b ? t11 : t10) : 0ull, Lb);
-      const bool em = Lb > 0 && b;
+      L = co_at(a ? (b ? t11 : t10) : t0, Lb);
+      const bool em = cs_emits(C.mode, Lb, M) && b;
       lm += em ? 1u : 0u;
       lbw |= Lb << (4 * q);
       law |= L << (4 * q);

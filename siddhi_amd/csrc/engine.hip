@@ -41,6 +41,9 @@ using namespace shp;
 struct DevError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+struct OutputError : std::runtime_error {  // a capacity found short after the push (SHP_ERR_OUTPUT)
+  using std::runtime_error::runtime_error;
+};
 
 // ---------------------------------------------------------------- kernels
 __global__ void k_iota(uint32_t* v, int64_t n) {
@@ -364,7 +367,9 @@ struct shp_engine {
     if (fast && want_sweep && SweepState::shape_ok(comp.P, comp.fast) &&
         SweepState::build_map(cfg.max_keys, nown, kmap))
       fast = 2;
-    if (!fast && cfg.force_general != 1 && CseqState::shape_ok(comp.P, comp.cseq)) fast = 3;
+    if (!fast && cfg.force_general != 1 && CseqState::shape_ok(comp.P, comp.cseq) &&
+        !(cseq_v1 && CseqState::mode_of(comp.cseq) != CS_EVERY1))  // (the round-2 kernels: every, min 1)
+      fast = 3;
     // the logical-absent automaton (labs.h): exact for any timestamp order, the default for its shape
     if (!fast && cfg.force_general == 4 && !LabsState::shape_ok(comp.P, comp.labs))
       throw CompileError(-2, "force_general 4: the query is not `every (x=X and y=Y) -> not Z for T` in playback");
@@ -1076,7 +1081,7 @@ struct shp_engine {
         o += firstKey ? "\"" : ",\"";
         firstKey = false;
         jnum(o, k);
-        const int L = len[k];
+        const int L = len[k] > C.M ? 0 : len[k];  // (M + 1: the once-armed start has been used)
         o += "\":{\"e1\":{\"Count\":";
         jnum(o, L);
         o += ",\"PendingStateEventList\":[{\"ts\":";
@@ -1294,7 +1299,7 @@ struct shp_engine {
     HIP_OK(hipStreamSynchronize(stream));
     if (herr & SWE_BOUND) throw DevError("internal: a match pair names an event outside its push (SWE_BOUND)");
     if (herr & E_OUT)  // (unreachable: rcap holds M + 1 refs per match for CHAIN32 engines)
-      throw std::runtime_error("SHP_ERR_OUTPUT: CHAIN32 expansion beyond the ref capacity (raise max_matches)");
+      throw OutputError("CHAIN32 expansion beyond the ref capacity (raise max_matches)");
     expanded = true;
   }
 
@@ -1531,6 +1536,9 @@ static int guarded(shp_engine* e, const std::function<int()>& f) {
   } catch (DevError& de) {
     e->err = de.what();
     return SHP_ERR_DEVICE;
+  } catch (OutputError& oe) {
+    e->err = oe.what();
+    return SHP_ERR_OUTPUT;
   } catch (std::exception& ex) {
     e->err = ex.what();
     return SHP_ERR_ARG;

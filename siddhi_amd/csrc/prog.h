@@ -135,7 +135,9 @@ struct FastShape {
 constexpr int CSEQ_MAXM = 8;
 struct CseqShape {
   int32_t ok;
-  int32_t M;  // max count (1..CSEQ_MAXM)
+  int32_t M;      // max count (1..CSEQ_MAXM)
+  int32_t every;  // `every e1=...` (else the start state is armed once)
+  int32_t minc;   // min count of e1's <min:M> (1..M)
   FPred f1, f2;
 };
 

@@ -345,6 +345,9 @@ __device__ __forceinline__ void sw_conv(uint32_t v, bool isfloat, double& f, dou
 // rounds 1-3 hashed the id onto the owner and looked the local key up in a table, a byte load per
 // event that the 100k-key C5 took from L2).  Dictionary ids are dense (shp_dict, and k / N on rank
 // k % N of a key-sharded group), so every owner gets max_keys / nown keys, one more at most.
+// shp_push_batch_device callers that bring their own ids must keep them dense for speed: strided
+// ids (all even, multiples of nown) put every event on a few owners, whose solves then run
+// serially and overflow to the spill path -- results stay exact, throughput drops.
 __host__ __device__ __forceinline__ uint32_t sw_owner(uint32_t k, int bits) {
   return bits == 0 ? 0u : (k & ((1u << bits) - 1u));
 }

@@ -5,7 +5,8 @@
   its own list (CountPostStateProcessor.java:49-57) and the sequence receiver resets the pending
   lists on every event (StreamPreStateProcessor.resetState :288-305 via
   SequenceMultiProcessStreamReceiver.java:45-50), so `<2:5>` never reaches 2 (SURVEY §0 finding 3).
-  The general NFA lanes (HBM arena, one lane per key) must reproduce that at 1M keys.
+  The count-sequence automaton (cseq.h, its "once, min >= 2" tables) and the general NFA lanes
+  (HBM arena, one lane per key) must both reproduce that at 1M keys.
 * C3' -- `every e1=S[v>20]<1:5>` -- at 1M keys on the general lanes (11 KB of HBM arena per key,
   two arenas) and on the count-sequence automaton (k_cseq), per key bit-exact against the oracle,
   over split pushes, with a few hot keys carrying long rising runs (chains that fill to max and
@@ -30,12 +31,13 @@ def _hip(force_general, batch):
     return make
 
 
-def test_c3_as_specified_at_1m_keys_emits_nothing():
+@pytest.mark.parametrize("force_general", [1, 0], ids=["lanes", "cseq"])
+def test_c3_as_specified_at_1m_keys_emits_nothing(force_general):
     cq = program_for(3)
     g = small_stream(3, 3_000_000, KEYS)
     want = run(OracleEngine(cq.program_json(), 0), cq, g)
-    eng = _hip(0, 1 << 20)(cq.program_json(), 0)
-    assert eng.path == 0  # no specialised automaton covers a min-2 sequence: the general lanes
+    eng = _hip(force_general, 1 << 20)(cq.program_json(), 0)
+    assert eng.path == (0 if force_general == 1 else 3)
     got = run(eng, cq, g, 1_000_003)
     assert len(want["key"]) == 0
     assert len(got["key"]) == 0

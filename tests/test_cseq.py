@@ -1,4 +1,4 @@
-"""The count-sequence path (siddhi_amd/csrc/cseq.h): `every e1=S[f1]<1:M>, e2=S[f2]` (C3').
+"""The count-sequence path (siddhi_amd/csrc/cseq.h): `[every] e1=S[f1]<min:M>, e2=S[f2]` (C3', C3).
 
 CPU: the per-key automaton cseq.h implements, restated here in Python, against the oracle's
 object-level restatement of CountPreStateProcessor / CountPostStateProcessor /
@@ -20,9 +20,10 @@ OPS = {"<": operator.lt, "<=": operator.le, ">": operator.gt, ">=": operator.ge,
        "!=": operator.ne}
 
 
-def _app(M, op, typ="float", f1="v > 20"):
+def _app(M, op, typ="float", f1="v > 20", every=True, mn=1):
+    ev = "every " if every else ""
     return (f"define stream S (k string, v {typ}); partition with (k of S) begin @info(name='q') "
-            f"from every e1=S[{f1}]<1:{M}>, e2=S[v {op} e1[last].v] select e1[0].v as a, e2.v as c "
+            f"from {ev}e1=S[{f1}]<{mn}:{M}>, e2=S[v {op} e1[last].v] select e1[0].v as a, e2.v as c "
             f"insert into Out; end;")
 
 
@@ -62,6 +63,44 @@ def automaton(M, op, ts, key, v, f1=lambda x: x > 20, nul=None):
     return out
 
 
+def tables(M, every, mn):
+    """cseq.h cs_tables: T0 (not f1), T10 (f1 without f2), T11 (f1 and f2) on L in 0..M+1, and
+    whether the shape emits.  D = M + 1 is the dead state of a start armed once (no `every`:
+    CountPreStateProcessor.init / resetState arm it once); min >= 2 never emits, since a chain
+    reaches e1's new-and-every list only at min, and the sequence resets the pending one on the
+    key's next event (CountPreStateProcessor.java:288-305, StreamPreStateProcessor.java:360)."""
+    D = M + 1
+    n = M + 2
+    if mn >= 2:
+        c = 0 if every else D
+        return [c] * n, [c] * n, [c] * n, False
+    if every:
+        return [0] * n, [1] + [i + 1 for i in range(1, M)] + [1, 1], [1] + [0] * (M - 1) + [1, 1], True
+    return [D] * n, [1] + [i + 1 for i in range(1, M)] + [D, D], [1] + [D] * M + [D], True
+
+
+def table_automaton(M, op, every, mn, ts, key, v, f1=lambda x: x > 20, nul=None):
+    """The table form the kernels run (cs_tables / co_tables): per key, L before the event and the
+    key's last M events; a match closes when 1 <= L <= M and f2 holds."""
+    cmp = OPS[op]
+    t0, t10, t11, emit_on = tables(M, every, mn)
+    out, L, hist = {}, {}, {}
+    for i in range(len(ts)):
+        k = int(key[i])
+        Lb = L.get(k, 0)
+        h = hist.setdefault(k, [])
+        xn = nul is not None and nul[i]
+        a = (not xn) and f1(v[i])
+        b = bool(h) and not xn and not (nul is not None and nul[h[-1]]) and cmp(v[i], v[h[-1]])
+        if emit_on and 1 <= Lb <= M and b:
+            out.setdefault(k, []).append((int(ts[i]), 0, i, (tuple(h[len(h) - Lb:]), (i,))))
+        L[k] = (t11 if b else t10)[Lb] if a else t0[Lb]
+        h.append(i)
+        if len(h) > M:
+            h.pop(0)
+    return out
+
+
 def _stream(rng, n, keys, lo=15, hi=30, nan=0.01):
     ts = np.cumsum(rng.integers(0, 3, n)).astype(np.int64) + 1000
     key = rng.integers(0, keys, n).astype(np.int32)
@@ -80,6 +119,39 @@ def test_automaton_matches_oracle(M, op):
     got = automaton(M, op, ts, key, v)
     assert compare(want, got) is None, compare(want, got)
     assert sum(len(x) for x in want.values()) > 200
+
+
+@pytest.mark.parametrize("every", [True, False], ids=["every", "once"])
+@pytest.mark.parametrize("M", range(1, 9))
+def test_table_automaton_matches_oracle_every_min_max(every, M):
+    """Every <min:M> with min <= M <= 8, with and without `every`, against the oracle: the rule
+    cs_tables encodes (C3 is `e1=S[v > 20]<2:5>` without every)."""
+    ops = ["<", ">=", "!="]
+    for mn in range(1, M + 1):
+        op = ops[(M + mn) % 3]
+        rng = np.random.default_rng(M * 100 + mn * 7 + every)
+        ts, key, v = _stream(rng, 4_000, 5)
+        cq = _cq(_app(M, op, every=every, mn=mn))
+        want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 1_999)
+        got = table_automaton(M, op, every, mn, ts, key, v)
+        assert compare(want, got) is None, (mn, op, compare(want, got))
+        if mn == 1:
+            assert sum(len(x) for x in want.values()) >= (50 if every else 1)
+    if every:  # the every / min 1 tables agree with the list form above
+        rng = np.random.default_rng(3)
+        ts, key, v = _stream(rng, 4_000, 7)
+        assert compare(automaton(M, "<", ts, key, v), table_automaton(M, "<", True, 1, ts, key, v)) is None
+
+
+def test_table_automaton_with_nulls_once():
+    rng = np.random.default_rng(19)
+    ts, key, v = _stream(rng, 12_000, 400, nan=0.0)
+    nul = (rng.random(len(ts)) < 0.05).astype(np.uint8)
+    cq = _cq(_app(4, "<", every=False))
+    want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 3_001, nul)
+    got = table_automaton(4, "<", False, 1, ts, key, v, nul=nul)
+    assert compare(want, got) is None, compare(want, got)
+    assert sum(len(x) for x in want.values()) > 100
 
 
 def test_automaton_matches_oracle_c3b_stream():
@@ -137,6 +209,27 @@ def test_cseq_shapes_vs_oracle(M, op, typ):
     got = _push(eng, ts, key, v, 40_009)
     assert compare(want, got) is None, compare(want, got)
     assert sum(len(x) for x in want.values()) > 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("every,mn,M,op,layout", [
+    (False, 1, 4, "<", 0), (False, 1, 6, ">=", 4), (False, 1, 7, "<", 4), (False, 1, 8, "!=", 0),
+    (False, 2, 5, "<", 0), (False, 2, 5, "<", 4), (True, 2, 5, "<", 4), (True, 3, 8, ">=", 0),
+    (True, 1, 3, "!=", 4)])
+def test_cseq_every_min_max_vs_oracle(every, mn, M, op, layout):
+    """The count sequence's modes (cs_tables) on path 3, FULL rows and CHAIN32 words (owner path
+    while M + 1 <= 7 without every, the sorted records past that)."""
+    from siddhi_amd.native import HipEngine
+    rng = np.random.default_rng(M * 13 + mn)
+    ts, key, v = _stream(rng, 160_000, 4_000)
+    cq = _cq(_app(M, op, every=every, mn=mn))
+    want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 40_009)
+    eng = HipEngine(cq.program_json(), 0, max_keys=4_000, max_batch=1 << 16, match_layout=layout)
+    assert eng.path == 3
+    got = _push(eng, ts, key, v, 40_009)
+    assert compare(want, got) is None, compare(want, got)
+    if mn == 1:
+        assert sum(len(x) for x in want.values()) > (1000 if every else 500)
 
 
 @pytest.mark.gpu

@@ -16,8 +16,9 @@ for c in ${CONFIGS:-c3b c5 c4 c3 c1}; do
     c3b) run c3b 400 --config 3b ;;
     c5) run c5 400 --config 5 ;;
     c4) run c4 500 --config 4 ;;
+    c4d) run c4d 500 --config 4 --disorder 0.01 --no-cpu-baseline ;;
     c4lanes) run c4lanes 700 --config 4 --path general --steps 2 --warmup 1 --latency-batches 0 ;;
-    c3) run c3 600 --config 3 --steps 3 --warmup 1 --latency-batches 0 ;;
+    c3) run c3 400 --config 3 ;;
     c1) run c1 500 --config 1 --steps 3 --warmup 1 ;;
   esac || exit 1
 done
