@@ -129,7 +129,7 @@ def main():
     force = {"auto": 0, "general": 1, "scan": 2, "labs": 4}[a.path]
     sweep = force == 0 and _sweep_shape(cq, local, K_local)
     layout = ("agg" if "aggregate" in cq.program else a.pairs_layout) if sweep else "full"
-    if cfg_id in ("3", "3b") and force == 0:  # the count-sequence path takes C3 and C3' by default
+    if cfg_id in (3, "3b") and force == 0:  # the count-sequence path takes C3 and C3' by default
         layout = a.cseq_layout
     mlay = {"agg": native.LAYOUT_AGG, "pairs": native.LAYOUT_PAIRS, "pairs32": native.LAYOUT_PAIRS32,
             "chain32": native.LAYOUT_CHAIN32, "full": native.LAYOUT_FULL}[layout]

@@ -150,13 +150,15 @@ __global__ void k_cs_pack(const int64_t* __restrict__ ts, const int32_t* __restr
   if (e) atomicOr(err, e);
 }
 
-// transition tables: entry i (4 bits at 4 i) = L after the event from L = i
-__device__ __forceinline__ uint64_t cs_tab_const(uint32_t c) { return 0x111111111ull * (uint64_t)c; }
+// transition tables: entry i (4 bits at 4 i) = L after the event from L = i, for L in 0..CS_NL-1
+// (0..M, and M + 1 the dead state of a once-armed start)
+constexpr int CS_NL = CSEQ_MAXM + 2;
+__device__ __forceinline__ uint64_t cs_tab_const(uint32_t c) { return 0x1111111111ull * (uint64_t)c; }
 __device__ __forceinline__ uint32_t cs_at(uint64_t f, uint32_t i) { return (uint32_t)(f >> (4 * i)) & 15u; }
 __device__ __forceinline__ uint64_t cs_comp(uint64_t g, uint64_t f) {  // g after f
   uint64_t h = 0;
 #pragma unroll
-  for (int i = 0; i <= CSEQ_MAXM; i++) h |= (uint64_t)cs_at(g, cs_at(f, i)) << (4 * i);
+  for (int i = 0; i < CS_NL; i++) h |= (uint64_t)cs_at(g, cs_at(f, i)) << (4 * i);
   return h;
 }
 // The shape's modes (CseqShape: `every` and min of e1's <min:M>), and per mode the tables T0
@@ -174,7 +176,7 @@ constexpr int CS_EVERY1 = 0, CS_ONCE1 = 1, CS_EVERYN = 2, CS_ONCEN = 3;
 __device__ __forceinline__ void cs_tables(int M, int mode, uint64_t& t0, uint64_t& t10, uint64_t& t11) {
   const uint64_t D = (uint64_t)M + 1u;
   t0 = t10 = t11 = 0;
-  for (int i = 0; i <= CSEQ_MAXM; i++) {
+  for (int i = 0; i < CS_NL; i++) {
     uint64_t a, b, z;
     if (mode == CS_EVERY1) {
       z = 0;
@@ -450,7 +452,7 @@ __global__ __launch_bounds__(256) void k_cs3(CseqDev C, BatchView B, MatchOut O,
   cs_tables(M, C.mode, t0, t10, t11);
   uint64_t ident = 0;
 #pragma unroll
-  for (int i = 0; i <= CSEQ_MAXM; i++) ident |= (uint64_t)i << (4 * i);
+  for (int i = 0; i < CS_NL; i++) ident |= (uint64_t)i << (4 * i);
   // carried from the previous tile (its last event): L after it, its value and null flag, its run start
   uint32_t cL = 0, cpv = 0;
   bool cpn = true;
@@ -1017,7 +1019,6 @@ struct CseqState {
   // can the lowered predicates run here (f1 and f2 each at most two terms)?
   static bool shape_ok(const DevProg& P, const CseqShape& s) {
     if (!s.ok) return false;
-    if (!s.every && s.minc <= 1 && s.M + 1 > CSEQ_MAXM) return false;  // (the dead state: nibble tables 0..8)
     if (P.ncol == 1 && !(P.colTag[0] == T_INT || P.colTag[0] == T_FLOAT || P.colTag[0] == T_STR)) return false;
     SwPred a, b;
     const int8_t vt = P.ncol == 1 ? P.colTag[0] : T_NULL;
