@@ -178,7 +178,8 @@ def main():
     torch.cuda.synchronize()
     ncol = max(1, len(cq.columns))
 
-    def push(ts, key, price, stream):
+    def push(ts, key, price, stream, e=None):
+        e = e or eng
         n = ts.numel()
         # one pointer per program column (cq.columns: (stream, attr, type)); every stream's
         # predicate attribute is the synthetic price column
@@ -186,9 +187,9 @@ def main():
         b = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), stream.data_ptr() if stream is not None else None,
                             ctypes.cast(colp, ctypes.c_void_p), None)
         mt = native.ShpMatches()
-        rc = L.shp_push_batch_device(eng.h, ctypes.byref(b), ctypes.byref(mt))
+        rc = L.shp_push_batch_device(e.h, ctypes.byref(b), ctypes.byref(mt))
         if rc != 0:
-            raise native.ShpError(rc, L.shp_last_error(eng.h).decode())
+            raise native.ShpError(rc, L.shp_last_error(e.h).decode())
         return n, mt.m
 
     def slices(i):
@@ -259,7 +260,17 @@ def main():
 
     expanded = None
     if G == 1 and layout in ("chain32", "pairs32") and not a.no_expanded:
-        expanded = expanded_rate(eng, L, native, [gen(steps + s, 0) for s in range(1 + a.steps)], push, layout)
+        fresh = [gen(steps + s, 0) for s in range(1 + a.steps)]
+        if layout == "chain32":  # the same path with FULL rows written by its run kernel (k_co_run)
+            full = native.HipEngine(cq.program_json(), 0, max_keys=K_local, max_batch=cap, max_matches=cap,
+                                    device=local, force_general=force, match_layout=native.LAYOUT_FULL)
+            try:
+                expanded = full_rate(full, fresh, push)
+            finally:
+                full.close()
+        else:
+            expanded = expanded_rate(eng, L, native, fresh, push, layout)
+        del fresh
 
     latency = None
     if rank == 0 and G == 1 and a.latency_batches > 0 and layout != "full":
@@ -392,6 +403,22 @@ def _path_desc(eng, layout):
 def native_stat(eng, which):
     from siddhi_amd import native
     return native.lib().shp_engine_stat(eng.h, which.encode())
+
+
+def full_rate(full, bats, push):
+    """The count sequence with FULL rows (self-contained: e1's chain refs written by k_co_run) on a
+    second engine over fresh batches: events/s and ms per step, beside the CHAIN32 headline."""
+    import torch
+    push(*bats[0], e=full)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev = 0
+    for b in bats[1:]:
+        ev += push(*b, e=full)[0]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k = len(bats) - 1
+    return {"value": ev / el, "ms_per_step": el / k * 1e3, "layout": "full (rows and refs written by the run kernel)"}
 
 
 def expanded_rate(eng, L, native, bats, push, layout):

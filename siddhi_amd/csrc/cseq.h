@@ -170,7 +170,10 @@ __device__ __forceinline__ uint64_t cs_comp(uint64_t g, uint64_t f) {  // g afte
 //                    T11: 0 -> 1, L -> D; D -> D
 //   2 every, min >= 2 / 3 no every, min >= 2: a chain never passes 1 (it reaches e1's new-and-every
 //                    list only from min on, and the sequence's per-event reset clears the pending
-//                    one) -- nothing is ever emitted; T* -> 0 (every re-arms) / D
+//                    one) -- nothing is ever emitted.  L = 1 is the count-1 partial of the key's last
+//                    event, alive until the key's next event: every: T10 = T11 -> 1, T0 -> 0; no
+//                    every: T10 = T11: 0 -> 1, else D; T0 -> D (tests/test_cseq.py checks the live
+//                    partials against the oracle's oldest live event)
 // A match closes at an event with f2 when L before it is in 1..M (modes 0, 1).
 constexpr int CS_EVERY1 = 0, CS_ONCE1 = 1, CS_EVERYN = 2, CS_ONCEN = 3;
 __device__ __forceinline__ void cs_tables(int M, int mode, uint64_t& t0, uint64_t& t10, uint64_t& t11) {
@@ -186,8 +189,12 @@ __device__ __forceinline__ void cs_tables(int M, int mode, uint64_t& t0, uint64_
       z = D;
       a = i == 0 ? 1u : (i < M ? (uint64_t)(i + 1) : D);
       b = i == 0 ? 1u : D;
+    } else if (mode == CS_EVERYN) {
+      z = 0;
+      a = b = 1;
     } else {
-      z = a = b = mode == CS_EVERYN ? 0u : D;
+      z = D;
+      a = b = i == 0 ? 1u : D;
     }
     t0 |= z << (4 * i);
     t10 |= a << (4 * i);
@@ -971,7 +978,11 @@ struct CseqState {
       (void)rocprim::exclusive_scan(nullptr, b4, rocprim::make_transform_iterator((const uint32_t*)ch, ChRefs{}),
                                     (int64_t*)nullptr, (int64_t)0, (size_t)mcap, rocprim::plus<int64_t>(), st);
       tmp_bytes = std::max(tmp_bytes, b4);
-      own = getenv("SHP_CO_OFF") == nullptr && own_plan(s.M, mode_of(s), max_keys);
+    }
+    // the owner path takes CHAIN32 words and FULL rows alike (k_co_run); SHP_CO_OFF: the sorted records
+    own = getenv("SHP_CO_OFF") == nullptr && (chain32 || getenv("SHP_CO_FULL_OFF") == nullptr) &&
+          own_plan(s.M, mode_of(s), max_keys);
+    {
       if (own) {
         const int64_t nst_max = (cap + CO_STLEN - 1) / CO_STLEN;
         const int64_t nc = (int64_t)P.nown * nst_max + 1;
@@ -982,7 +993,9 @@ struct CseqState {
         (void)rocprim::exclusive_scan(nullptr, b5, P.cnt, P.off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), st);
         tmp_bytes = std::max(tmp_bytes, b5);
         const int dyn = (int)co_dyn_bytes(P.kpo, s.M);
-        const void* runs[3] = {(const void*)k_co_run<0>, (const void*)k_co_run<1>, (const void*)k_co_run<2>};
+        const void* runs[6] = {(const void*)k_co_run<0, false>, (const void*)k_co_run<1, false>,
+                               (const void*)k_co_run<2, false>, (const void*)k_co_run<0, true>,
+                               (const void*)k_co_run<1, true>,  (const void*)k_co_run<2, true>};
         for (const void* f : runs)
           if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, dyn) != hipSuccess)
             throw std::runtime_error("count-sequence owner path: LDS request refused");
@@ -1163,9 +1176,13 @@ struct CseqState {
     kt.mark("co_run", s);
     const size_t dyn = co_dyn_bytes(P.kpo, D.M);
     switch (D.f2.n) {
-      case 0: k_co_run<0><<<(unsigned)P.nown, CO_THREADS, dyn, s>>>(P, D, B, O, err); break;
-      case 1: k_co_run<1><<<(unsigned)P.nown, CO_THREADS, dyn, s>>>(P, D, B, O, err); break;
-      default: k_co_run<2><<<(unsigned)P.nown, CO_THREADS, dyn, s>>>(P, D, B, O, err); break;
+#define CO_RUN(N)                                                                           \
+  if (D.ch32) k_co_run<N, false><<<(unsigned)P.nown, CO_THREADS, dyn, s>>>(P, D, B, O, err); \
+  else k_co_run<N, true><<<(unsigned)P.nown, CO_THREADS, dyn, s>>>(P, D, B, O, err);
+      case 0: CO_RUN(0) break;
+      case 1: CO_RUN(1) break;
+      default: CO_RUN(2) break;
+#undef CO_RUN
     }
     kt.mark(nullptr, s);
   }

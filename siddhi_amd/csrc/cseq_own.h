@@ -260,6 +260,7 @@ struct CoSmem {
   int32_t wh[CO_WAVES];        // ... its latest run start
   uint32_t sc[CO_WAVES];
   uint32_t base;
+  unsigned long long fb[2];    // FULL rows: the chunk's first match and first ref
 };
 
 // dynamic LDS after CoSmem: wc[CO_WAVES][kpo + 1] (uint16, per-wave counts then cursors), then per
@@ -270,7 +271,9 @@ __host__ __device__ inline size_t co_dyn_bytes(int kpo, int M) {
 }
 
 // (<= 128 VGPRs: two 512-thread workgroups per CU, as their LDS allows)
-template <int NT2>
+// FR: FULL rows (else CHAIN32 words) -- a template parameter, so the words' variant keeps the wait
+// counters it had (the rows' gathers wait on their loads; tools/isa_check.py)
+template <int NT2, bool FR>
 __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_co_run(CoDev P, CseqDev C, BatchView B, MatchOut O, int* err) {
   __shared__ CoSmem S;
   extern __shared__ uint8_t co_key[];
@@ -499,7 +502,7 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     }
     const uint32_t Lin = co_at(ev, 0);
     // walk 2: L before each position, the closing ones
-    uint32_t L = Lin, lm = 0, lbw = 0, law = 0, emw = 0;
+    uint32_t L = Lin, lm = 0, lr = 0, lbw = 0, law = 0, emw = 0;
 #pragma unroll
     for (int q = 0; q < CO_PER; q++) {
       if (!((vb >> q) & 1u)) break;
@@ -509,22 +512,82 @@ __global__ __launch_bounds__(CO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       L = co_at(a ? (b ? t11 : t10) : t0, Lb);
       const bool em = cs_emits(C.mode, Lb, M) && b;
       lm += em ? 1u : 0u;
+      lr += em ? Lb + 1u : 0u;
       lbw |= Lb << (4 * q);
       law |= L << (4 * q);
       emw |= (em ? 1u : 0u) << q;
     }
     uint32_t tot;
-    const uint32_t mo = co_block_scan(lm, S.sc, tot);
-    if (tid == 0) {  // (+ a lane count that is always 0: keeps the atomic optimizer, which reads the
-                     // result back at once, off this one-lane add)
-      pres = tot ? atomicAdd(O.count + __builtin_amdgcn_mbcnt_lo(0u, 0u), (unsigned long long)tot) : 0ull;
-      ppend = true;
+    if constexpr (FR) {  // FULL rows: matches (low 16 bits: <= 2048 a chunk) and refs (high: <= 9 * 2048)
+      const uint32_t mr = co_block_scan(lm | (lr << 16), S.sc, tot);
+      if (tid == 0) {
+        const uint32_t tm = tot & 0xffffu, tr = tot >> 16;
+        S.fb[0] = tm ? atomicAdd(O.count, (unsigned long long)tm) : 0ull;
+        S.fb[1] = tr ? atomicAdd(O.count + 1, (unsigned long long)tr) : 0ull;
+      }
+      __syncthreads();
+      // e1's chain of each closing position: the key's Lb events before it -- in the chunk from its
+      // run start rs, before that from the ring of the key's events in earlier chunks, and before
+      // those from the history the push started from (copy rd).  Read before walk 3 moves the ring.
+      const int64_t mb = (int64_t)S.fb[0] + (mr & 0xffffu), rbase = (int64_t)S.fb[1] + (mr >> 16);
+      int64_t mi = mb, ri = rbase;
+      int rs = rs_in;
+      int64_t tq[CO_PER];  // e2's ts, loaded for every closing position before any row is stored
+#pragma unroll
+      for (int q = 0; q < CO_PER; q++) tq[q] = ((emw >> q) & 1u) ? B.ts[xg[q] & 0x7fffffffu] : 0;
+#pragma unroll
+      for (int q = 0; q < CO_PER; q++) {
+        if (!((vb >> q) & 1u)) break;
+        const int p = p0 + q;
+        if ((hb >> q) & 1u) rs = p;
+        if (!((emw >> q) & 1u)) continue;
+        const uint32_t Lb = (lbw >> (4 * q)) & 15u;
+        const uint32_t g = xg[q] & 0x7fffffffu, lk = xl[q] & 0x7fffu;
+        const uint32_t k = (lk << P.bits) | (uint32_t)o;
+        if (mi >= O.cap || ri + (int64_t)Lb + 1 > O.refcap) {
+          e |= E_OUT;
+        } else {
+          const int64_t sg = bseq(B, g);
+          O.key[mi] = B.partitioned ? (int32_t)k : 0;
+          O.ts[mi] = tq[q];  // StateEvent ts = e2's (StreamPostStateProcessor.process :64-83)
+          O.type[mi] = 0;
+          O.pos[mi] = sg;
+          O.ref_off[mi] = ri;
+          O.slot_len[mi * MAXS] = (int16_t)Lb;
+          O.slot_len[mi * MAXS + 1] = 1;
+          const int h = sRh[lk], f = sRf[lk];
+          for (uint32_t t = 1; t <= Lb; t++) {
+            const int pp = p - (int)t;
+            int64_t qs;
+            if (pp >= rs) {
+              qs = bseq(B, S.cg[pp] & 0x7fffffffu);
+            } else {
+              const int d = rs - pp - 1;  // 0: the key's latest event before this chunk
+              qs = d < f ? bseq(B, sH[(size_t)((h + M - 1 - d) % M) * kpo + lk])
+                         : C.hseq[rd][cs_hslot(M - 1 - (d - f), (int64_t)k, M)];
+            }
+            O.refs[ri + (Lb - t)] = qs;
+          }
+          O.refs[ri + Lb] = sg;
+        }
+        mi++;
+        ri += Lb + 1;
+      }
+      emw = 0;  // (no words)
+      __syncthreads();
+    } else {
+      const uint32_t mo = co_block_scan(lm, S.sc, tot);
+      pmo = mo;
+      if (tid == 0) {  // (+ a lane count that is always 0: keeps the atomic optimizer, which reads the
+                       // result back at once, off this one-lane add)
+        pres = tot ? atomicAdd(O.count + __builtin_amdgcn_mbcnt_lo(0u, 0u), (unsigned long long)tot) : 0ull;
+        ppend = true;
+      }
+      __syncthreads();
     }
-    __syncthreads();
     // walk 3: the words (written during the next chunk), and at each run end the key's state after
     // the run
     pem = emw;
-    pmo = mo;
     int rs = rs_in;
     const uint32_t lnext = p0 + CO_PER <= nc ? (S.cl[p0 + CO_PER] & 0x7fffu) : 0xffffu;
 #pragma unroll

@@ -71,9 +71,10 @@ def tables(M, every, mn):
     key's next event (CountPreStateProcessor.java:288-305, StreamPreStateProcessor.java:360)."""
     D = M + 1
     n = M + 2
-    if mn >= 2:
-        c = 0 if every else D
-        return [c] * n, [c] * n, [c] * n, False
+    if mn >= 2:  # L = 1: the count-1 partial of the key's last event (alive until its next event)
+        if every:
+            return [0] * n, [1] * n, [1] * n, False
+        return [D] * n, [1] + [D] * (n - 1), [1] + [D] * (n - 1), False
     if every:
         return [0] * n, [1] + [i + 1 for i in range(1, M)] + [1, 1], [1] + [0] * (M - 1) + [1, 1], True
     return [D] * n, [1] + [i + 1 for i in range(1, M)] + [D, D], [1] + [D] * M + [D], True
@@ -141,6 +142,32 @@ def test_table_automaton_matches_oracle_every_min_max(every, M):
         rng = np.random.default_rng(3)
         ts, key, v = _stream(rng, 4_000, 7)
         assert compare(automaton(M, "<", ts, key, v), table_automaton(M, "<", True, 1, ts, key, v)) is None
+
+
+@pytest.mark.parametrize("every", [True, False], ids=["every", "once"])
+def test_table_automaton_live_chains_equal_oracle_oldest_live(every):
+    """After every event: the oldest event the tables keep alive (the last L events of each key with
+    1 <= L <= M) is the oracle's oldest live event -- including min >= 2, where L = 1 is the count-1
+    partial the reference holds until the key's next event (shp_engine_oldest_live_seq, describe)."""
+    for M, mn in ((5, 1), (5, 2), (3, 3), (8, 4), (2, 1)):
+        rng = np.random.default_rng(M * 3 + mn + every)
+        ts, key, v = _stream(rng, 500, 7, nan=0.0)
+        cq = _cq(_app(M, "<", every=every, mn=mn))
+        o = OracleEngine(cq.program_json(), 0)
+        t0, t10, t11, _ = tables(M, every, mn)
+        L, hist = {}, {}
+        for i in range(len(ts)):
+            o.push(ts[i:i + 1], key[i:i + 1], np.zeros(1, np.int32), [v[i:i + 1]], [None])
+            o.fetch()
+            k = int(key[i])
+            h = hist.setdefault(k, [])
+            Lb = L.get(k, 0)
+            a, b = v[i] > 20, bool(h) and v[i] < v[h[-1]]
+            L[k] = (t11 if b else t10)[Lb] if a else t0[Lb]
+            h.append(i)
+            del h[:-M]
+            live = [hist[q][-L[q]] for q in L if 1 <= L[q] <= M]
+            assert o.oldest_live_seq() == (min(live) if live else i + 1), (M, mn, i)
 
 
 def test_table_automaton_with_nulls_once():
@@ -264,8 +291,17 @@ def test_cseq_wide_ts_span_reruns_with_16_byte_records():
     ts[30_000:] += 3 << 31  # a jump of ~200 days inside the first push
     cq = _cq(_app(5, "<"))
     want = _push(OracleEngine(cq.program_json(), 0), ts, key, v, 40_000)
-    eng = _hip(cq, 200, 1 << 16)
+    import os
+    os.environ["SHP_CO_FULL_OFF"] = "1"  # (read at create) the sorted records, not the owner path
+    try:
+        eng = _hip(cq, 200, 1 << 16)
+    finally:
+        del os.environ["SHP_CO_FULL_OFF"]
     got = _push(eng, ts, key, v, 40_000)
     assert compare(want, got) is None, compare(want, got)
     assert eng.stat("cseq_wide_reruns") == 1  # the second push (20k events after the jump) is narrow
     assert sum(len(x) for x in want.values()) > 100
+    own = _hip(cq, 200, 1 << 16)  # the owner path reads ts only per row: no re-run
+    got = _push(own, ts, key, v, 40_000)
+    assert compare(want, got) is None, compare(want, got)
+    assert own.stat("cseq_wide_reruns") == 0

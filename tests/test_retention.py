@@ -125,7 +125,7 @@ def _hip_factory(max_keys):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg,n,keys,ms,layout", [(2, 200_000, 10_000, 0.05, 3), ("3b", 100_000, 1_000, 1, 4),
-                                                  (5, 60_000, 2_000, 0.2, 3), (3, 20_000, 1_000, 1, 0),
+                                                  (5, 60_000, 2_000, 0.2, 3), (3, 20_000, 1_000, 1, 4),
                                                   (4, 20_000, 100, 5, 0)])
 def test_sync_pushes_compact_with_engine_retention(cfg, n, keys, ms, layout):
     """C2 (10k keys, 2*10^5 pushes) and C3' (10^5 pushes) one event per push (C5, C3 and C4 shorter):

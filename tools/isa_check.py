@@ -122,7 +122,9 @@ def main(argv=None) -> int:
         print("isa_check: no budget file (run with --update)", file=sys.stderr)
         return 1
     bud = json.load(open(BUDGET))
-    bad = [(k, v[:2], bud[k]) for k, v in cur.items() if k in bud and (v[0] > bud[k][0] or v[1] > bud[k][1])]
+    # nested-loop waits may not grow; a wait moved out of a nested loop into the outer one is no regression
+    bad = [(k, v[:2], bud[k]) for k, v in cur.items()
+           if k in bud and (v[1] > bud[k][1] or v[0] > bud[k][0] + (bud[k][1] - v[1]))]
     missing = [k for k in bud if k not in cur]
     for k, n, b in bad:
         print(f"isa_check: {k}: s_waitcnt vmcnt(0) in loops / nested loops {n[0]} / {n[1]} (budget {b[0]} / {b[1]})",
