@@ -564,7 +564,7 @@ struct shp_engine {
       bool la_v1 = labs_v1;
       if (fast == 4 && !la_v1) {  // the logical-absent records sorted with their keys (labs.h)
         HIP_OK(hipMemsetAsync(d_kbeg, 0, (cfg.max_keys + 1) * sizeof(uint32_t), stream));
-        la.sort_events(B, x_key, d_skey, d_skey2, key_bits, d_err, stream, kt);
+        la.sort_events(B, x_key, d_skey, d_skey2, key_bits, d_err, stream, kt, d_kbeg, d_kcnt);
         int e0 = 0;  // a push beyond the 16-byte records' ranges: the 32-byte form (pack + gather)
         HIP_OK(hipMemcpyAsync(&e0, d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
@@ -600,7 +600,7 @@ struct shp_engine {
         kt.mark("radix_sort", stream);
         HIP_OK(rocprim::radix_sort_pairs(d_tmp, tb, d_skey, d_skey2, d_idx, d_perm, (size_t)n, 0, key_bits + 1, stream));
       }
-      if (bounds) {
+      if (bounds && !(fast == 4 && !la_v1 && la.bounds)) {  // (the logical-absent multisplit set them)
         kt.mark("key_bounds", stream);
         k_key_bounds<<<(unsigned)((cfg.max_keys + 255) / 256), 256, 0, stream>>>(d_skey2, n, d_kbeg, d_kcnt,
                                                                                 (uint32_t)cfg.max_keys);
@@ -1692,8 +1692,9 @@ double shp_last_kernel_ms(const shp_engine* e, const char* which) {
 // diagnostic build only: per-owner solve phase cycles of the last push (nown * 8)
 int shp_debug_la_stamps(shp_engine* e, unsigned long long* host, int64_t n) {
   if (!e || e->fast != 4 || !e->la.D.stamps) return SHP_ERR_ARG;
-  int64_t k = std::min<int64_t>(n, (int64_t)e->la.D.nk * 8);
-  return hipMemcpy(host, e->la.D.stamps, k * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)(k / 8) : SHP_ERR_DEVICE;
+  int64_t k = std::min<int64_t>(n, (int64_t)e->la.D.nk * LA_NSTAMP);
+  return hipMemcpy(host, e->la.D.stamps, k * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)(k / LA_NSTAMP)
+                                                                                    : SHP_ERR_DEVICE;
 }
 int shp_debug_sw_stamps(shp_engine* e, unsigned long long* host, int64_t n) {
   if (!e || e->fast != 2 || !e->sw.D.stamps) return SHP_ERR_ARG;

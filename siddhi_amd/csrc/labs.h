@@ -48,17 +48,17 @@ constexpr int LA_SB = 16;                        // events of a key staged in LD
 struct __attribute__((aligned(16))) LaEv {  // one event: packed (32 B, one sector), key order, LDS staging
   int64_t ts, clk;
   uint32_t g, v;
-  int32_t st;
-  uint32_t n;
+  int32_t role;  // its stream's state: 0 x, 1 y, 2 z, -1 none (clock-only, or a stream the query does not read)
+  uint32_t n;    // 1: its value is null; 2: its own filter holds (fx for x, fy for y: la_pack_q)
 };
 constexpr int LA_WIDE = 1 << 26;       // a push's ts / clock leave base +- 2^31 ms or its batch index 2^27:
                                         // the push re-runs with the 32-byte records (not an error)
 
 // the sorted form of LaEv (round 3): 16 bytes, so rocPRIM moves 20-byte (key, record) pairs; ts and
-// clock relative to the push's first ts, stream + 1 and the null flag above the index
+// clock relative to the push's first ts, role + 1, the filter flag and the null flag above the index
 struct __attribute__((aligned(16))) LaEv16 {
   int32_t ts, clk;
-  uint32_t gs;  // batch index (27 bits) | stream + 1 << 27 (4 bits) | null << 31
+  uint32_t gs;  // batch index (27 bits) | role + 1 << 27 (2 bits) | filter << 29 | null << 31
   uint32_t v;
 };
 
@@ -146,11 +146,18 @@ __device__ __forceinline__ LaEv la_ev_at(const LabsDev& D, const BatchView& B, i
   x.ts = base + r.ts;
   x.clk = base + r.clk;
   x.g = r.gs & 0x7FFFFFFu;
-  x.st = (int32_t)((r.gs >> 27) & 15u) - 1;
-  x.n = r.gs >> 31;
+  x.role = (int32_t)((r.gs >> 27) & 3u) - 1;
+  x.n = (r.gs >> 31) | (((r.gs >> 29) & 1u) << 1);
   x.v = r.v;
   return x;
 }
+
+// the event's role, and whether its own filter holds (the x / y filters of a k_labs_w shape read only
+// their own event: LabsState::wave_ok; for other shapes the flag is unused)
+__device__ __forceinline__ int la_pack_role(const LabsDev& D, int st) {
+  return st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
+}
+__device__ __forceinline__ bool la_pack_q(const LabsDev& D, int role, uint32_t v, bool nl);
 
 // event g in arrival order (coalesced reads): ts, clock, batch index, the value of its stream's
 // column, stream, null -- one 32-byte record, so the key-order gather reads one sector per event
@@ -158,15 +165,16 @@ __device__ __forceinline__ LaEv la_ev_at(const LabsDev& D, const BatchView& B, i
 static __global__ void k_labs_pack(LabsDev D, BatchView B, int64_t n) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x) {
     const int st = B.stream ? B.stream[g] : 0;
-    const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
+    const int role = la_pack_role(D, st);
     const int c = role == 0 ? D.col[0] : (role == 1 ? D.col[1] : (role == 2 ? D.col[2] : -1));
     LaEv x;
     x.ts = B.ts[g];
     x.clk = B.rmax[g];
     x.g = (uint32_t)g;
     x.v = c >= 0 ? ((const uint32_t*)B.cols[c])[g] : 0u;
-    x.st = st;
-    x.n = c < 0 || (B.nulls[c] && B.nulls[c][g]) ? 1u : 0u;
+    x.role = role;
+    const bool nl = c < 0 || (B.nulls[c] && B.nulls[c][g]);
+    x.n = (nl ? 1u : 0u) | (la_pack_q(D, role, x.v, nl) ? 2u : 0u);
     D.p_ev[g] = x;
   }
 }
@@ -179,7 +187,7 @@ static __global__ void k_labs_pack2(LabsDev D, BatchView B, const int32_t* __res
   LaEv16* out = reinterpret_cast<LaEv16*>(D.p_ev);
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x) {
     const int st = B.stream ? B.stream[g] : 0;
-    const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
+    const int role = la_pack_role(D, st);
     const int c = role == 0 ? D.col[0] : (role == 1 ? D.col[1] : (role == 2 ? D.col[2] : -1));
     uint32_t k = 0;
     if (st < 0) {
@@ -196,17 +204,128 @@ static __global__ void k_labs_pack2(LabsDev D, BatchView B, const int32_t* __res
     okey[g] = k;
     const int64_t base = B.ts[0];
     const int64_t dt = B.ts[g] - base, dc = B.rmax[g] - base;
-    if (dt != (int64_t)(int32_t)dt || dc != (int64_t)(int32_t)dc || g >= (1ll << 27) || st < -1 || st > 14)
-      e |= LA_WIDE;
+    if (dt != (int64_t)(int32_t)dt || dc != (int64_t)(int32_t)dc || g >= (1ll << 27)) e |= LA_WIDE;
     LaEv16 x;
     x.ts = (int32_t)dt;
     x.clk = (int32_t)dc;
     const bool nl = c < 0 || (B.nulls[c] && B.nulls[c][g]);
-    x.gs = ((uint32_t)g & 0x7FFFFFFu) | ((uint32_t)(st + 1) & 15u) << 27 | (nl ? 0x80000000u : 0u);
     x.v = c >= 0 ? ((const uint32_t*)B.cols[c])[g] : 0u;
+    x.gs = ((uint32_t)g & 0x7FFFFFFu) | (uint32_t)(role + 1) << 27 | (la_pack_q(D, role, x.v, nl) ? 1u << 29 : 0u) |
+           (nl ? 0x80000000u : 0u);
     out[g] = x;
   }
   if (e) atomicOr(err, e);
+}
+
+// ---- the key-order batch by a stable multisplit (round 5), for up to LA_MS_BINS keys: per segment
+// of LA_MS_SEG events a key histogram (k_la_ms_count), one scan of the bin-major counts, then one
+// wave per segment packs each event's 16-byte record straight to its key-order position
+// (k_la_ms_scatter) -- in place of k_labs_pack2 + a radix sort of (key, record) pairs
+constexpr int LA_MS_SEG = 16384;
+constexpr int LA_MS_BINS = 4096;
+__device__ __forceinline__ uint32_t la_bin(const BatchView& B, const int32_t* __restrict__ key, int64_t g, int st,
+                                           uint32_t nokey, int& e) {
+  if (st < 0) return nokey;
+  if (!B.partitioned) return 0u;
+  const int32_t x = key[g];
+  if (x < 0 || (uint32_t)x >= nokey) {
+    e |= 1 << 20;  // SWE_KEYS
+    return nokey;
+  }
+  return (uint32_t)x;
+}
+static __global__ __launch_bounds__(256) void k_la_ms_count(BatchView B, const int32_t* __restrict__ key, int64_t n,
+                                                            uint32_t nokey, int32_t nseg, uint32_t* __restrict__ cnt,
+                                                            int* err) {
+  __shared__ uint32_t h[LA_MS_BINS];
+  const uint32_t nb = nokey + 1u;
+  for (uint32_t b = threadIdx.x; b < nb; b += 256) h[b] = 0;
+  __syncthreads();
+  int e = 0;
+  const int64_t lo = (int64_t)blockIdx.x * LA_MS_SEG, hi = min(n, lo + LA_MS_SEG);
+  for (int64_t g = lo + threadIdx.x; g < hi; g += 256) {
+    const int st = B.stream ? B.stream[g] : 0;
+    atomicAdd(&h[la_bin(B, key, g, st, nokey, e)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += 256) cnt[(int64_t)b * nseg + blockIdx.x] = h[b];
+  if (e) atomicOr(err, e);
+}
+static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchView B, const int32_t* __restrict__ key,
+                                                             int64_t n, uint32_t nokey, int32_t nseg, int bits,
+                                                             const uint32_t* __restrict__ off, int* err) {
+  __shared__ uint32_t cur[LA_MS_BINS];
+  const uint32_t nb = nokey + 1u, lane = threadIdx.x;
+  const int seg = blockIdx.x;
+  for (uint32_t b = lane; b < nb; b += 64) cur[b] = off[(int64_t)b * nseg + seg];
+  __syncthreads();
+  const uint64_t lt = sw_lanemask_lt();
+  LaEv16* out = reinterpret_cast<LaEv16*>(D.s_ev);
+  const int64_t base = B.n > 0 ? B.ts[0] : 0;
+  int e = 0;
+  const int64_t lo = (int64_t)seg * LA_MS_SEG, hi = min(n, lo + LA_MS_SEG);
+  // one step of 64 events in arrival order; the next step's columns are loaded before this one is placed
+  int64_t n_ts = 0, n_clk = 0;
+  int32_t n_st = 0, n_k = 0;
+  uint32_t n_v = 0;
+  uint8_t n_nl = 0;
+  auto fetch = [&](int64_t g) __attribute__((always_inline)) {
+    if (g < hi) {
+      n_st = B.stream ? B.stream[g] : 0;
+      n_k = B.partitioned ? key[g] : 0;
+      n_ts = B.ts[g];
+      n_clk = B.rmax[g];
+    }
+  };
+  fetch(lo + lane);
+  for (int64_t g0 = lo; g0 < hi; g0 += 64) {
+    const int64_t g = g0 + lane;
+    const bool valid = g < hi;
+    const int st = n_st;
+    const int32_t kx = n_k;
+    const int64_t ts = n_ts, clk = n_clk;
+    fetch(g + 64);
+    uint32_t bin = nokey;
+    if (valid && st >= 0) {
+      if (!B.partitioned) bin = 0;
+      else if (kx < 0 || (uint32_t)kx >= nokey) bin = nokey;  // (k_la_ms_count raised SWE_KEYS)
+      else bin = (uint32_t)kx;
+    }
+    const uint64_t peers = sw_match_peers(bin, bits, valid);
+    const uint32_t below = (uint32_t)__popcll(peers & lt);
+    const bool lead = valid && (peers & lt) == 0;
+    const uint32_t ldl = peers ? (uint32_t)__ffsll((unsigned long long)peers) - 1u : 0u;
+    uint32_t old = 0;
+    if (lead) {
+      old = cur[bin];
+      cur[bin] = old + (uint32_t)__popcll(peers);
+    }
+    const uint32_t pos = __shfl(old, (int)ldl, 64) + below;
+    if (valid) {
+      const int role = la_pack_role(D, st);
+      const int c = role == 0 ? D.col[0] : (role == 1 ? D.col[1] : (role == 2 ? D.col[2] : -1));
+      const int64_t dt = ts - base, dc = clk - base;
+      if (dt != (int64_t)(int32_t)dt || dc != (int64_t)(int32_t)dc || g >= (1ll << 27)) e |= LA_WIDE;
+      const bool nl = c < 0 || (B.nulls[c] && B.nulls[c][g]);
+      LaEv16 x;
+      x.ts = (int32_t)dt;
+      x.clk = (int32_t)dc;
+      x.v = c >= 0 ? ((const uint32_t*)B.cols[c])[g] : 0u;
+      x.gs = ((uint32_t)g & 0x7FFFFFFu) | (uint32_t)(role + 1) << 27 | (la_pack_q(D, role, x.v, nl) ? 1u << 29 : 0u) |
+             (nl ? 0x80000000u : 0u);
+      out[pos] = x;
+    }
+  }
+  if (e) atomicOr(err, e);
+}
+// each key's run: kbeg = its bin's first position, kcnt = its length (bins 0..nk-1; bin nk: no key)
+static __global__ void k_la_ms_bounds(const uint32_t* __restrict__ off, int32_t nseg, uint32_t nk, uint32_t* kbeg,
+                                      uint32_t* kcnt) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk) return;
+  const uint32_t a = off[(int64_t)k * nseg], b = off[(int64_t)(k + 1) * nseg];
+  kbeg[k] = a;
+  kcnt[k] = b - a;
 }
 
 // sorted position i <- the packed event perm[i]
@@ -253,6 +372,10 @@ __device__ __forceinline__ bool la_pred(const LaPredD& p, const LaVals& V) {
   if (p.n == 1) return a;
   const bool b = la_term(p.t[1], V);
   return p.combine ? (a || b) : (a && b);
+}
+__device__ __forceinline__ bool la_pack_q(const LabsDev& D, int role, uint32_t v, bool nl) {
+  const LaVals V0{v, v, 0u, nl, nl, true, D.tag[0], D.tag[1], D.tag[2]};
+  return (role == 0 && la_pred(D.fx, V0)) || (role == 1 && la_pred(D.fy, V0));
 }
 
 // ------------------------------------------------------------------ k_labs: the exact rule
@@ -484,9 +607,9 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
         s.nw = o;
       }
     }
-    const int role = x.st == D.st[0] ? 0 : (x.st == D.st[1] ? 1 : (x.st == D.st[2] ? 2 : -1));
+    const int role = x.role;
     if (role < 0) return;
-    const bool en = x.n != 0;
+    const bool en = (x.n & 1u) != 0;
     LaVals V{s.xv, s.yv, 0u, (s.fl & 1u) != 0, (s.fl & 2u) != 0, true, D.tag[0], D.tag[1], D.tag[2]};
     if (role == 2) {  // Z: new-and-every -> pending, then each pending pair fz matches is dropped
       move_nae();
@@ -657,7 +780,17 @@ __device__ __forceinline__ bool la_kill(const LaPredD& p, const LaKill& K, doubl
 // The queue lives in registers, entry i in lane i (sorted); the entries a block queues are counted
 // per event lane (a completion, or the pairs a Z event kills), all at that event's ts + T.
 constexpr int LA_WF = 64;  // queue entries k_labs_w holds (one per lane)
+// diagnostic build (SHP_SW_STAMPS): per key, phase cycles 0 load, 1 partial, 2 doomed E_D, 3 leave
+// search, 4 settle, 5 queue, 8 Z kills, 9 firings; counts 6 pairs, 7 events, 10 kill rounds, 11 Z events
+constexpr int LA_NSTAMP = 16;
 
+// FZ1: fz is one term comparing the Z event's value with a constant or a slot's value (C4's
+// `S3[price > e1.price]`): the Z side is converted once per event, the other once per pair, and the
+// kill test in the pairs' walk over the Z events is one double compare (la_fz1_side / la_kill1)
+__host__ __device__ inline bool la_fz1(const LaPredD& p) {
+  return p.n == 1 && ((p.t[0].ak == 3) != (p.t[0].bk == 3));
+}
+template <bool FZ1>
 static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
                                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                                int* err) {
@@ -759,7 +892,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     __syncthreads();
   };
 #ifdef SHP_SW_STAMPS  // diagnostic build: wave cycles per phase, and counts (trips, pairs, Z events)
-  unsigned long long lst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long lst[LA_NSTAMP] = {};
   uint64_t lsp = clock64();
 #define LA_STAMP(x)               \
   do {                            \
@@ -787,7 +920,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       n_clk = x.clk;
       n_g = x.g;
       n_v = x.v;
-      n_st = x.st;
+      n_st = x.role;
       n_n = x.n;
     }
   };
@@ -797,10 +930,10 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     const bool valid = lane < nv;
     const int64_t ts = n_ts, clk = n_clk;
     const uint32_t g = n_g, v = n_v;
-    const int32_t st = valid ? n_st : -1;
-    const bool en = n_n != 0;
+    const int role = valid ? n_st : -1;
+    const bool en = (n_n & 1u) != 0;
+    const bool qf = (n_n & 2u) != 0;  // its own filter (la_pack_q)
     if (j0 + 64 < cnt) fetch(j0 + 64);
-    const int role = st == D.st[0] ? 0 : (st == D.st[1] ? 1 : (st == D.st[2] ? 2 : -1));
     {  // the ordered formulation: timestamps do not decrease within the key, and no event lags the
        // clock by T or more (an entry queued then could fire at a send far past it)
       const int64_t tp = __shfl_up(ts, 1, 64);
@@ -814,9 +947,8 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       }
     }
     const int64_t seqg = bseq(B, g);
-    const LaVals V0{v, v, 0u, en, en, true, t0g, t1g, t2g};
-    const uint64_t QX = __ballot(valid && role == 0 && la_pred(D.fx, V0));
-    const uint64_t QY = __ballot(valid && role == 1 && la_pred(D.fy, V0));
+    const uint64_t QX = __ballot(valid && role == 0 && qf);
+    const uint64_t QY = __ballot(valid && role == 1 && qf);
     LA_STAMP(0);
     // 1. the partial.  A half partial carried into the block resolves first (its partner, or the
     //    first event beyond W).  Then, from an empty partial at lane p, the next step depends on
@@ -893,25 +1025,9 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     const int b = opp ? __builtin_ctzll(opp) : 64;
     const int bc = b < 64 ? b : 0;
     const int64_t tsa = __shfl(ts, ac, 64), tsb = __shfl(ts, bc, 64);
-    int zq = nv;  // the first lane after a whose ts is beyond ts_a + W (ts ascend within the block)
-    // searched only when some lane's step can reset: no partner within W, and a later event beyond W
-    const int64_t tsl = la_rl64(ts, nv - 1);
-    const bool need = useW && a < nv && !(b < nv && tsb - tsa <= Wn) && tsl - tsa > Wn;
-    if (__ballot(need)) {
-      int l2 = a + 1, h2 = nv;
-#pragma unroll
-      for (int it = 0; it < 7; it++) {
-        const int mid = (l2 + h2) >> 1;
-        const int64_t tm = __shfl(ts, mid < 64 ? mid : 0, 64);
-        if (l2 < h2) {
-          if (mid < nv && tm - tsa > Wn) h2 = mid;
-          else l2 = mid + 1;
-        }
-      }
-      zq = l2;
-    }
-    // kind: 0 nothing fills a slot in [p, nv); 1 pair (a, b), empty at b + 1; 2 reset at zq;
-    // 3 a half partial (a) at the block's end
+    // kind: 0 nothing fills a slot in [p, nv); 1 pair (a, b), empty at b + 1; 2 no partner within W:
+    // a reset at the first event beyond ts_a + W if the block has one (found by a ballot when the
+    // chain reaches the step -- few steps a block), else a half partial (a) at the block's end
     int kind, J;
     if (a >= nv) {
       kind = 0;
@@ -919,12 +1035,9 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     } else if (b < nv && (!useW || tsb - tsa <= Wn)) {
       kind = 1;
       J = b + 1;
-    } else if (zq < nv) {
-      kind = 2;
-      J = zq;
     } else {
-      kind = 3;
-      J = 64;
+      kind = 2;
+      J = a;
     }
     const int KJ = J | (kind << 8);
     uint64_t PM = 0;  // chain positions whose step completes a pair
@@ -936,9 +1049,15 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
         PM |= 1ull << p;
         p = kj & 0xFF;
       } else if (kd == 2) {
-        p = kj & 0xFF;
+        const int ap = kj & 0xFF;
+        const int64_t tap = la_rl64(ts, ap);
+        const uint64_t zb = useW ? __ballot(valid && lane > ap && ts - tap > Wn) : 0ull;
+        if (!zb) {
+          hk = p;
+          break;
+        }
+        p = __builtin_ctzll(zb);
       } else {
-        if (kd == 3) hk = p;
         break;
       }
     }
@@ -998,6 +1117,12 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     LA_STAMP(1);
     LA_COUNT(6, nal);
     const uint64_t zm = __ballot(valid && role == 2);
+    LA_COUNT(11, __popcll(zm));
+    // FZ1: the Z side of fz per event (a null Z event kills nothing: left out of the kills' walk)
+    const LaTermD& z1 = D.fz.t[0];
+    const bool z1a = z1.ak == 3;
+    const double zd1 = FZ1 ? la_val(v, t2g, z1a ? z1.aflt : z1.bflt) : 0.0;
+    const uint64_t zmk = FZ1 ? zm & __ballot(!en) : zm;  // the Z events that may kill
     const int lastz = zm ? 63 - __builtin_clzll(zm) : -1;  // the block's last Z event (new-and-every -> pending)
     const int64_t clkl = la_rl64(clk, nv - 1);            // the clock at the block's last event
     const uint64_t cmask = __ballot(valid && Ec[lane] != 0);  // lanes that completed a pair
@@ -1059,9 +1184,33 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
           const int fx = xm ? __builtin_ctzll(xm) : 64;
           if (lane == j) f = min(f, fx);
         }
+        LA_STAMP(3);
+        LA_COUNT(10, 1);
         killed = false;
         kq = 64;
-        if (zm) {
+        if (FZ1 && zmk) {  // each pair walks its Z events (c, f): one shuffle and one compare a step
+          const int oi = z1a ? 0 : 1;  // the pair's side of the term
+          const LaKill K = la_kill_pre(D.fz, w, t0g, t1g, t2g);
+          const double kv = oi == 0 ? K.b[0] : K.a[0];
+          auto nextz = [&](int x) __attribute__((always_inline)) -> int {
+            if (x >= 64) return 64;
+            const uint64_t r = zmk >> x;
+            return r ? x + __builtin_ctzll(r) : 64;
+          };
+          int q = nextz(c + 1);
+          bool act = lane < nal && q < f && !K.nul[0];
+          while (__ballot(act)) {
+            const double zq = __shfl(zd1, q < 64 ? q : 0, 64);
+            if (act) {
+              const double A = z1a ? zq : kv, Bv = z1a ? kv : zq;
+              const int o3 = (A < Bv ? 1 : 0) | (A == Bv ? 2 : 0) | (A > Bv ? 4 : 0);
+              killed = ((o3 | (o3 == 0 ? 8 : 0)) & z1.mask) != 0;
+              if (killed) kq = q;
+              q = nextz(q + 1);
+              act = !killed && q < f;
+            }
+          }
+        } else if (!FZ1 && zm) {
           const LaKill K = la_kill_pre(D.fz, w, t0g, t1g, t2g);
           auto nextz = [&](int x) __attribute__((always_inline)) -> int {
             if (x >= 64) return 64;
@@ -1082,6 +1231,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
             }
           }
         }
+        LA_STAMP(8);
         const uint64_t km = __ballot(killed);
         if (!km || !doom) break;
         // the kills' lanes: do they come before a doomed pair's completion?
@@ -1102,7 +1252,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
         }
         if (!redo) break;
       }
-      LA_STAMP(3);
+      LA_STAMP(8);
       // the kills, counted per event lane (each queues an entry at the event's ts + T)
       if (killed) atomicAdd(&Ec[kq], 1);
       __syncthreads();
@@ -1128,6 +1278,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
           lastf = max(lastf, __builtin_ctzll(r));
         }
       }
+      LA_STAMP(9);
       const bool tonae = lane < nal && Anae[lane] && c >= lastf && c >= lastz;  // no Z / firing after it
       settle(left, killed, tonae, f == 0 ? lo : gp + 1, gf, w, ed);
       LA_STAMP(4);
@@ -1213,7 +1364,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
 #ifdef SHP_SW_STAMPS
   LA_COUNT(7, cnt);
   if (lane == 0 && D.stamps)
-    for (int x = 0; x < 8; x++) D.stamps[(int64_t)k * 8 + x] = lst[x];
+    for (int x = 0; x < LA_NSTAMP; x++) D.stamps[(int64_t)k * LA_NSTAMP + x] = lst[x];
 #endif
 #undef LA_STAMP
 #undef LA_COUNT
@@ -1411,7 +1562,7 @@ struct LabsState {
     wave_ok = own(D.fx, 1) && own(D.fy, 2) && !getenv("SHP_NO_LABS_W");
     if (wave_ok) al(D.rec, la_region((uint32_t)std::min<int64_t>(cap, 0xFFFFFFFFll), max_keys) + 1);
 #ifdef SHP_SW_STAMPS
-    al(D.stamps, (int64_t)max_keys * 8);
+    al(D.stamps, (int64_t)max_keys * LA_NSTAMP);
 #endif
     k_labs_init<<<(unsigned)((max_keys + 255) / 256), 256, 0, s>>>(D);
   }
@@ -1438,7 +1589,8 @@ struct LabsState {
       (void)hipMemsetAsync(D.maxstep, 0, sizeof(unsigned long long), s);
       if (B.n > 1) k_labs_steps<<<1024, 256, 0, s>>>(B.rmax, B.n, D.maxstep);
       kt.mark("labs", s);
-      k_labs_w<<<(unsigned)D.nk, 64, 0, s>>>(D, B, perm, kbeg, kcnt, err);
+      if (la_fz1(D.fz)) k_labs_w<true><<<(unsigned)D.nk, 64, 0, s>>>(D, B, perm, kbeg, kcnt, err);
+      else k_labs_w<false><<<(unsigned)D.nk, 64, 0, s>>>(D, B, perm, kbeg, kcnt, err);
       kt.mark("labs_scan", s);
       size_t tb = tmp_bytes;
       (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
@@ -1459,8 +1611,37 @@ struct LabsState {
 
   // the push's events in key order with their sort keys (skey_out, for the key runs): k_labs_pack2,
   // then one stable radix sort of (key, record) pairs
+  // (ms: the multisplit's counts / offsets; bounds: kbeg / kcnt were set here, no key_bounds pass)
+  uint32_t* ms_cnt = nullptr;
+  uint32_t* ms_off = nullptr;
+  bool bounds = false;
+  bool split_ok(int64_t cap) const {
+    return D.nk + 1 <= LA_MS_BINS && cap < (1ll << 27) && !getenv("SHP_LABS_SORT");
+  }
   void sort_events(const BatchView& B, const int32_t* key, uint32_t* skey_in, uint32_t* skey_out, int key_bits,
-                   int* err, hipStream_t s, KTimer& kt) {
+                   int* err, hipStream_t s, KTimer& kt, uint32_t* kbeg = nullptr, uint32_t* kcnt = nullptr) {
+    bounds = false;
+    if (ms_cnt && kbeg && B.n > 0) {  // the stable multisplit
+      const int32_t nseg = (int32_t)((B.n + LA_MS_SEG - 1) / LA_MS_SEG);
+      const uint32_t nokey = (uint32_t)D.nk;
+      int bits = 0;
+      while ((1u << bits) < nokey + 1u) bits++;
+      const size_t nc = (size_t)(nokey + 1) * nseg + 1;
+      kt.mark("labs_count", s);
+      k_la_ms_count<<<(unsigned)nseg, 256, 0, s>>>(B, key, B.n, nokey, nseg, ms_cnt, err);
+      (void)hipMemsetAsync(ms_cnt + nc - 1, 0, sizeof(uint32_t), s);
+      kt.mark("labs_mscan", s);
+      size_t tb = stmp_bytes;
+      (void)rocprim::exclusive_scan(stmp, tb, ms_cnt, ms_off, 0u, nc, rocprim::plus<uint32_t>(), s);
+      kt.mark("labs_split", s);
+      k_la_ms_scatter<<<(unsigned)nseg, 64, 0, s>>>(D, B, key, B.n, nokey, nseg, bits, ms_off, err);
+      k_la_ms_bounds<<<(unsigned)((nokey + 255) / 256), 256, 0, s>>>(ms_off, nseg, nokey, kbeg, kcnt);
+      kt.mark(nullptr, s);
+      sorted = true;
+      bounds = true;
+      D.ev16 = 1;
+      return;
+    }
     kt.mark("labs_pack", s);
     if (B.n > 0) k_labs_pack2<<<2048, 256, 0, s>>>(D, B, key, B.n, (uint32_t)D.nk, skey_in, err);
     kt.mark("labs_sort", s);
@@ -1476,6 +1657,14 @@ struct LabsState {
     size_t b = 0;
     (void)rocprim::radix_sort_pairs(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (LaEv16*)nullptr,
                                     (LaEv16*)nullptr, (size_t)std::max<int64_t>(cap, 1), 0, key_bits + 1, s);
+    if (split_ok(cap)) {
+      const size_t nc = (size_t)(D.nk + 1) * (size_t)((std::max<int64_t>(cap, 1) + LA_MS_SEG - 1) / LA_MS_SEG) + 1;
+      al(ms_cnt, (int64_t)nc);
+      al(ms_off, (int64_t)nc);
+      size_t b2 = 0;
+      (void)rocprim::exclusive_scan(nullptr, b2, ms_cnt, ms_off, 0u, nc, rocprim::plus<uint32_t>(), s);
+      b = std::max(b, b2);
+    }
     stmp_bytes = std::max<size_t>(b, 16);
     if (hipMalloc(&stmp, stmp_bytes) != hipSuccess) throw std::runtime_error("hipMalloc failed (logical-absent sort)");
   }
@@ -1525,11 +1714,12 @@ struct LabsState {
     }
     if (D.wtmp) (void)hipFree(D.wtmp);
     if (D.ftmp) (void)hipFree(D.ftmp);
-    void* qs[] = {D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp, D.maxstep};
+    void* qs[] = {D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp, D.maxstep, ms_cnt, ms_off};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = LabsDev{};
     stmp = nullptr;
+    ms_cnt = ms_off = nullptr;
   }
 };
 

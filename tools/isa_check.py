@@ -28,7 +28,7 @@ OBJ = os.path.join(ROOT, "siddhi_amd", "build_obj")
 BUDGET = os.path.join(ROOT, "tools", "isa_budget.json")
 LLVM = "/opt/rocm/lib/llvm/bin"
 # the kernels of the default paths of SURVEY §8d's configs (demangled-name prefixes)
-HOT = ("k_sw_count", "k_sw_scatter", "k_sw_lean", "k_co_count", "k_co_scatter", "k_co_run", "k_cs3", "k_cs_pack",
+HOT = ("k_sw_count", "k_sw_scatter", "k_sw_lean", "k_co_count", "k_co_scatter", "k_co_run", "k_cs3", "k_cs_pack", "k_la_ms",
        "k_labs_w", "k_labs_pack", "k_labs_out")
 UNITS = ("sweep_solve0", "sweep_lean", "sweep_lean_agg", "engine")
 

@@ -49,18 +49,20 @@ def main():
         ks = {k: eng.kernel_ms(k) for k in ("labs_gather", "labs", "labs_out", "radix_sort", "clock_scan")}
         print(f"rep {rep}: m={mt.m} " + " ".join(f"{k}={v:.3f}ms" for k, v in ks.items()), flush=True)
         if stamps:
-            buf = (ctypes.c_ulonglong * (K * 8))()
+            S = 16
+            buf = (ctypes.c_ulonglong * (K * S))()
             L.shp_debug_la_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
-            nk = L.shp_debug_la_stamps(eng.h, buf, K * 8)
-            st = np.frombuffer(buf, dtype=np.uint64, count=nk * 8).reshape(nk, 8).astype(np.float64)
-            names = ["load+filters", "partial", "fire", "kill", "settle", "queue"]
-            tot = st[:, :6].sum()
+            nk = L.shp_debug_la_stamps(eng.h, buf, K * S)
+            st = np.frombuffer(buf, dtype=np.uint64, count=nk * S).reshape(nk, S).astype(np.float64)
+            phases = [(0, "load+filters"), (1, "partial"), (2, "doomed E_D"), (3, "leave search"), (8, "Z kills"),
+                      (9, "firings"), (4, "settle"), (5, "queue")]
+            tot = sum(st[:, x].sum() for x, _ in phases)
             blocks = st[:, 7].sum() / 64
-            for x in range(6):
-                print(f"    {names[x]:<14} {100 * st[:, x].sum() / tot:5.1f}%  cycles/block {st[:, x].sum() / blocks:8.0f}")
-            print(f"    waiting pairs/block {st[:, 6].sum() / blocks:.1f}"
-                  f"  events/key {st[:, 7].mean():.0f}  cycles/key {st[:, :5].sum(1).mean():.3e}")
-
+            for x, name in phases:
+                print(f"    {name:<14} {100 * st[:, x].sum() / tot:5.1f}%  cycles/block {st[:, x].sum() / blocks:8.0f}")
+            print(f"    waiting pairs/block {st[:, 6].sum() / blocks:.1f}  kill rounds/block {st[:, 10].sum() / blocks:.2f}"
+                  f"  Z/block {st[:, 11].sum() / blocks:.1f}  events/key {st[:, 7].mean():.0f}"
+                  f"  cycles/block {tot / blocks:.0f}")
 
 if __name__ == "__main__":
     main()
