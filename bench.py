@@ -40,7 +40,7 @@ BYTES_PER_MATCH = {"pairs32": 8,  # (e2 batch index, e2 seq - e1 seq) as two u32
 KERNELS = ("sw_count", "sw_scan", "sw_scatter", "sw_win", "sw_win_tail", "sw_lean", "sw_solve", "sw_spill", "sw_expand",
            "radix_sort", "clock_scan", "key_hist", "key_scan", "sort_keys", "iota", "clamp_clock",
            "fast_gather", "fast_search", "nclose_scan", "fast_total", "fast_emit", "fast_carry", "nfa_lanes",
-           "cseq_count", "cseq_scan", "cseq", "co_count", "co_scan", "co_scatter", "co_run", "cs_pack", "cs_sort", "cs_count", "cs_scan", "cs_emit", "cs_state", "labs_pack", "labs_sort", "labs_gather", "labs_count", "labs_mscan", "labs_split", "labs_steps", "labs_scan", "labs", "labs_pos", "labs_out",
+           "cseq_count", "cseq_scan", "cseq", "co_count", "co_scan", "co_scatter", "co_run", "cs_pack", "cs_sort", "cs_count", "cs_scan", "cs_emit", "cs_state", "labs_pack", "labs_sort", "labs_gather", "labs_count", "labs_mscan", "labs_split", "labs_steps", "labs_segcheck", "labs_scan", "labs", "labs_pos", "labs_out",
            "key_bounds")
 WORKLOADS = {
     "1": "C1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec (one key)",

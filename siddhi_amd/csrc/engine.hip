@@ -276,7 +276,7 @@ struct shp_engine {
   int lds_lanes = 0;
   double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
   int64_t last_m = 0;
-  int64_t pushes = 0, lean_pushes = 0, lean_fallbacks = 0, labs_fallbacks = 0;  // shp_engine_stat
+  int64_t pushes = 0, lean_pushes = 0, lean_fallbacks = 0, labs_fallbacks = 0, labs_segmiss = 0;  // shp_engine_stat
   int64_t win_pushes = 0, win_fallbacks = 0;
   int64_t spill_reruns = 0;
 
@@ -691,6 +691,20 @@ struct shp_engine {
       HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
       cs.run2(B, x_key, x_stream, key_bits, O, d_err, stream, kt, false);
       HIP_OK(hipMemcpyAsync(h_tsmax, cs.D.tsmax, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipEventRecord(ev2, stream));
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      std::memcpy(&herr, h_status + 2, sizeof(int));
+    }
+    if (fast == 4 && (herr & LA_SEGMISS) && !(herr & (LA_SLOW | SWE_KEYS))) {
+      // a warmed-up segment of k_labs_w started from another state than its predecessor ended
+      // with: the push re-runs unsegmented from the same committed state
+      labs_segmiss++;
+      HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
+      la.noseg = true;
+      la.run(B, O, d_perm, d_kbeg, d_kcnt, d_err, d_tmp, tmp_bytes, stream, kt);
+      la.noseg = false;
       HIP_OK(hipEventRecord(ev2, stream));
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
@@ -1673,6 +1687,7 @@ int64_t shp_engine_stat(const shp_engine* e, const char* which) {
   if (w == "cseq_wide_reruns") return e->cseq_wide_reruns;
   if (w == "cseq_owner") return e->fast == 3 && e->cs.own ? 1 : 0;  // CHAIN32 pushes on the owner kernels
   if (w == "labs_fallbacks") return e->labs_fallbacks;
+  if (w == "labs_segmiss") return e->labs_segmiss;
   if (w == "match_layout") return e->cfg.match_layout;  // as resolved at create (SHP_LAYOUT_COMPACT)
   if (w == "spill_reruns") return e->spill_reruns;
   if (w == "spilled_owners") return e->fast == 2 ? e->sw.count_spilled() : 0;
@@ -1692,7 +1707,7 @@ double shp_last_kernel_ms(const shp_engine* e, const char* which) {
 // diagnostic build only: per-owner solve phase cycles of the last push (nown * 8)
 int shp_debug_la_stamps(shp_engine* e, unsigned long long* host, int64_t n) {
   if (!e || e->fast != 4 || !e->la.D.stamps) return SHP_ERR_ARG;
-  int64_t k = std::min<int64_t>(n, (int64_t)e->la.D.nk * LA_NSTAMP);
+  int64_t k = std::min<int64_t>(n, (int64_t)e->la.D.nk * e->la.D.seg * LA_NSTAMP);
   return hipMemcpy(host, e->la.D.stamps, k * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)(k / LA_NSTAMP)
                                                                                     : SHP_ERR_DEVICE;
 }

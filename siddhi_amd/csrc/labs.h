@@ -131,6 +131,9 @@ struct LabsDev {
   LaEv* p_ev;        // the batch's events in arrival order, packed (k_labs_pack: one sector each)
   LaEv* s_ev;        // ... in key order (k_labs_gather)
   int32_t ev16;      // this push's key-order batch is LaEv16 records in s_ev's memory (sort_events)
+  int32_t seg;       // k_labs_w segments per key (LA_H; 1: none) -- the slot stride of cm / om / rec
+  uint32_t warm;     // warm-up events before a cut (LA_WARM; SHP_LABS_WARM for tests)
+  struct LaSnap* snap[2];  // segment boundary states: [0] warmed-up start of segment h, [1] end of h - 1
   int32_t pad2;
   unsigned long long* stamps;  // diagnostic build (SHP_SW_STAMPS): k_labs_w phase cycles per key
   LaRec* rec;        // k_labs_w's records, per key region (la_region)
@@ -264,32 +267,52 @@ static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchVie
   const int64_t base = B.n > 0 ? B.ts[0] : 0;
   int e = 0;
   const int64_t lo = (int64_t)seg * LA_MS_SEG, hi = min(n, lo + LA_MS_SEG);
-  // one step of 64 events in arrival order; the next step's columns are loaded before this one is placed
-  int64_t n_ts = 0, n_clk = 0;
-  int32_t n_st = 0, n_k = 0;
-  uint32_t n_v = 0;
-  uint8_t n_nl = 0;
-  auto fetch = [&](int64_t g) __attribute__((always_inline)) {
+  // one step of 64 events in arrival order; the next step's columns load before this one is placed.
+  // The value column follows from the stream, so the three roles' columns (uniform pointers, one
+  // load when they are the same array) are read independently of it and the role picks one.
+  const uint32_t* cp[3];
+  const uint8_t* np[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    cp[r] = D.col[r] >= 0 ? (const uint32_t*)B.cols[D.col[r]] : nullptr;
+    np[r] = D.col[r] >= 0 ? B.nulls[D.col[r]] : nullptr;
+  }
+  const bool onecol = cp[0] == cp[1] && cp[1] == cp[2] && np[0] == np[1] && np[1] == np[2];
+  struct Pf {
+    int64_t ts, clk;
+    int32_t st, k;
+    uint32_t v[3];
+    uint8_t n[3];
+  };
+  auto fetch = [&](Pf& f, int64_t g) __attribute__((always_inline)) {
     if (g < hi) {
-      n_st = B.stream ? B.stream[g] : 0;
-      n_k = B.partitioned ? key[g] : 0;
-      n_ts = B.ts[g];
-      n_clk = B.rmax[g];
+      f.st = B.stream ? B.stream[g] : 0;
+      f.k = B.partitioned ? key[g] : 0;
+      f.ts = B.ts[g];
+      f.clk = B.rmax[g];
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        if (r > 0 && onecol) {
+          f.v[r] = f.v[0];
+          f.n[r] = f.n[0];
+        } else {
+          f.v[r] = cp[r] ? cp[r][g] : 0u;
+          f.n[r] = cp[r] == nullptr ? 1 : (np[r] ? np[r][g] : 0);
+        }
+      }
     }
   };
-  fetch(lo + lane);
-  for (int64_t g0 = lo; g0 < hi; g0 += 64) {
+  auto place = [&](const Pf& f, int64_t g0) __attribute__((always_inline)) {
     const int64_t g = g0 + lane;
     const bool valid = g < hi;
-    const int st = n_st;
-    const int32_t kx = n_k;
-    const int64_t ts = n_ts, clk = n_clk;
-    fetch(g + 64);
+    const int rl = la_pack_role(D, f.st);
+    const uint32_t xv = rl == 0 ? f.v[0] : (rl == 1 ? f.v[1] : (rl == 2 ? f.v[2] : 0u));
+    const bool nl = rl == 0 ? f.n[0] != 0 : (rl == 1 ? f.n[1] != 0 : (rl == 2 ? f.n[2] != 0 : true));
     uint32_t bin = nokey;
-    if (valid && st >= 0) {
+    if (valid && f.st >= 0) {
       if (!B.partitioned) bin = 0;
-      else if (kx < 0 || (uint32_t)kx >= nokey) bin = nokey;  // (k_la_ms_count raised SWE_KEYS)
-      else bin = (uint32_t)kx;
+      else if (f.k < 0 || (uint32_t)f.k >= nokey) bin = nokey;  // (k_la_ms_count raised SWE_KEYS)
+      else bin = (uint32_t)f.k;
     }
     const uint64_t peers = sw_match_peers(bin, bits, valid);
     const uint32_t below = (uint32_t)__popcll(peers & lt);
@@ -302,19 +325,27 @@ static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchVie
     }
     const uint32_t pos = __shfl(old, (int)ldl, 64) + below;
     if (valid) {
-      const int role = la_pack_role(D, st);
-      const int c = role == 0 ? D.col[0] : (role == 1 ? D.col[1] : (role == 2 ? D.col[2] : -1));
-      const int64_t dt = ts - base, dc = clk - base;
+      const int64_t dt = f.ts - base, dc = f.clk - base;
       if (dt != (int64_t)(int32_t)dt || dc != (int64_t)(int32_t)dc || g >= (1ll << 27)) e |= LA_WIDE;
-      const bool nl = c < 0 || (B.nulls[c] && B.nulls[c][g]);
       LaEv16 x;
       x.ts = (int32_t)dt;
       x.clk = (int32_t)dc;
-      x.v = c >= 0 ? ((const uint32_t*)B.cols[c])[g] : 0u;
-      x.gs = ((uint32_t)g & 0x7FFFFFFu) | (uint32_t)(role + 1) << 27 | (la_pack_q(D, role, x.v, nl) ? 1u << 29 : 0u) |
+      x.v = xv;
+      x.gs = ((uint32_t)g & 0x7FFFFFFu) | (uint32_t)(rl + 1) << 27 | (la_pack_q(D, rl, xv, nl) ? 1u << 29 : 0u) |
              (nl ? 0x80000000u : 0u);
       out[pos] = x;
     }
+  };
+  // two register sets, so a step's loads land where the step after next reads them (no copies,
+  // whose waits would hold each step for the loads just issued)
+  Pf fa{}, fb{};
+  fetch(fa, lo + lane);
+  for (int64_t g0 = lo; g0 < hi; g0 += 128) {
+    fetch(fb, g0 + 64 + lane);
+    place(fa, g0);
+    if (g0 + 64 >= hi) break;
+    fetch(fa, g0 + 128 + lane);
+    place(fb, g0 + 64);
   }
   if (e) atomicOr(err, e);
 }
@@ -716,6 +747,7 @@ __global__ __launch_bounds__(64) void k_labs(LabsDev D, BatchView B, MatchOut O,
 //           Firing follows completion order, so the emitted records keep the FIFO order.
 // More than 64 waiting pairs in a key raise LA_SLOW: the engine re-runs the push with k_labs.
 constexpr int LA_SLOW = 1 << 28;
+constexpr int LA_SEGMISS = 1 << 27;  // a warmed-up segment start differed from the state before it: re-run unsegmented
 constexpr int LA_BOUND = 1 << 29;  // a key's records would leave its region (a broken invariant: fail, never write)
 
 __device__ __forceinline__ int64_t la_rl64(int64_t x, int l) {
@@ -784,6 +816,34 @@ constexpr int LA_WF = 64;  // queue entries k_labs_w holds (one per lane)
 // search, 4 settle, 5 queue, 8 Z kills, 9 firings; counts 6 pairs, 7 events, 10 kill rounds, 11 Z events
 constexpr int LA_NSTAMP = 16;
 
+// Segments (round 5).  With few keys (one wave each cannot fill the CUs) a key's events are cut into
+// up to LA_H segments of whole 64-event blocks, one wave each.  The state at a cut depends only on the
+// key's recent events (a pair leaves at its due or when its slots pass W, a timer fires once the
+// clock reaches it, the partial expires after W), so the wave of segment h > 0 starts from the empty
+// state LA_WARM events before its cut and runs them without writing records; at the cut it stores
+// the state it reached, the wave of segment h - 1 stores the state it ends with, and k_labs_segcheck
+// compares the two field by field.  Any difference raises LA_SEGMISS and the engine re-runs the push
+// unsegmented, so the records and the state are always the sequential kernel's.  Only the last
+// segment settles the push's end and writes the key's state.
+constexpr int LA_H = 4;
+constexpr uint32_t LA_MINSEG = 4096;   // events per segment at least
+constexpr uint32_t LA_WARM = 4 * 64;   // warm-up events before a cut
+constexpr int LA_SEG_MAXKEYS = 4096;   // segments only while keys are this few
+struct LaSnap {
+  int64_t xseq, xts, yseq, yts, last, lsched, lo;
+  uint32_t xv, yv, fl, hxy, nal, nef;
+  LaWait A[64];
+  int64_t ed[64];
+  int64_t qe[64];
+  uint8_t nae[64];
+};
+__host__ __device__ __forceinline__ int la_nseg(uint32_t cnt, int H) {
+  return H <= 1 ? 1 : (int)min((uint32_t)H, max(1u, cnt / LA_MINSEG));
+}
+__host__ __device__ __forceinline__ uint32_t la_segb(uint32_t cnt, int hk, int i) {  // cut i of hk segments
+  return i >= hk ? cnt : (uint32_t)(((uint64_t)cnt * (uint64_t)i / (uint64_t)hk) & ~63ull);
+}
+
 // FZ1: fz is one term comparing the Z event's value with a constant or a slot's value (C4's
 // `S3[price > e1.price]`): the Z side is converted once per event, the other once per pair, and the
 // kill test in the pairs' walk over the Z events is one double compare (la_fz1_side / la_kill1)
@@ -793,20 +853,37 @@ __host__ __device__ inline bool la_fz1(const LaPredD& p) {
 template <bool FZ1>
 static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
                                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
-                                               int* err) {
+                                               int H, int* err) {
   __shared__ LaWait A[64];      // the pairs on the absent state's lists, list (= completion) order
   __shared__ int32_t Ac[64];    // completing lane in the current block (-1: an earlier block)
   __shared__ int64_t Aed[64];   // E_D of each pair
   __shared__ uint8_t Anae[64];  // on new-and-every (no Z event and no firing since its completion)
   __shared__ int32_t Ec[64];    // per event lane of the block: entries it queued (completion + kills)
   __shared__ int64_t Es[64];    // staging of the queue's new order
-  const int k = blockIdx.x;
+  const int S = D.seg;  // slot stride
+  const int k = blockIdx.x / S, h = blockIdx.x % S, ks = blockIdx.x;
   if (k >= D.nk) return;
   const int lane = (int)threadIdx.x;
+  const uint32_t beg = kbeg[k], cnt = kcnt[k];
+  const int hk = la_nseg(cnt, H);
+  if (h >= hk) {  // (an unused slot: no records)
+    if (lane == 0) D.cm[ks] = 0;
+    return;
+  }
+  const uint32_t s_beg = la_segb(cnt, hk, h), s_end = la_segb(cnt, hk, h + 1);
+  const uint32_t w_beg = h == 0 ? 0u : (s_beg > D.warm ? s_beg - D.warm : 0u);
+  const bool lastseg = h == hk - 1;
   const uint64_t lt = sw_lanemask_lt();
   const int rd = D.cur, wr = rd ^ 1;
   const int cap = D.wcap, msk = cap - 1;
-  const LaPend s0 = D.pend[rd][k];
+  LaPend s0{};
+  if (h == 0) {
+    s0 = D.pend[rd][k];
+  } else {  // the empty state (k_labs_init's)
+    s0.xseq = s0.yseq = -1;
+    s0.last = INT64_MIN;
+    s0.reg = 1;
+  }
   const bool useW = D.within >= 0;
   const int64_t Wn = D.within, Tw = D.wait;
   const int64_t Wb = useW ? Wn : (1ll << 60);  // D = min slot ts + Wb
@@ -818,7 +895,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     if (!slow && *D.maxstep > (unsigned long long)Tw) slow = true;             // a step at a later send
     if (slow) {
       if (lane == 0) {
-        D.cm[k] = 0;  // k_labs_out runs before the host sees LA_SLOW
+        D.cm[ks] = 0;  // k_labs_out runs before the host sees LA_SLOW
         atomicOr(err, LA_SLOW);
       }
       return;
@@ -847,9 +924,9 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     if (lane < nal) Aed[lane] = ed;
   }
   __syncthreads();
-  const uint32_t beg = kbeg[k], cnt = kcnt[k];
-  LaRec* rec = D.rec + la_region(beg, k);
-  const uint32_t rcap = (cnt + 1u) / 2u + 64u;  // the region's records (la_region)
+  LaRec* rec = D.rec + la_region(beg + s_beg, ks);
+  const uint32_t rcap = (s_end - s_beg + 1u) / 2u + 64u;  // the region's records (la_region)
+  bool emit_on = w_beg == s_beg;  // (warm-up blocks write no records)
   const int8_t t0g = D.tag[0], t1g = D.tag[1], t2g = D.tag[2];
   int e = 0;
   uint32_t nm = 0;
@@ -864,7 +941,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   // time -- or are killed; the survivors are compacted in order
   auto settle = [&](bool left, bool killed, bool tonae, int64_t flo, int64_t fhi, LaWait w, int64_t ed)
                     __attribute__((always_inline)) {
-    const bool ok = lane < nal && left && !killed &&
+    const bool ok = emit_on && lane < nal && left && !killed &&
                     (!useW || (llabs(w.xts - w.due) <= Wn && llabs(w.yts - w.due) <= Wn));
     const uint64_t em = __ballot(ok);
     if (nm + (uint32_t)__popcll(em) > rcap) e |= LA_BOUND;
@@ -914,7 +991,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   uint32_t n_g = 0, n_v = 0, n_n = 1;
   int32_t n_st = -1;
   auto fetch = [&](uint32_t j0) __attribute__((always_inline)) {
-    if (j0 + (uint32_t)lane < cnt) {
+    if (j0 + (uint32_t)lane < s_end) {
       const LaEv x = la_ev_at(D, B, (int64_t)beg + j0 + lane);
       n_ts = x.ts;
       n_clk = x.clk;
@@ -924,23 +1001,51 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       n_n = x.n;
     }
   };
-  fetch(0);
-  for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
-    const int nv = (int)min(64u, cnt - j0);
+  // the state at a cut, for k_labs_segcheck (between blocks: the pairs are compacted, Ac = -1, Ec = 0)
+  auto dump = [&](LaSnap* sp) __attribute__((always_inline)) {
+    if (lane == 0) {
+      sp->xseq = hx ? xseq : -1;
+      sp->yseq = hy ? yseq : -1;
+      sp->xts = hx ? xts : 0;
+      sp->yts = hy ? yts : 0;
+      sp->xv = hx ? xv : 0u;
+      sp->yv = hy ? yv : 0u;
+      sp->fl = fl;
+      sp->hxy = (hx ? 1u : 0u) | (hy ? 2u : 0u);
+      sp->last = last;
+      sp->lsched = lsched;
+      sp->lo = lo;
+      sp->nal = (uint32_t)nal;
+      sp->nef = (uint32_t)nef;
+    }
+    if (lane < nal) {
+      sp->A[lane] = A[lane];
+      sp->ed[lane] = Aed[lane];
+      sp->nae[lane] = Anae[lane];
+    }
+    if (lane < nef) sp->qe[lane] = qe;
+  };
+  fetch(w_beg);
+  for (uint32_t j0 = w_beg; j0 < s_end; j0 += 64) {
+    if (j0 == s_beg && h > 0) {  // the cut: the state the warm-up reached
+      dump(D.snap[0] + ks);
+      emit_on = true;
+    }
+    const int nv = (int)min(64u, s_end - j0);
     const bool valid = lane < nv;
     const int64_t ts = n_ts, clk = n_clk;
     const uint32_t g = n_g, v = n_v;
     const int role = valid ? n_st : -1;
     const bool en = (n_n & 1u) != 0;
     const bool qf = (n_n & 2u) != 0;  // its own filter (la_pack_q)
-    if (j0 + 64 < cnt) fetch(j0 + 64);
+    if (j0 + 64 < s_end) fetch(j0 + 64);
     {  // the ordered formulation: timestamps do not decrease within the key, and no event lags the
        // clock by T or more (an entry queued then could fire at a send far past it)
       const int64_t tp = __shfl_up(ts, 1, 64);
       const int64_t prev = lane == 0 ? last : tp;
       if (__ballot(valid && ((prev != INT64_MIN && ts < prev) || clk - ts >= Tw))) {
         if (lane == 0) {
-          D.cm[k] = 0;
+          D.cm[ks] = 0;
           atomicOr(err, LA_SLOW);
         }
         return;
@@ -966,7 +1071,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       if (b < z) {  // the partner: the pair completes and waits on the absent state
         if (nal >= 64) {
           if (lane == 0) {
-            D.cm[k] = 0;
+            D.cm[ks] = 0;
             atomicOr(err, LA_SLOW);
           }
           return;
@@ -1065,7 +1170,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       const int npm = __popcll(PM);
       if (nal + npm > 64) {
         if (lane == 0) {
-          D.cm[k] = 0;
+          D.cm[ks] = 0;
           atomicOr(err, LA_SLOW);
         }
         return;
@@ -1304,7 +1409,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
         const int n1 = __shfl(pos, 63, 64);
         if (n0 + n1 > LA_WF) {
           if (lane == 0) {
-            D.cm[k] = 0;
+            D.cm[ks] = 0;
             atomicOr(err, LA_SLOW);
           }
           return;
@@ -1324,6 +1429,20 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     lo = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)g, nv - 1) + 1;
     last = la_rl64(ts, nv - 1);
     __syncthreads();
+  }
+  auto stamps_out = [&]() {
+#ifdef SHP_SW_STAMPS
+    LA_COUNT(7, s_end - w_beg);
+    if (lane == 0 && D.stamps)
+      for (int x = 0; x < LA_NSTAMP; x++) D.stamps[(int64_t)ks * LA_NSTAMP + x] = lst[x];
+#endif
+  };
+  if (!lastseg) {  // the state this segment ends with, for the next one's check; no push-end settle
+    stamps_out();
+    dump(D.snap[1] + ks + 1);
+    if (lane == 0) D.cm[ks] = min(nm, rcap);
+    if (e) atomicOr(err, e);
+    return;
   }
   // the timers the push's last clock reaches
   const int64_t lastclk = B.n > 0 ? B.rmax[B.n - 1] : B.clock0;
@@ -1361,17 +1480,13 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     const uint64_t notq = all & ~m;
     nae = notq ? nal - 1 - (63 - __builtin_clzll(notq)) : nal;
   }
-#ifdef SHP_SW_STAMPS
-  LA_COUNT(7, cnt);
-  if (lane == 0 && D.stamps)
-    for (int x = 0; x < LA_NSTAMP; x++) D.stamps[(int64_t)k * LA_NSTAMP + x] = lst[x];
-#endif
+  stamps_out();
 #undef LA_STAMP
 #undef LA_COUNT
   if (nal > cap || nef > cap) e |= E_LIST;
   else if (lane < nal) D.wq[wr][(int64_t)k * cap + lane] = A[lane];
   if (lane == 0) {
-    D.cm[k] = min(nm, rcap);
+    D.cm[ks] = min(nm, rcap);
     LaPend s{};
     s.xseq = hx ? xseq : -1;
     s.yseq = hy ? yseq : -1;
@@ -1396,17 +1511,22 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
 // k_labs_w's records of each key (its region of D.rec) to the push's output at the key's offset,
 // with the fire event found as k_labs_pos does
 static __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ kbeg,
-                                                  const uint32_t* __restrict__ kcnt, int* err) {
-  const int k = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-  if (k >= D.nk) return;
+                                                  const uint32_t* __restrict__ kcnt, int H, int* err) {
+  const int S = D.seg;
+  const int ks = blockIdx.x * 4 + (int)(threadIdx.x >> 6);  // a slot: key k's segment h
+  if (ks >= D.nk * S) return;
+  const int k = ks / S, h = ks % S;
   const int lane = (int)(threadIdx.x & 63);
-  const int64_t mi = D.om[k];
-  const uint32_t nm = min(D.cm[k], (kcnt[k] + 1u) / 2u + 64u);
-  if (k == D.nk - 1 && lane == 0) {
+  const int64_t mi = D.om[ks];
+  const uint32_t cnt = kcnt[k];
+  const int hk = la_nseg(cnt, H);
+  const uint32_t s_beg = h < hk ? la_segb(cnt, hk, h) : 0u, s_end = h < hk ? la_segb(cnt, hk, h + 1) : 0u;
+  const uint32_t nm = h < hk ? min(D.cm[ks], (s_end - s_beg + 1u) / 2u + 64u) : 0u;
+  if (ks == D.nk * S - 1 && lane == 0) {
     O.count[0] = (unsigned long long)(mi + nm);
     O.count[1] = 2ull * (unsigned long long)(mi + nm);
   }
-  const LaRec* rec = D.rec + la_region(kbeg[k], k);
+  const LaRec* rec = D.rec + la_region(kbeg[k] + s_beg, ks);
   int e = 0;
   for (uint32_t r = (uint32_t)lane; r < nm; r += 64) {
     const int64_t m = mi + r;
@@ -1436,6 +1556,31 @@ static __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B,
     }
   }
   if (e) atomicOr(err, e);
+}
+
+// the segment cuts: the warmed-up state of segment h against the state segment h - 1 ended with
+static __global__ __launch_bounds__(64) void k_labs_segcheck(LabsDev D, const uint32_t* __restrict__ kcnt, int H,
+                                                            int* err) {
+  const int S = D.seg;
+  const int k = blockIdx.x / S, h = blockIdx.x % S;
+  if (k >= D.nk || h == 0 || h >= la_nseg(kcnt[k], H)) return;
+  const int lane = (int)threadIdx.x;
+  const LaSnap& a = D.snap[0][blockIdx.x];
+  const LaSnap& b = D.snap[1][blockIdx.x];
+  bool bad = false;
+  if (lane == 0)
+    bad = a.xseq != b.xseq || a.yseq != b.yseq || a.xts != b.xts || a.yts != b.yts || a.xv != b.xv || a.yv != b.yv ||
+          a.fl != b.fl || a.hxy != b.hxy || a.last != b.last || a.lsched != b.lsched || a.lo != b.lo ||
+          a.nal != b.nal || a.nef != b.nef;
+  const uint32_t nal = min(a.nal, 64u), nef = min(a.nef, 64u);
+  if ((uint32_t)lane < nal && (uint32_t)lane < b.nal) {
+    const LaWait& x = a.A[lane];
+    const LaWait& y = b.A[lane];
+    bad |= x.due != y.due || x.xseq != y.xseq || x.xts != y.xts || x.yseq != y.yseq || x.yts != y.yts ||
+           x.xv != y.xv || x.yv != y.yv || x.fl != y.fl || a.ed[lane] != b.ed[lane] || a.nae[lane] != b.nae[lane];
+  }
+  if ((uint32_t)lane < nef && (uint32_t)lane < b.nef) bad |= a.qe[lane] != b.qe[lane];
+  if (__ballot(bad) && lane == 0) atomicOr(err, LA_SEGMISS);
 }
 
 // a key's pairs and queue entries into rings of another capacity (tier change), heads reset to 0
@@ -1481,6 +1626,7 @@ struct LabsState {
   int tier = 0;
   bool wave_ok = false;  // k_labs_w applies: x's and y's filters read only their own event
   bool slow = false;     // this push re-runs on k_labs (k_labs_w raised LA_SLOW)
+  bool noseg = false;    // this push re-runs k_labs_w unsegmented (LA_SEGMISS)
   bool sorted = false;   // this push's key-order batch came from sort_events (no pack + gather)
   void* stmp = nullptr;  // sort_events' rocPRIM scratch
   size_t stmp_bytes = 0;
@@ -1547,8 +1693,12 @@ struct LabsState {
     al(D.wtmp, (int64_t)max_keys * LA_WCAP);
     al(D.ftmp, (int64_t)max_keys * LA_WCAP);
     al(D.maxstep, 1);
-    al(D.cm, max_keys);
-    al(D.om, max_keys);
+    // segments while the keys are few (a wave per key leaves CUs idle) and k_labs_w can run
+    D.seg = max_keys <= LA_SEG_MAXKEYS && !getenv("SHP_LABS_NOSEG") ? LA_H : 1;
+    D.warm = LA_WARM;
+    if (const char* w = getenv("SHP_LABS_WARM")) D.warm = (uint32_t)(atoi(w) / 64 * 64);  // (a multiple of 64)
+    al(D.cm, (int64_t)max_keys * D.seg);
+    al(D.om, (int64_t)max_keys * D.seg);
     al(D.p_ev, cap);
     al(D.s_ev, cap);
     D.wcap = LA_CAPS[0];
@@ -1560,9 +1710,15 @@ struct LabsState {
       return true;
     };
     wave_ok = own(D.fx, 1) && own(D.fy, 2) && !getenv("SHP_NO_LABS_W");
-    if (wave_ok) al(D.rec, la_region((uint32_t)std::min<int64_t>(cap, 0xFFFFFFFFll), max_keys) + 1);
+    if (!wave_ok) D.seg = 1;
+    if (wave_ok) al(D.rec, la_region((uint32_t)std::min<int64_t>(cap, 0xFFFFFFFFll), max_keys * D.seg) + 1);
+    if (D.seg > 1) {
+      al(D.snap[0], (int64_t)max_keys * D.seg + 1);
+      al(D.snap[1], (int64_t)max_keys * D.seg + 1);
+    }
 #ifdef SHP_SW_STAMPS
-    al(D.stamps, (int64_t)max_keys * LA_NSTAMP);
+    al(D.stamps, (int64_t)max_keys * D.seg * LA_NSTAMP);
+    (void)hipMemset(D.stamps, 0, (size_t)max_keys * D.seg * LA_NSTAMP * sizeof(unsigned long long));
 #endif
     k_labs_init<<<(unsigned)((max_keys + 255) / 256), 256, 0, s>>>(D);
   }
@@ -1589,13 +1745,19 @@ struct LabsState {
       (void)hipMemsetAsync(D.maxstep, 0, sizeof(unsigned long long), s);
       if (B.n > 1) k_labs_steps<<<1024, 256, 0, s>>>(B.rmax, B.n, D.maxstep);
       kt.mark("labs", s);
-      if (la_fz1(D.fz)) k_labs_w<true><<<(unsigned)D.nk, 64, 0, s>>>(D, B, perm, kbeg, kcnt, err);
-      else k_labs_w<false><<<(unsigned)D.nk, 64, 0, s>>>(D, B, perm, kbeg, kcnt, err);
+      const int H = noseg ? 1 : D.seg;
+      const unsigned gs = (unsigned)(D.nk * D.seg);
+      if (la_fz1(D.fz)) k_labs_w<true><<<gs, 64, 0, s>>>(D, B, perm, kbeg, kcnt, H, err);
+      else k_labs_w<false><<<gs, 64, 0, s>>>(D, B, perm, kbeg, kcnt, H, err);
+      if (H > 1) {
+        kt.mark("labs_segcheck", s);
+        k_labs_segcheck<<<gs, 64, 0, s>>>(D, kcnt, H, err);
+      }
       kt.mark("labs_scan", s);
       size_t tb = tmp_bytes;
-      (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)D.nk, rocprim::plus<uint32_t>(), s);
+      (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)gs, rocprim::plus<uint32_t>(), s);
       kt.mark("labs_out", s);
-      k_labs_out<<<(unsigned)((D.nk + 3) / 4), 256, 0, s>>>(D, B, O, kbeg, kcnt, err);
+      k_labs_out<<<(gs + 3) / 4, 256, 0, s>>>(D, B, O, kbeg, kcnt, H, err);
       kt.mark(nullptr, s);
       return;
     }
@@ -1714,7 +1876,7 @@ struct LabsState {
     }
     if (D.wtmp) (void)hipFree(D.wtmp);
     if (D.ftmp) (void)hipFree(D.ftmp);
-    void* qs[] = {D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp, D.maxstep, ms_cnt, ms_off};
+    void* qs[] = {D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp, D.maxstep, ms_cnt, ms_off, D.snap[0], D.snap[1]};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = LabsDev{};

@@ -526,3 +526,43 @@ def test_labs_wave_and_thread_kernels_leave_the_same_state(monkeypatch, keys, st
 def synth_t0():
     from siddhi_amd import synth
     return synth.T0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("step,warm", [(300, None), (40, None), (300, "0")], ids=["sparse", "denser", "no-warmup"])
+def test_labs_segments_vs_oracle_and_unsegmented_state(monkeypatch, step, warm):
+    """Few keys with long runs: k_labs_w cuts each key's events into segments (a wave each, the later
+    ones warmed up from the empty state over the 256 events before their cut).  Sparse keys (a key
+    event every 1.2 s) and denser ones (every 160 ms) converge at every cut; without a warm-up
+    (SHP_LABS_WARM=0) the later segments start empty, the cut check sees the difference and the push
+    re-runs unsegmented.  Either way the records equal the oracle's and the state after every push
+    equals an unsegmented engine's (SHP_LABS_NOSEG)."""
+    from siddhi_amd.native import HipEngine
+    cq = program_for(4)
+    g = small_stream(4, 200_000, 4)
+    g["ts"] = (synth_t0() + np.arange(len(g["ts"])) * step).astype(np.int64)
+    want = per_key(run(OracleEngine(cq.program_json(), 0), cq, g, 100_003))
+    if warm is not None:
+        monkeypatch.setenv("SHP_LABS_WARM", warm)
+    a = HipEngine(cq.program_json(), 0, max_keys=4, max_batch=1 << 17)
+    monkeypatch.delenv("SHP_LABS_WARM", raising=False)
+    monkeypatch.setenv("SHP_LABS_NOSEG", "1")
+    b = HipEngine(cq.program_json(), 0, max_keys=4, max_batch=1 << 17)
+    cols = [g["price"].astype(np.float32)] * 3
+    n, ga, gb = len(g["ts"]), [], []
+    for lo in range(0, n, 100_003):
+        hi = min(n, lo + 100_003)
+        args = (g["ts"][lo:hi], g["key"][lo:hi], g["stream"][lo:hi], [c[lo:hi] for c in cols], [None] * 3)
+        a.push(*args)
+        b.push(*args)
+        ga.append(a.fetch())
+        gb.append(b.fetch())
+        assert a.describe(a.snapshot())["keys"] == b.describe(b.snapshot())["keys"], lo
+    ra = {}
+    for m in ga:
+        for k, v in per_key(m).items():
+            ra.setdefault(k, []).extend(v)
+    assert compare(want, ra) is None, compare(want, ra)
+    assert sum(len(x) for x in want.values()) > 50
+    assert a.stat("labs_fallbacks") == 0
+    assert (a.stat("labs_segmiss") > 0) == (warm is not None)

@@ -46,13 +46,15 @@ def main():
         mt = native.ShpMatches()
         rc = L.shp_push_batch_device(eng.h, ctypes.byref(b), ctypes.byref(mt))
         assert rc == 0, L.shp_last_error(eng.h)
-        ks = {k: eng.kernel_ms(k) for k in ("labs_gather", "labs", "labs_out", "radix_sort", "clock_scan")}
-        print(f"rep {rep}: m={mt.m} " + " ".join(f"{k}={v:.3f}ms" for k, v in ks.items()), flush=True)
+        ks = {k: eng.kernel_ms(k) for k in ("labs_count", "labs_mscan", "labs_split", "labs", "labs_segcheck",
+                                            "labs_out", "clock_scan")}
+        print(f"rep {rep}: m={mt.m} segmiss={eng.stat('labs_segmiss')} " +
+              " ".join(f"{k}={v:.3f}ms" for k, v in ks.items()), flush=True)
         if stamps:
             S = 16
-            buf = (ctypes.c_ulonglong * (K * S))()
+            buf = (ctypes.c_ulonglong * (K * 4 * S))()  # (k_labs_w segments: up to 4 slots per key)
             L.shp_debug_la_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
-            nk = L.shp_debug_la_stamps(eng.h, buf, K * S)
+            nk = L.shp_debug_la_stamps(eng.h, buf, K * 4 * S)
             st = np.frombuffer(buf, dtype=np.uint64, count=nk * S).reshape(nk, S).astype(np.float64)
             phases = [(0, "load+filters"), (1, "partial"), (2, "doomed E_D"), (3, "leave search"), (8, "Z kills"),
                       (9, "firings"), (4, "settle"), (5, "queue")]
