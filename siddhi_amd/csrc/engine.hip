@@ -573,6 +573,7 @@ struct shp_engine {
           HIP_OK(hipMemcpyAsync(d_err, &keep, sizeof(int), hipMemcpyHostToDevice, stream));
           HIP_OK(hipStreamSynchronize(stream));
           la.sorted = false;
+          la.steps_done = false;
           la_v1 = true;
         }
       }

@@ -302,9 +302,17 @@ static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchVie
       }
     }
   };
+  unsigned long long mxs = 0;  // the push's largest clock step after its first send (k_labs_w's check)
+  int64_t pclk = lo > 0 ? B.rmax[lo - 1] : INT64_MIN;  // the clock before the step's first event
   auto place = [&](const Pf& f, int64_t g0) __attribute__((always_inline)) {
     const int64_t g = g0 + lane;
     const bool valid = g < hi;
+    {
+      int64_t pc = __shfl_up(f.clk, 1, 64);
+      if (lane == 0) pc = pclk;
+      if (valid && g >= 1) mxs = max(mxs, (unsigned long long)(f.clk - pc));
+      pclk = __shfl(f.clk, 63, 64);
+    }
     const int rl = la_pack_role(D, f.st);
     const uint32_t xv = rl == 0 ? f.v[0] : (rl == 1 ? f.v[1] : (rl == 2 ? f.v[2] : 0u));
     const bool nl = rl == 0 ? f.n[0] != 0 : (rl == 1 ? f.n[1] != 0 : (rl == 2 ? f.n[2] != 0 : true));
@@ -347,6 +355,8 @@ static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchVie
     fetch(fa, g0 + 128 + lane);
     place(fb, g0 + 64);
   }
+  for (int o = 32; o > 0; o >>= 1) mxs = max(mxs, (unsigned long long)__shfl_xor((long long)mxs, o, 64));
+  if (lane == 0 && mxs) atomicMax(D.maxstep, mxs);
   if (e) atomicOr(err, e);
 }
 // each key's run: kbeg = its bin's first position, kcnt = its length (bins 0..nk-1; bin nk: no key)
@@ -1627,6 +1637,7 @@ struct LabsState {
   bool wave_ok = false;  // k_labs_w applies: x's and y's filters read only their own event
   bool slow = false;     // this push re-runs on k_labs (k_labs_w raised LA_SLOW)
   bool noseg = false;    // this push re-runs k_labs_w unsegmented (LA_SEGMISS)
+  bool steps_done = false;  // this push's largest clock step is in D.maxstep (the multisplit)
   bool sorted = false;   // this push's key-order batch came from sort_events (no pack + gather)
   void* stmp = nullptr;  // sort_events' rocPRIM scratch
   size_t stmp_bytes = 0;
@@ -1741,9 +1752,11 @@ struct LabsState {
       k_labs_gather<<<4096, 256, 0, s>>>(D, perm, B.n);
     }
     if (wave_ok && !slow) {  // one pass, then the records to their offsets
-      kt.mark("labs_steps", s);
-      (void)hipMemsetAsync(D.maxstep, 0, sizeof(unsigned long long), s);
-      if (B.n > 1) k_labs_steps<<<1024, 256, 0, s>>>(B.rmax, B.n, D.maxstep);
+      if (!steps_done) {  // (the multisplit found it)
+        kt.mark("labs_steps", s);
+        (void)hipMemsetAsync(D.maxstep, 0, sizeof(unsigned long long), s);
+        if (B.n > 1) k_labs_steps<<<1024, 256, 0, s>>>(B.rmax, B.n, D.maxstep);
+      }
       kt.mark("labs", s);
       const int H = noseg ? 1 : D.seg;
       const unsigned gs = (unsigned)(D.nk * D.seg);
@@ -1783,6 +1796,7 @@ struct LabsState {
   void sort_events(const BatchView& B, const int32_t* key, uint32_t* skey_in, uint32_t* skey_out, int key_bits,
                    int* err, hipStream_t s, KTimer& kt, uint32_t* kbeg = nullptr, uint32_t* kcnt = nullptr) {
     bounds = false;
+    steps_done = false;
     if (ms_cnt && kbeg && B.n > 0) {  // the stable multisplit
       const int32_t nseg = (int32_t)((B.n + LA_MS_SEG - 1) / LA_MS_SEG);
       const uint32_t nokey = (uint32_t)D.nk;
@@ -1796,6 +1810,8 @@ struct LabsState {
       size_t tb = stmp_bytes;
       (void)rocprim::exclusive_scan(stmp, tb, ms_cnt, ms_off, 0u, nc, rocprim::plus<uint32_t>(), s);
       kt.mark("labs_split", s);
+      (void)hipMemsetAsync(D.maxstep, 0, sizeof(unsigned long long), s);
+      steps_done = true;
       k_la_ms_scatter<<<(unsigned)nseg, 64, 0, s>>>(D, B, key, B.n, nokey, nseg, bits, ms_off, err);
       k_la_ms_bounds<<<(unsigned)((nokey + 255) / 256), 256, 0, s>>>(ms_off, nseg, nokey, kbeg, kcnt);
       kt.mark(nullptr, s);
