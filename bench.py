@@ -261,6 +261,7 @@ def main():
     expanded = None
     if G == 1 and layout in ("chain32", "pairs32") and not a.no_expanded:
         fresh = [gen(steps + s, 0) for s in range(1 + a.steps)]
+        torch.cuda.synchronize()  # (generated on torch's stream: complete before the engine reads them)
         if layout == "chain32":  # the same path with FULL rows written by its run kernel (k_co_run)
             full = native.HipEngine(cq.program_json(), 0, max_keys=K_local, max_batch=cap, max_matches=cap,
                                     device=local, force_general=force, match_layout=native.LAYOUT_FULL)

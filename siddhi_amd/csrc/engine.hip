@@ -277,7 +277,7 @@ struct shp_engine {
   double last_ms_part = 0, last_ms_nfa = 0, last_ms_total = 0;
   int64_t last_m = 0;
   int64_t pushes = 0, lean_pushes = 0, lean_fallbacks = 0, labs_fallbacks = 0, labs_segmiss = 0;  // shp_engine_stat
-  int64_t win_pushes = 0, win_fallbacks = 0;
+  int64_t win_pushes = 0, win_fallbacks = 0, r16_reruns = 0;
   int64_t spill_reruns = 0;
 
   ~shp_engine() { release(); }
@@ -645,6 +645,23 @@ struct shp_engine {
       // it on to the exact solve below if it does not cover it either
       win_fallbacks++;
       HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
+      kt.mark("sw_lean", stream);
+      sw.launch_lean(B, O, d_err, stream);
+      kt.mark(nullptr, stream);
+      if (cfg.match_layout == SHP_LAYOUT_FULL) sw.expand(B, x_key, O, d_err, stream, kt);
+      HIP_OK(hipEventRecord(ev2, stream));
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(h_status, d_status, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      std::memcpy(&herr, h_status + 2, sizeof(int));
+    }
+    if (fast == 2 && (herr & SWE_LEAN) && !(herr & (SWE_KEYS | SWE_RANGE)) && sw.D.r12) {
+      // k_sw_lean handed back a push scattered in 12-byte records (ts beyond base +- 2^22 ms, or a
+      // reason the 16-byte form shares): the push is scattered again in the 16-byte form and the
+      // lean solve re-runs; what it hands back again goes to the exact solve below
+      r16_reruns++;
+      HIP_OK(hipMemsetAsync(d_status, 0, 3 * sizeof(unsigned long long), stream));
+      sw.rescatter16(B, x_key, d_err, stream, kt);
       kt.mark("sw_lean", stream);
       sw.launch_lean(B, O, d_err, stream);
       kt.mark(nullptr, stream);
@@ -1689,6 +1706,7 @@ int64_t shp_engine_stat(const shp_engine* e, const char* which) {
   if (w == "cseq_owner") return e->fast == 3 && e->cs.own ? 1 : 0;  // CHAIN32 pushes on the owner kernels
   if (w == "labs_fallbacks") return e->labs_fallbacks;
   if (w == "labs_segmiss") return e->labs_segmiss;
+  if (w == "sweep_r16_reruns") return e->r16_reruns;
   if (w == "match_layout") return e->cfg.match_layout;  // as resolved at create (SHP_LAYOUT_COMPACT)
   if (w == "spill_reruns") return e->spill_reruns;
   if (w == "spilled_owners") return e->fast == 2 ? e->sw.count_spilled() : 0;

@@ -101,6 +101,48 @@ struct __attribute__((aligned(16))) SwRec {
   uint32_t v;
 };
 
+// 12-byte record (round 5) for pushes the lean solve takes (one stream column, no nulls): kt = local
+// key << 24 | e1's filter << 23 | ts - base (23 bits, signed).  A push whose ts leave base +- 2^22 ms
+// raises the scatter's overflow flag (D.tsmax[1] bit 1) and re-runs with the 16-byte records.
+struct SwRec12 {
+  uint32_t kt;
+  uint32_t ref;
+  uint32_t v;
+};
+constexpr int64_t SW_R12_SPAN = 1ll << 22;
+__device__ __forceinline__ uint32_t sw_rec_lk(const SwRec& r) { return (uint32_t)(r.kt >> 56); }
+__device__ __forceinline__ int32_t sw_rec_ts32(const SwRec& r) { return (int32_t)(uint32_t)r.kt; }
+__device__ __forceinline__ bool sw_rec_f1(const SwRec& r) { return (r.kt & (1ull << 53)) != 0; }
+__device__ __forceinline__ uint32_t sw_rec_lk(const SwRec12& r) { return r.kt >> 24; }
+__device__ __forceinline__ int32_t sw_rec_ts32(const SwRec12& r) { return ((int32_t)(r.kt << 9)) >> 9; }
+__device__ __forceinline__ bool sw_rec_f1(const SwRec12& r) { return ((r.kt >> 23) & 1u) != 0; }
+// a record held in registers across a loop: the 12-byte form in a 4-register tuple, so a prefetch
+// lands where the loop reads it (a 3-register load result copied into the loop's tuple waited for
+// the load: tools/isa_check.py)
+template <class R>
+struct SwRecReg {
+  using T = R;
+  static __device__ __forceinline__ T load(const R* p, int64_t i) { return p[i]; }
+};
+struct __attribute__((aligned(16))) SwRec12R {
+  uint32_t kt, ref, v, pad;
+};
+template <>
+struct SwRecReg<SwRec12> {
+  using T = SwRec12R;
+  static __device__ __forceinline__ T load(const SwRec12* p, int64_t i) {
+    T t;
+    t.kt = p[i].kt;
+    t.ref = p[i].ref;
+    t.v = p[i].v;
+    t.pad = 0;
+    return t;
+  }
+};
+__device__ __forceinline__ uint32_t sw_rec_lk(const SwRec12R& r) { return r.kt >> 24; }
+__device__ __forceinline__ int32_t sw_rec_ts32(const SwRec12R& r) { return ((int32_t)(r.kt << 9)) >> 9; }
+__device__ __forceinline__ bool sw_rec_f1(const SwRec12R& r) { return ((r.kt >> 23) & 1u) != 0; }
+
 constexpr uint64_t SW_TSBIAS = 1ull << 49;
 constexpr uint64_t SW_TSMASK = (1ull << 50) - 1;
 constexpr uint64_t SW_CARRIED = 1ull << 55;
@@ -156,6 +198,7 @@ struct SweepDev {
   int64_t st_len;
   int32_t cur;           // which copy of the double-buffered per-owner state the next push reads
   int32_t f1ct;          // e1's filter in the scatter: typed compare class (1 float, 2 int; 0 generic doubles)
+  int32_t r12;           // this push's records are SwRec12 (set per push by SweepState::run)
   const uint8_t* lk8;    // unused since round 4 (the local key is sw_local(key)); kept null
   int32_t lk_lds;
   uint32_t* cnt;         // nown * nst + 1: counts, scanned into off
@@ -500,7 +543,7 @@ inline bool getenv_flag_scatter_nopf() {
 // into registers as soon as this round's are consumed, so they are in flight while this round is
 // ranked and its scattered stores drain (tools/scatter_micro.hip: 1.44 -> 1.21 ms on 100M events
 // over 512 owners, even at one workgroup per CU)
-template <bool PF>
+template <bool PF, bool R12>
 static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchView B, const int32_t* __restrict__ key,
                                                            int* err) {
   // dynamic LDS: per-wave counts (then write cursors) [SWP_WAVES][nown] and the running owner
@@ -520,6 +563,7 @@ static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, B
   const bool vnull = D.vtag == T_NULL, vflt = D.vtag == T_FLOAT;
   int e = 0;
   bool wide = false;  // some ts beyond base +- 2^30: the lean solve's 32-bit ts do not hold
+  bool r12o = false;  // R12: some ts beyond base +- 2^22 (the 12-byte record's 23 bits)
   int64_t tmax = INT64_MIN;
   int32_t pk[PF ? SWP_SUB : 1];  // PF: the next round's raw key / ts / value
   int64_t pt[PF ? SWP_SUB : 1];
@@ -578,6 +622,7 @@ static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, B
         const int64_t rel = t - base;
         if (!sw_rel_ok(rel)) e |= SWE_RANGE;
         wide |= rel >= (1ll << 30) || rel < -(1ll << 30);
+        if (R12) r12o |= rel >= SW_R12_SPAN || rel < -SW_R12_SPAN;
         const bool nl = (kk[s] & 0x40000000) != 0;
         double af = 0.0, ai = 0.0;
         if (D.f1ct == 0) sw_conv(rec[s].v, vflt, af, ai);
@@ -633,13 +678,22 @@ static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, B
       // (vmcnt(8)), not for these stores too
       const bool ok = own[s] != 0xffffffffu;
       const int64_t dst = ok ? (int64_t)wcw[ok ? own[s] : 0u] + rk[s] : D.trash;
-      D.recs[dst] = rec[s];
+      if constexpr (R12) {
+        SwRec12 r;
+        r.kt = (uint32_t)(rec[s].kt >> 56) << 24 | ((rec[s].kt & SW_F1) ? 1u << 23 : 0u) |
+               ((uint32_t)(int32_t)sw_ts(rec[s].kt) & 0x7FFFFFu);
+        r.ref = rec[s].ref;
+        r.v = rec[s].v;
+        reinterpret_cast<SwRec12*>(D.recs)[dst] = r;
+      } else {
+        D.recs[dst] = rec[s];
+      }
     }
 #endif
     __syncthreads();
   }
   if (e) atomicOr(err, e);
-  if (wide) atomicOr(D.tsmax + 1, 1ull);
+  if (wide || r12o) atomicOr(D.tsmax + 1, (wide ? 1ull : 0ull) | (r12o ? 2ull : 0ull));
   // running max of ts (the engine clock after the push)
   for (int d = 32; d > 0; d >>= 1) tmax = max(tmax, (int64_t)__shfl_xor((long long)tmax, d, 64));
   if (lane == 0 && tmax != INT64_MIN) atomicMax(D.tsmax, (unsigned long long)tmax ^ (1ull << 63));
@@ -1810,12 +1864,13 @@ struct SweepState {
       D.lk8 = nullptr;
       D.lk_lds = 0;
       const size_t lds = (size_t)(SWP_WAVES + 1) * nown * 4;
-      if (lds > 65536 &&
-          (hipFuncSetAttribute((const void*)k_sw_scatter<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-               hipSuccess ||
-           hipFuncSetAttribute((const void*)k_sw_scatter<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-               hipSuccess))
-        throw std::runtime_error("sweep: scatter LDS request refused");
+      if (lds > 65536) {
+        const void* fs[4] = {(const void*)k_sw_scatter<false, false>, (const void*)k_sw_scatter<true, false>,
+                             (const void*)k_sw_scatter<false, true>, (const void*)k_sw_scatter<true, true>};
+        for (const void* f : fs)
+          if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            throw std::runtime_error("sweep: scatter LDS request refused");
+      }
     }
     int64_t nc = (int64_t)nown * nst_max + 1;
     al(D.cnt, nc);
@@ -1930,13 +1985,13 @@ struct SweepState {
     size_t tb = tmp_bytes;
     (void)rocprim::exclusive_scan(tmp, tb, D.cnt, D.off, 0u, nc, rocprim::plus<uint32_t>(), s);
     kt.mark("sw_scatter", s);
-    const size_t lds = (size_t)(SWP_WAVES + 1) * D.nown * 4;
-    if (!B.stream && !B.nulls[0] && !getenv_flag_scatter_nopf())
-      k_sw_scatter<true><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
-    else
-      k_sw_scatter<false><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
+    const bool win = win_push_for(B);
+    // 12-byte records when the lean solve takes the push (k_sw_win, k_sw_solve and k_sw_spill read
+    // the 16-byte form: a push the lean solve hands back is scattered again, rescatter16)
+    D.r12 = !win && lean_push_for(B) && !D.spill_on && !r16_env() ? 1 : 0;
+    scatter(B, key, err, s);
     last_win = false;
-    if (win_push_for(B)) {
+    if (win) {
       const int64_t units = (B.n + SWW_U - 1) / SWW_U;
       if (units > w_units) throw std::runtime_error("sweep: k_sw_win units beyond the batch capacity");
       (void)hipMemsetAsync(D.w_ticket, 0, sizeof(uint32_t), s);
@@ -1954,6 +2009,30 @@ struct SweepState {
     } else {
       solve(B, O, err, s, kt);
     }
+  }
+
+  static bool r16_env() {
+    static const bool v = getenv("SHP_SW_R16") != nullptr;  // A/B: the 16-byte records on every push
+    return v;
+  }
+  void scatter(const BatchView& B, const int32_t* key, int* err, hipStream_t s) {
+    const size_t lds = (size_t)(SWP_WAVES + 1) * D.nown * 4;
+    const bool pf = !B.stream && !B.nulls[0] && !getenv_flag_scatter_nopf();
+    if (pf && D.r12) k_sw_scatter<true, true><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
+    else if (pf) k_sw_scatter<true, false><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
+    else if (D.r12) k_sw_scatter<false, true><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
+    else k_sw_scatter<false, false><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
+  }
+  // the push's records again in the 16-byte form, for the solves that read it (same counts and
+  // offsets; the overflow flags of the 12-byte pass are cleared, the wide flag set again if so)
+  bool rescatter16(const BatchView& B, const int32_t* key, int* err, hipStream_t s, KTimer& kt) {
+    if (!D.r12) return false;
+    D.r12 = 0;
+    (void)hipMemsetAsync(D.tsmax, 0, 2 * sizeof(unsigned long long), s);
+    kt.mark("sw_scatter16", s);
+    scatter(B, key, err, s);
+    kt.mark(nullptr, s);
+    return true;
   }
 
   // does this push run k_sw_lean (so SWE_LEAN may come back and ask for solve())?

@@ -134,8 +134,11 @@ __device__ __forceinline__ void sl_expand_block(uint8_t* scr, uint32_t lane, uin
 // HS: the batch carries a seq column (B.seq).  A template parameter, not a branch: with both
 // variants in one body the compiler's wait counters, merging the variant that loads seqs with the
 // one that does not, held the emission's stores at the scanner step (s_waitcnt vmcnt(0)).
-template <int CT, int OPC, bool AGG = false, bool HS = false>
+// R: the scatter's record form (SwRec12 for the pushes it takes since round 5, SwRec after a k_sw_win
+// hand-back)
+template <int CT, int OPC, bool AGG = false, bool HS = false, class R = SwRec12>
 __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView B, MatchOut O, int* err) {
+  const R* recs = reinterpret_cast<const R*>(D.recs);
   using T = typename SwTy<CT>::T;
   __shared__ SwLeanSmem S;
   __shared__ double ag[AGG ? 2 * 256 : 1];  // AGG: per local key (running sum, count) before the chunk emitted next
@@ -215,13 +218,19 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     if (x == 0 || D.c_lk[rd][c - 1] != lk) S.ckf[0][lk] = (uint16_t)x;
   }
   int cur = 0;
-  SwRec pf[SL_R];
+  using RR = SwRecReg<R>;
+  constexpr bool R12 = std::is_same<R, SwRec12>::value;
+  typename RR::T pf[SL_R];
+  // (12-byte records: every lane loads, past the region's end its last record -- unused -- so the
+  // loads land in the loop's registers instead of merging with their old values)
+  auto pload = [&](int64_t i, typename RR::T& x) __attribute__((always_inline)) {
+    if constexpr (R12) x = RR::load(recs, min(i, re - 1));
+    else if (i < re) x = RR::load(recs, i);
+  };
 #pragma unroll
-  for (int s = 0; s < SL_R; s++) {
-    const int jj = (int)w * (64 * SL_R) + s * 64 + (int)lane;
-    if (rb + jj < re) pf[s] = D.recs[rb + jj];
-  }
-  uint64_t tbk = D.recs[rb].kt;
+  for (int s = 0; s < SL_R; s++) pload(rb + (int)w * (64 * SL_R) + s * 64 + (int)lane, pf[s]);
+  auto rawkt = [&](int64_t i) __attribute__((always_inline)) -> uint64_t { return (uint64_t)recs[i].kt; };
+  uint64_t tbk = rawkt(rb);  // (decoded where the chunk starts)
   // 6. emit (a chunk's matches are written between barriers A and B of the next chunk, once the
   //    last wave through the chunk has reserved its output range with one global atomic):
   //    slot = offset(q) + (closes(q) - 1 - later), later = closers of q nearer than p
@@ -448,14 +457,14 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
   for (int64_t cb = rb; cb < re; cb += SL_CHUNK, ci++) {
     const int nchunk = (int)min((int64_t)SL_CHUNK, re - cb);
     const int nx = cur ^ 1;
-    const int32_t tb32 = (int32_t)(uint32_t)tbk;  // chunk base, batch-relative (|.| < 2^30)
+    const int32_t tb32 = R12 ? sw_rec_ts32(SwRec12{(uint32_t)tbk, 0u, 0u}) : (int32_t)(uint32_t)tbk;  // chunk base, batch-relative
     // 1. rank by local key (stable: wave-major, then slot, then lane = arrival order)
     uint32_t rk[SL_R], bin[SL_R];
 #pragma unroll
     for (int s = 0; s < SL_R; s++) {
       const int j = (int)w * (64 * SL_R) + s * 64 + (int)lane;
       const bool valid = j < nchunk;
-      const uint32_t lk = valid ? (uint32_t)(pf[s].kt >> 56) : 0u;
+      const uint32_t lk = valid ? sw_rec_lk(pf[s]) : 0u;
       const uint64_t peers = sw_match_peers(lk, lkbits, valid);
       bin[s] = valid ? lk : 0xFFFFu;
       rk[s] = 0;
@@ -552,11 +561,11 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
     for (int s = 0; s < SL_R; s++) {
       if (bin[s] == 0xFFFFu) continue;
       const uint32_t p = S.wc[w][bin[s]] + rk[s];
-      const int32_t rel = (int32_t)(uint32_t)pf[s].kt - tb32;
+      const int32_t rel = sw_rec_ts32(pf[s]) - tb32;
       if (rel > (int32_t)SW_TS_SPAN || rel < -(int32_t)SW_TS_SPAN) S.flag = 1;
       S.tv[p] = make_int2(rel, (int32_t)pf[s].v);
       S.meta[p] = bin[s] | (S.binoff[bin[s] + 1] << 8) | ((uint32_t)S.fe[bin[s]] << 20);
-      S.ref[p] = pf[s].ref | ((pf[s].kt & SW_F1) ? 0x80000000u : 0u);
+      S.ref[p] = pf[s].ref | (sw_rec_f1(pf[s]) ? 0x80000000u : 0u);
     }
     {
       const int ncur = S.cn[cur];
@@ -581,9 +590,9 @@ __global__ __launch_bounds__(SL_THREADS, 4) void k_sw_lean(SweepDev D, BatchView
 #pragma unroll
       for (int s = 0; s < SL_R; s++) {
         const int jj = (int)w * (64 * SL_R) + s * 64 + (int)lane;
-        if (nbk + jj < re) pf[s] = D.recs[nbk + jj];
+        pload(nbk + jj, pf[s]);
       }
-      if (nbk < re) tbk = D.recs[nbk].kt;
+      if (nbk < re) tbk = rawkt(nbk);
     }
     __syncthreads();  // C
     SL_STAMP(3);

@@ -9,9 +9,14 @@ namespace shp {
 void sw_launch_lean_agg(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                         const MatchOut& O, int* err) {
 #define SA_CASE(c, p) \
-  case c * 8 + p:                                                                       \
-    if (B.seq) k_sw_lean<c, p, true, true><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);  \
-    else k_sw_lean<c, p, true, false><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);       \
+  case c * 8 + p:                                                                                        \
+    if (D.r12) {                                                                                         \
+      if (B.seq) k_sw_lean<c, p, true, true, SwRec12><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);        \
+      else k_sw_lean<c, p, true, false, SwRec12><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);             \
+    } else {                                                                                             \
+      if (B.seq) k_sw_lean<c, p, true, true, SwRec><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);          \
+      else k_sw_lean<c, p, true, false, SwRec><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);               \
+    }                                                                                                    \
     break;
   switch (ct * 8 + opc) {
     SA_CASE(1, 1) SA_CASE(1, 2) SA_CASE(1, 3) SA_CASE(1, 4) SA_CASE(1, 5) SA_CASE(1, 6)
@@ -36,9 +41,14 @@ void sw_launch_solve(int nt1, int nt2, int ct, unsigned grid, hipStream_t s, con
 void sw_launch_lean(int ct, int opc, unsigned grid, hipStream_t s, const SweepDev& D, const BatchView& B,
                     const MatchOut& O, int* err) {
 #define SL_CASE(c, p) \
-  case c * 8 + p:                                                                        \
-    if (B.seq) k_sw_lean<c, p, false, true><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);  \
-    else k_sw_lean<c, p, false, false><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);       \
+  case c * 8 + p:                                                                                        \
+    if (D.r12) {                                                                                         \
+      if (B.seq) k_sw_lean<c, p, false, true, SwRec12><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);       \
+      else k_sw_lean<c, p, false, false, SwRec12><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);            \
+    } else {                                                                                             \
+      if (B.seq) k_sw_lean<c, p, false, true, SwRec><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);         \
+      else k_sw_lean<c, p, false, false, SwRec><<<grid, SL_THREADS, 0, s>>>(D, B, O, err);              \
+    }                                                                                                    \
     break;
   switch (ct * 8 + opc) {
     SL_CASE(1, 1) SL_CASE(1, 2) SL_CASE(1, 3) SL_CASE(1, 4) SL_CASE(1, 5) SL_CASE(1, 6)

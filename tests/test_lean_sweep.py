@@ -168,6 +168,32 @@ def test_wide_push_falls_back_exactly():
     assert eng.stat("pushes") == 2 and eng.stat("lean_pushes") == 2 and eng.stat("lean_fallbacks") == 1
 
 
+@pytest.mark.parametrize("agg", [False, True], ids=["pairs", "avg"])
+def test_push_beyond_12_byte_records_rescatters(agg):
+    """The scatter writes 12-byte records (ts in 23 bits around the push's first ts) for the lean
+    solve; a push spanning more than 2^22 ms (a jump of ~2.3 h in its middle) overflows them and is
+    scattered again in the 16-byte form, the lean solve re-running it (no exact-kernel fallback);
+    the next, narrow push is back on the 12-byte records.  Output equal to the oracle's."""
+    rng = np.random.default_rng(9)
+    n, keys = 40_000, 500
+    ts = 1_000_000 + np.arange(n, dtype=np.int64) * 5
+    ts[n // 2:] += 1 << 23
+    key = rng.integers(0, keys, n).astype(np.int32)
+    v = (rng.integers(0, 10000, n) / 100.0).astype(np.float32)
+    app = _app(within="1 sec")
+    if agg:
+        app = app.replace("select e1.v as a, e2.v as b", "select avg(e2.v) as a")
+    cq = _cq(app)
+    want = _push_all(OracleEngine(cq.program_json(), 0), ts, key, v, 30_000)
+    eng = _eng(cq, keys, 1 << 15)
+    got = _push_all(eng, ts, key, v, 30_000)
+    if not agg:
+        assert compare(want, got) is None, compare(want, got)
+        assert sum(len(x) for x in want.values()) > 1000
+    assert eng.stat("pushes") == 2 and eng.stat("lean_fallbacks") == 0
+    assert eng.stat("sweep_r16_reruns") == 1
+
+
 @pytest.mark.parametrize("fn", ["avg", "max"])
 def test_lean_agg_closers_with_many_matches(fn):
     """SHP_LAYOUT_AGG through k_sw_lean where one event closes up to ~200 candidates of its key

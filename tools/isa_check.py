@@ -98,8 +98,7 @@ def collect():
         dm = _demangle(list(lw))
         for mname, v in lw.items():
             d = dm[mname]
-            base = d.split("(")[0].split("::")[-1]
-            base = re.sub(r"<.*", "", base)
+            base = re.sub(r"<.*", "", d.split("(")[0]).split("::")[-1]
             if base.startswith(HOT):
                 out[f"{u}:{d.split('(')[0]}"] = v
     return out
