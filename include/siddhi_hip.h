@@ -52,10 +52,11 @@ typedef struct shp_config {
   int64_t start_clock;     /* event-time clock at start() (0 in playback mode) */
   int32_t force_general;   /* 0 auto; 1 general NFA lanes only; 2 no sweep path (scan kernels or
                               lanes); 3 sweep path whenever the shape allows (any key count).
-                              The count-sequence path (3) is taken for its shape unless 1.
-                              4: the logical-absent path for the playback pattern `every (x=X and
-                              y=Y) -> not Z for T [within W]` (labs.h): needs non-decreasing
-                              timestamps per key (a push breaking that fails, engine unchanged). */
+                              The count-sequence path (3) and the logical-absent path (4, the
+                              playback pattern `every (x=X and y=Y) -> not Z for T [within W]`,
+                              exact for any timestamp order; labs.h) are taken for their shapes
+                              unless 1.  4: require the logical-absent path (create fails for
+                              another shape). */
   int32_t profile_kernels; /* 1: time every kernel of a push with HIP events (shp_last_kernel_ms) */
   int32_t match_layout;    /* SHP_LAYOUT_FULL (0), SHP_LAYOUT_PAIRS (1), SHP_LAYOUT_AGG (2),
                               SHP_LAYOUT_PAIRS32 (3), SHP_LAYOUT_CHAIN32 (4) or SHP_LAYOUT_COMPACT (5);
@@ -79,7 +80,7 @@ typedef struct shp_config {
  * value after that match, double), in per-key emission order. The aggregate state per key
  * carries across pushes. Null values in the aggregated column are rejected (SHP_ERR_UNSUPPORTED). */
 #define SHP_LAYOUT_AGG 2
-/* CHAIN32 (count-sequence path, `every e1=S[f1]<1:M>, e2=S[f2]` in a partition): `refs` holds m
+/* CHAIN32 (count-sequence path, `[every] e1=S[f1]<min:M>, e2=S[f2]` in a partition): `refs` holds m
  * uint32 words, word = e2's index in the pushed batch (bits 0-27) | L << 28.  The match's e1 chain
  * is the L events of e2's partition key immediately before e2 in that key's arrival order (the
  * pattern is a sequence: CountPreStateProcessor.java:53-95 keeps them consecutive), some possibly
@@ -222,9 +223,10 @@ int shp_engine_num_states(const shp_engine* e);
  * core/util/parser/helper/QueryParserHelper.java:161-167). */
 int shp_engine_state_stream(const shp_engine* e, int state);
 /* Which kernels the engine runs: 2 = sweep (owner partition + LDS sweep), 1 = specialised 2-state
- * scan kernel, 0 = general NFA lanes, 3 = count-sequence automaton (`every e1=S[f1]<1:M>, e2=S[f2]`
- * with f2 over e2 and e1[last], M <= 8, no within; siddhi_amd/csrc/cseq.h), 4 = logical-absent
- * (opt-in, force_general 4; siddhi_amd/csrc/labs.h).  A path-3 snapshot
+ * scan kernel, 0 = general NFA lanes, 3 = count-sequence automaton (`[every] e1=S[f1]<min:M>,
+ * e2=S[f2]` with f2 over e2 and e1[last], 1 <= min <= M <= 8, no within; siddhi_amd/csrc/cseq.h),
+ * 4 = logical-absent (`every (x and y) -> not z for T` in playback: the default for that shape,
+ * exact for any timestamp order; siddhi_amd/csrc/labs.h).  A path-3 snapshot
  * describes each key as {"e1": {"Count": L, "PendingStateEventList": [the chain partial]},
  * "LastEvent": {seq, ts}}. */
 int shp_engine_path(const shp_engine* e);
