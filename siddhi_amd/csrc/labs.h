@@ -134,6 +134,7 @@ struct LabsDev {
   int32_t seg;       // k_labs_w segments per key (LA_H; 1: none) -- the slot stride of cm / om / rec
   uint32_t warm;     // warm-up events before a cut (LA_WARM; SHP_LABS_WARM for tests)
   struct LaSnap* snap[2];  // segment boundary states: [0] warmed-up start of segment h, [1] end of h - 1
+  int64_t* rc;             // the push's clock at the end of each 64-event block (k_labs_out's coarse search)
   int32_t pad2;
   unsigned long long* stamps;  // diagnostic build (SHP_SW_STAMPS): k_labs_w phase cycles per key
   LaRec* rec;        // k_labs_w's records, per key region (la_region)
@@ -1546,6 +1547,16 @@ static __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B,
     }
     const LaRec x = rec[r];
     int64_t a = x.flo, b = min((int64_t)x.fhi, B.n - 1);
+    if (D.rc && a < b) {  // the 64-event block first reaching due (rc: each block's last clock), then within it
+      int64_t ja = a >> 6, jb = b >> 6;
+      while (ja < jb) {
+        const int64_t mid = ja + ((jb - ja) >> 1);
+        if (D.rc[mid] >= x.due) jb = mid;
+        else ja = mid + 1;
+      }
+      a = max(a, ja << 6);
+      b = min(b, (ja << 6) + 63);
+    }
     while (a < b) {
       const int64_t mid = a + ((b - a) >> 1);
       if (B.rmax[mid] >= x.due) b = mid;
@@ -1591,6 +1602,11 @@ static __global__ __launch_bounds__(64) void k_labs_segcheck(LabsDev D, const ui
   }
   if ((uint32_t)lane < nef && (uint32_t)lane < b.nef) bad |= a.qe[lane] != b.qe[lane];
   if (__ballot(bad) && lane == 0) atomicOr(err, LA_SEGMISS);
+}
+
+static __global__ void k_labs_coarse(const int64_t* __restrict__ rmax, int64_t n, int64_t* __restrict__ rc) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((j << 6) < n) rc[j] = rmax[min((j << 6) + 63, n - 1)];
 }
 
 // a key's pairs and queue entries into rings of another capacity (tier change), heads reset to 0
@@ -1723,6 +1739,7 @@ struct LabsState {
     wave_ok = own(D.fx, 1) && own(D.fy, 2) && !getenv("SHP_NO_LABS_W");
     if (!wave_ok) D.seg = 1;
     if (wave_ok) al(D.rec, la_region((uint32_t)std::min<int64_t>(cap, 0xFFFFFFFFll), max_keys * D.seg) + 1);
+    if (wave_ok) al(D.rc, (cap + 63) / 64 + 1);
     if (D.seg > 1) {
       al(D.snap[0], (int64_t)max_keys * D.seg + 1);
       al(D.snap[1], (int64_t)max_keys * D.seg + 1);
@@ -1770,6 +1787,7 @@ struct LabsState {
       size_t tb = tmp_bytes;
       (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)gs, rocprim::plus<uint32_t>(), s);
       kt.mark("labs_out", s);
+      if (D.rc && B.n > 0) k_labs_coarse<<<(unsigned)(((B.n + 63) / 64 + 255) / 256), 256, 0, s>>>(B.rmax, B.n, D.rc);
       k_labs_out<<<(gs + 3) / 4, 256, 0, s>>>(D, B, O, kbeg, kcnt, H, err);
       kt.mark(nullptr, s);
       return;
@@ -1892,7 +1910,7 @@ struct LabsState {
     }
     if (D.wtmp) (void)hipFree(D.wtmp);
     if (D.ftmp) (void)hipFree(D.ftmp);
-    void* qs[] = {D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp, D.maxstep, ms_cnt, ms_off, D.snap[0], D.snap[1]};
+    void* qs[] = {D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp, D.maxstep, ms_cnt, ms_off, D.snap[0], D.snap[1], D.rc};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = LabsDev{};

@@ -10,11 +10,11 @@ for c in 2 3b 4 5; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats_c$c -o run -- python3 -u bench.py --config $c $Q > gpurun_out/stats_c$c.log 2>&1 || { tail -5 gpurun_out/stats_c$c.log; exit 1; }
   echo "stats c$c done"
 done
-bash tools/pmc_run.sh > gpurun_out/pmc_run_c2.log 2>&1 || { tail -5 gpurun_out/pmc_run_c2.log; exit 1; }
+BENCH_ARGS="--no-expanded" bash tools/pmc_run.sh > gpurun_out/pmc_run_c2.log 2>&1 || { tail -5 gpurun_out/pmc_run_c2.log; exit 1; }
 echo "pmc c2 done"
 for c in 3b 4 5; do
   k=1000000; [ $c = 4 ] && k=1000; [ $c = 5 ] && k=100000
-  NO_LV=1 CFG=$c KEYS=$k bash tools/pmc_cfg.sh > gpurun_out/pmc_cfg_$c.log 2>&1 || { tail -5 gpurun_out/pmc_cfg_$c.log; exit 1; }
+  BENCH_ARGS="--no-expanded" NO_LV=1 CFG=$c KEYS=$k bash tools/pmc_cfg.sh > gpurun_out/pmc_cfg_$c.log 2>&1 || { tail -5 gpurun_out/pmc_cfg_$c.log; exit 1; }
   echo "pmc c$c done"
 done
 echo done
