@@ -14,6 +14,7 @@ for c in ${CONFIGS:-c3b c5 c4 c3 c1}; do
   case $c in
     c2) run c2 400 ;;
     c3b) run c3b 400 --config 3b ;;
+    c3bfull) run c3bfull 400 --config 3b --cseq-layout full --no-cpu-baseline ;;
     c5) run c5 400 --config 5 ;;
     c4) run c4 500 --config 4 ;;
     c4d) run c4d 500 --config 4 --disorder 0.01 --no-cpu-baseline ;;
