@@ -394,10 +394,10 @@ class _EngineView:
 
 def _path_desc(eng, layout):
     d = PATHS.get(eng.path, str(eng.path))
-    if eng.path == 3 and layout == "chain32":
+    if eng.path == 3:
         own = native_stat(eng, "cseq_owner")
         d = ("count-sequence automaton by owners (owner multisplit + per-owner key order in LDS, cseq_own.h)"
-             if own else d) + ", CHAIN32 words"
+             if own else d) + (", CHAIN32 words" if layout == "chain32" else ", FULL rows")
     return d
 
 
