@@ -1150,6 +1150,7 @@ struct CseqState {
   }
 
   // the owner path over one push (cseq_own.h): count, scan, scatter, per-owner run
+  bool stg_attr = false;  // the staged scatter's LDS limit is set (once per engine)
   void run_own(const BatchView& B, const int32_t* key, const int32_t* stream, const MatchOut& O, int* err,
                hipStream_t s, KTimer& kt) {
     const int64_t n = B.n;
@@ -1164,8 +1165,25 @@ struct CseqState {
     kt.mark("co_scatter", s);
     const size_t lds = (size_t)(CO_SCT_WAVES + 1) * P.nown * 4;
     const bool pf = !stream && !B.nulls[0] && !getenv_flag_scatter_nopf();
+    // the LDS-staged scatter (round 5: co_scatter 1.21 -> 1.08 ms on C3', profiles/r05_scatter_stage_ab.txt);
+    // SHP_SCATTER_NOSTAGE=1 is the A/B back to the direct scattered stores
+    static const bool nostage = getenv("SHP_SCATTER_NOSTAGE") != nullptr;
+    const bool stg = pf && !nostage;
+    const size_t stg_lds = (size_t)(CO_SCT_WAVES + 2) * P.nown * 4 + (size_t)4 * CO_SCT_ROUND * 4;
+    if (stg && !stg_attr) {
+      const void* fs[3] = {(const void*)k_co_scatter<0, true, true>, (const void*)k_co_scatter<1, true, true>,
+                           (const void*)k_co_scatter<2, true, true>};
+      for (const void* f : fs)
+        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)((size_t)(CO_SCT_WAVES + 2) * CO_MAXOWN * 4 + (size_t)4 * CO_SCT_ROUND * 4)) !=
+            hipSuccess)
+          throw std::runtime_error("count-sequence: staged scatter LDS request refused");
+      stg_attr = true;
+    }
 #define CO_SCT(N)                                                                              \
-  if (pf) k_co_scatter<N, true><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream); \
+  if (stg) {                                                                                   \
+    k_co_scatter<N, true, true><<<(unsigned)P.nst, CO_SCT_THREADS, stg_lds, s>>>(P, D, B, key, stream); \
+  } else if (pf) k_co_scatter<N, true><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream); \
   else k_co_scatter<N, false><<<(unsigned)P.nst, CO_SCT_THREADS, lds, s>>>(P, D, B, key, stream);
     switch (D.f1.n) {
       case 0: CO_SCT(0) break;

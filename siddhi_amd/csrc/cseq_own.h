@@ -112,10 +112,15 @@ static __global__ __launch_bounds__(CO_CNT_THREADS) void k_co_count(CoDev P, Bat
 // offsets [nown]
 // PF (no stream column, no null bytes): the next round's keys and values are loaded as soon as this
 // round's are consumed (as k_sw_scatter's PF path)
-template <int NT1, bool PF>
+// STG (PF only, round 5, the default for PF): the round's records placed in LDS in owner order, then
+// written out by position, so a store instruction covers whole owner runs (k_sw_scatter's STG form);
+// extra LDS: lofs [nown] and the stage, CO_SCT_ROUND x 4 words (104 KB at 1024 owners).  Measured
+// 1.21 -> 1.08 ms on C3' (profiles/r05_scatter_stage_ab.txt); the sweep's 12-byte scatter lost with it.
+template <int NT1, bool PF, bool STG = false>
 __global__ __launch_bounds__(CO_SCT_THREADS) void k_co_scatter(CoDev P, CseqDev C, BatchView B,
                                                                const int32_t* __restrict__ key,
                                                                const int32_t* __restrict__ stream) {
+  static_assert(!STG || PF, "the staged scatter is built for the prefetched form");
   extern __shared__ uint32_t co_dyn[];
   const int nown = P.nown;
   uint32_t* grun = co_dyn + CO_SCT_WAVES * nown;
@@ -190,6 +195,67 @@ __global__ __launch_bounds__(CO_SCT_THREADS) void k_co_scatter(CoDev P, CseqDev 
 #pragma unroll
     for (int s = 0; s < CO_SCT_SUB; s++) rk[s] += __shfl(old[s], (int)ld[s], 64);
     __syncthreads();
+    if constexpr (STG) {
+      __shared__ uint32_t stg_w[CO_SCT_WAVES];
+      uint32_t* lofs = grun + nown;
+      uint32_t* sv = lofs + nown;
+      uint32_t* sg = sv + CO_SCT_ROUND;
+      uint32_t* slk = sg + CO_SCT_ROUND;
+      uint32_t* sdst = slk + CO_SCT_ROUND;
+      const int per = (nown + CO_SCT_THREADS - 1) / CO_SCT_THREADS;
+      const int b0 = min(nown, (int)threadIdx.x * per), b1 = min(nown, b0 + per);
+      uint32_t tsum = 0;
+      for (int b = b0; b < b1; b++)
+#pragma unroll
+        for (int ww = 0; ww < CO_SCT_WAVES; ww++) tsum += co_dyn[ww * nown + b];
+      const uint32_t inc = dpp_incl_add(tsum, lane);
+      if (lane == 63) stg_w[w] = inc;
+      __syncthreads();
+      uint32_t tot = 0, wpre = 0;
+#pragma unroll
+      for (int ww = 0; ww < CO_SCT_WAVES; ww++) {
+        const uint32_t t = stg_w[ww];
+        wpre += ww < (int)w ? t : 0u;
+        tot += t;
+      }
+      uint32_t g = wpre + inc - tsum;
+      for (int b = b0; b < b1; b++) {
+        lofs[b] = g;
+#pragma unroll
+        for (int ww = 0; ww < CO_SCT_WAVES; ww++) {
+          const uint32_t c = co_dyn[ww * nown + b];
+          co_dyn[ww * nown + b] = g;
+          g += c;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < CO_SCT_SUB; s++)
+        if (own[s] != 0xffffffffu) {
+          const uint32_t o = own[s];
+          const uint32_t p = wcw[o] + rk[s];
+          sv[p] = rec[s].v;
+          sg[p] = rec[s].g;
+          slk[p] = rec[s].lk;
+          sdst[p] = grun[o] + (p - lofs[o]);
+        }
+      __syncthreads();
+      // only the round's records are stored (the recs array has no trash slot)
+#pragma unroll
+      for (int q = 0; q < CO_SCT_PER_CFG; q++) {
+        const uint32_t p = (uint32_t)(q * CO_SCT_THREADS) + threadIdx.x;
+        if (p < tot) {
+          CoRec r;
+          r.v = sv[p];
+          r.g = sg[p];
+          r.lk = slk[p];
+          P.recs[sdst[p]] = r;
+        }
+      }
+      for (int b = b0; b < b1; b++) grun[b] += (b + 1 < nown ? lofs[b + 1] : tot) - lofs[b];
+      __syncthreads();
+      continue;
+    }
     for (int b = threadIdx.x; b < nown; b += CO_SCT_THREADS) {
       uint32_t g = grun[b];
 #pragma unroll

@@ -543,11 +543,16 @@ inline bool getenv_flag_scatter_nopf() {
 // into registers as soon as this round's are consumed, so they are in flight while this round is
 // ranked and its scattered stores drain (tools/scatter_micro.hip: 1.44 -> 1.21 ms on 100M events
 // over 512 owners, even at one workgroup per CU)
-template <bool PF, bool R12>
+// STG (PF + R12 only, round 5, A/B): the round's records are placed in LDS in owner order first and
+// then written out by position, so one store instruction covers whole owner runs (consecutive
+// lanes, consecutive addresses) instead of 64 scattered 12-byte records.  Extra LDS: the round-local
+// owner starts [nown] and the stage, SWP_ROUND x (kt, ref, v, destination) words.
+template <bool PF, bool R12, bool STG = false>
 static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, BatchView B, const int32_t* __restrict__ key,
                                                            int* err) {
+  static_assert(!STG || (PF && R12), "the staged scatter is built for the prefetched 12-byte form");
   // dynamic LDS: per-wave counts (then write cursors) [SWP_WAVES][nown] and the running owner
-  // offsets [nown]
+  // offsets [nown] (STG: then lofs [nown] and the stage)
   extern __shared__ uint32_t sw_dyn[];
   const int nown = D.nown;
   uint32_t* grun = sw_dyn + SWP_WAVES * nown;
@@ -656,6 +661,69 @@ static __global__ __launch_bounds__(SWP_THREADS) void k_sw_scatter(SweepDev D, B
 #pragma unroll
     for (int s = 0; s < SWP_SUB; s++) rk[s] += __shfl(old[s], (int)ld[s], 64);
     __syncthreads();
+    if constexpr (STG) {
+      __shared__ uint32_t stg_w[SWP_WAVES];
+      uint32_t* lofs = grun + nown;  // round-local start of each owner's records
+      uint32_t* skt = lofs + nown;
+      uint32_t* sref = skt + SWP_ROUND;
+      uint32_t* sv = sref + SWP_ROUND;
+      uint32_t* sdst = sv + SWP_ROUND;
+      // round totals per owner (thread t: owners [t * per, t * per + per)), block exclusive scan
+      const int per = (nown + SWP_THREADS - 1) / SWP_THREADS;
+      const int b0 = min(nown, (int)threadIdx.x * per), b1 = min(nown, b0 + per);
+      uint32_t tsum = 0;
+      for (int b = b0; b < b1; b++)
+#pragma unroll
+        for (int ww = 0; ww < SWP_WAVES; ww++) tsum += sw_dyn[ww * nown + b];
+      const uint32_t inc = dpp_incl_add(tsum, lane);
+      if (lane == 63) stg_w[w] = inc;
+      __syncthreads();
+      uint32_t tot = 0, wpre = 0;
+#pragma unroll
+      for (int ww = 0; ww < SWP_WAVES; ww++) {
+        const uint32_t t = stg_w[ww];
+        wpre += ww < (int)w ? t : 0u;
+        tot += t;
+      }
+      uint32_t g = wpre + inc - tsum;
+      for (int b = b0; b < b1; b++) {
+        lofs[b] = g;
+#pragma unroll
+        for (int ww = 0; ww < SWP_WAVES; ww++) {
+          const uint32_t c = sw_dyn[ww * nown + b];
+          sw_dyn[ww * nown + b] = g;
+          g += c;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < SWP_SUB; s++)
+        if (own[s] != 0xffffffffu) {
+          const uint32_t o = own[s];
+          const uint32_t p = wcw[o] + rk[s];  // round-local, owner order
+          skt[p] = (uint32_t)(rec[s].kt >> 56) << 24 | ((rec[s].kt & SW_F1) ? 1u << 23 : 0u) |
+                   ((uint32_t)(int32_t)sw_ts(rec[s].kt) & 0x7FFFFFu);
+          sref[p] = rec[s].ref;
+          sv[p] = rec[s].v;
+          sdst[p] = grun[o] + (p - lofs[o]);
+        }
+      __syncthreads();
+      // a fixed store count per lane (positions past the round's records go to the trash slot), as
+      // in the unstaged form, so the next round's start waits for the prefetched loads only
+#pragma unroll
+      for (int q = 0; q < SWP_PER_LANE_CFG; q++) {
+        const uint32_t p = (uint32_t)(q * SWP_THREADS) + threadIdx.x;
+        const bool ok = p < tot;
+        SwRec12 r;
+        r.kt = skt[p];
+        r.ref = sref[p];
+        r.v = sv[p];
+        reinterpret_cast<SwRec12*>(D.recs)[ok ? (int64_t)sdst[p] : D.trash] = r;
+      }
+      for (int b = b0; b < b1; b++) grun[b] += (b + 1 < nown ? lofs[b + 1] : tot) - lofs[b];
+      __syncthreads();
+      continue;
+    }
     for (int b = threadIdx.x; b < nown; b += SWP_THREADS) {
       uint32_t g = grun[b];
 #pragma unroll
@@ -1864,6 +1932,10 @@ struct SweepState {
       D.lk8 = nullptr;
       D.lk_lds = 0;
       const size_t lds = (size_t)(SWP_WAVES + 1) * nown * 4;
+      // the staged scatter's LDS (> 64 KB at every owner count): counters, lofs and the stage
+      if (hipFuncSetAttribute((const void*)k_sw_scatter<true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)stg_lds(nown)) != hipSuccess)
+        throw std::runtime_error("sweep: staged scatter LDS request refused");
       if (lds > 65536) {
         const void* fs[4] = {(const void*)k_sw_scatter<false, false>, (const void*)k_sw_scatter<true, false>,
                              (const void*)k_sw_scatter<false, true>, (const void*)k_sw_scatter<true, true>};
@@ -2015,10 +2087,16 @@ struct SweepState {
     static const bool v = getenv("SHP_SW_R16") != nullptr;  // A/B: the 16-byte records on every push
     return v;
   }
+  static size_t stg_lds(int nown) { return (size_t)(SWP_WAVES + 2) * nown * 4 + (size_t)4 * SWP_ROUND * 4; }
+  static bool stg_env() {
+    static const bool v = getenv("SHP_SCATTER_STAGE") != nullptr;  // A/B: the LDS-staged 12-byte scatter
+    return v;
+  }
   void scatter(const BatchView& B, const int32_t* key, int* err, hipStream_t s) {
     const size_t lds = (size_t)(SWP_WAVES + 1) * D.nown * 4;
     const bool pf = !B.stream && !B.nulls[0] && !getenv_flag_scatter_nopf();
-    if (pf && D.r12) k_sw_scatter<true, true><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
+    if (pf && D.r12 && stg_env()) k_sw_scatter<true, true, true><<<D.nst, SWP_THREADS, stg_lds(D.nown), s>>>(D, B, key, err);
+    else if (pf && D.r12) k_sw_scatter<true, true><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
     else if (pf) k_sw_scatter<true, false><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
     else if (D.r12) k_sw_scatter<false, true><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
     else k_sw_scatter<false, false><<<D.nst, SWP_THREADS, lds, s>>>(D, B, key, err);
