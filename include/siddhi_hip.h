@@ -195,6 +195,13 @@ int shp_push_batch_compact(shp_engine* e, const shp_batch* in, shp_matches* out)
  * (StreamPreStateProcessor.java:364-403).  The engine's next sequence number when nothing is open.
  * Costs a snapshot (device to host copy of the state): call it when the kept rows grow, not per push. */
 int shp_engine_oldest_live_seq(shp_engine* e, int64_t* out);
+/* The earliest due time among the keys' absent-state timers of the committed state: the head of each
+ * key's Scheduler queue (a FIFO, core/util/Scheduler.java:113-127, 332).  Returns 1 and writes *out
+ * when a timer is pending, 0 when none is (the 2-state and count-sequence paths have no timers), or a
+ * negative status.  A live-mode (non-playback) host schedules a wall-clock wake-up at that time and
+ * then calls shp_advance_clock(now), as Scheduler.schedule / EventCaller.run do (:129-155, :287-326).
+ * Costs a snapshot (device to host copy of the state), as shp_engine_oldest_live_seq. */
+int shp_engine_next_due(shp_engine* e, int64_t* out);
 /* Copy the matches of the last shp_push_batch_device to host memory (none after shp_restore). */
 int shp_fetch_matches(shp_engine* e, shp_matches* out);
 int shp_advance_clock(shp_engine* e, int64_t now, shp_matches* out);

@@ -22,7 +22,6 @@ import io.siddhi.core.event.stream.StreamEvent;
 
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
-import java.util.ArrayDeque;
 import java.util.ArrayList;
 import java.util.Arrays;
 import java.util.List;
@@ -80,8 +79,10 @@ final class ColumnarBatch {
     private final NativeDictionary strings;           // string-attribute dictionary (shared with the filters)
     private long n;
     private long seq0;                                // sequence number of row 0 of the open batch
-    // rows of committed pushes still named by open partials (or not yet trimmed), oldest first
-    private final ArrayDeque<Block> history = new ArrayDeque<>();
+    // rows of committed pushes still named by open partials (or not yet trimmed), oldest first:
+    // blocks [head, size) of the list, ordered by seq0, so a match slot's row is found by bisection
+    private final ArrayList<Block> history = new ArrayList<>();
+    private int head;
     private long kept;                                // rows held in `history`
     private long floor;                               // every row below it was dropped
     private final long minTrim;
@@ -125,6 +126,14 @@ final class ColumnarBatch {
      * the query is not partitioned; streamIndex: -1 for a clock-only event (a send on a stream this
      * query does not read, which in playback still sets the app's clock). */
     void append(long timestamp, int keyId, int streamIndex, Object[] data) {
+        if (streamIndex >= 0 && n > 0 && streamAt(n - 1) < 0 && rowTs.get((int) n - 1) == timestamp) {
+            // the clock-only row the query's TimeChangeListener appended for this very send
+            // (InputHandler.send sets the clock before the event reaches the receiver): the event
+            // carries the same clock, so it takes the row's place
+            n--;
+            rows.remove(rows.size() - 1);
+            rowTs.remove(rowTs.size() - 1);
+        }
         ts.setAtIndex(JAVA_LONG, n, timestamp);
         key.setAtIndex(JAVA_INT, n, keyId);
         stream.setAtIndex(JAVA_INT, n, streamIndex);
@@ -147,6 +156,13 @@ final class ColumnarBatch {
         rows.add(data);
         rowTs.add(timestamp);
         n++;
+    }
+
+    /** A clock-only row (stream -1, no key, no values): the app clock moved to `now` with no event of
+     * this query (a send on another stream, the playback heartbeat) -- GpuStateStreamRuntime's
+     * TimeChangeListener under FlushPolicy.DEFERRED.  The engine fires the timers due by then. */
+    void appendClock(long now) {
+        append(now, 0, -1, null);
     }
 
     /** The shp_batch descriptor of the rows appended so far (host memory; shp_push_batch copies it). */
@@ -181,7 +197,7 @@ final class ColumnarBatch {
             for (int i = 0; i < t.length; i++) {
                 t[i] = rowTs.get(i);
             }
-            history.addLast(new Block(seq0, rows.toArray(new Object[0][]), t));
+            history.add(new Block(seq0, rows.toArray(new Object[0][]), t));
             kept += n;
         }
         seq0 += n;
@@ -215,16 +231,22 @@ final class ColumnarBatch {
 
     /** Drops every row below `lo`; a push partly below keeps its tail. */
     void trim(long lo) {
-        while (!history.isEmpty() && history.peekFirst().end() <= lo) {
-            kept -= history.removeFirst().rows.length;
+        while (head < history.size() && history.get(head).end() <= lo) {
+            kept -= history.get(head).rows.length;
+            history.set(head++, null);
         }
-        Block b = history.peekFirst();
-        if (b != null && b.seq0 < lo) {
-            int cut = (int) (lo - b.seq0);
-            history.removeFirst();
-            history.addFirst(new Block(lo, Arrays.copyOfRange(b.rows, cut, b.rows.length),
-                    Arrays.copyOfRange(b.ts, cut, b.ts.length)));
-            kept -= cut;
+        if (head < history.size()) {
+            Block b = history.get(head);
+            if (b.seq0 < lo) {
+                int cut = (int) (lo - b.seq0);
+                history.set(head, new Block(lo, Arrays.copyOfRange(b.rows, cut, b.rows.length),
+                        Arrays.copyOfRange(b.ts, cut, b.ts.length)));
+                kept -= cut;
+            }
+        }
+        if (head > 64 && head * 2 > history.size()) {  // drop the dead prefix, amortised
+            history.subList(0, head).clear();
+            head = 0;
         }
         floor = Math.max(floor, Math.min(lo, seq0));
     }
@@ -233,12 +255,22 @@ final class ColumnarBatch {
      * before-window data the query's MetaStreamEvent expects for that stream. */
     StreamEvent event(long seq, int outputDataSize) {
         Block block = null;
-        var it = history.descendingIterator();   // recent pushes first: most matches name them
-        while (it.hasNext()) {
-            Block b = it.next();
-            if (seq >= b.seq0 && seq < b.end()) {
-                block = b;
-                break;
+        int last = history.size() - 1;
+        if (last >= head && seq >= history.get(last).seq0) {   // the latest push: most matches name it
+            block = seq < history.get(last).end() ? history.get(last) : null;
+        } else {
+            int lo = head;
+            int hi = last;
+            while (lo <= hi) {   // the last block with seq0 <= seq
+                int mid = (lo + hi) >>> 1;
+                if (history.get(mid).seq0 <= seq) {
+                    lo = mid + 1;
+                } else {
+                    hi = mid - 1;
+                }
+            }
+            if (hi >= head && seq < history.get(hi).end()) {
+                block = history.get(hi);
             }
         }
         if (block == null) {
@@ -265,7 +297,8 @@ final class ColumnarBatch {
         List<Long> s = new ArrayList<>();
         List<Long> t = new ArrayList<>();
         List<Object[]> d = new ArrayList<>();
-        for (Block b : history) {
+        for (int h = head; h < history.size(); h++) {
+            Block b = history.get(h);
             for (int i = 0; i < b.rows.length; i++) {
                 if (b.seq0 + i >= lo) {
                     s.add(b.seq0 + i);
@@ -287,6 +320,7 @@ final class ColumnarBatch {
      * numbers become blocks) and the next push starts at the engine's restored counter. */
     void restoreRows(long[] seqs, long[] tss, Object[][] data, long nextSeq) {
         history.clear();
+        head = 0;
         kept = 0;
         int i = 0;
         while (i < seqs.length) {
@@ -294,7 +328,7 @@ final class ColumnarBatch {
             while (j < seqs.length && seqs[j] == seqs[j - 1] + 1) {
                 j++;
             }
-            history.addLast(new Block(seqs[i], Arrays.copyOfRange(data, i, j), Arrays.copyOfRange(tss, i, j)));
+            history.add(new Block(seqs[i], Arrays.copyOfRange(data, i, j), Arrays.copyOfRange(tss, i, j)));
             kept += j - i;
             i = j;
         }

@@ -33,6 +33,21 @@
  *     event) to the same batch instead of one send() per key run (GpuStateReceiver.append(ts, key,
  *     data), then endOfChunk()).
  *
+ * Egress: every match reaches the QuerySelector inside its key's partition flow (emit():
+ * SiddhiAppContext.startPartitionFlow(key) around selector.process, the caller's flow restored
+ * after), as the reference emits them -- PartitionStreamReceiver.send (:262-272) for event matches,
+ * the Scheduler's timer loop (core/util/Scheduler.java:88-97) for timer matches -- so the selector's
+ * per-key state (PartitionStateHolder.getState, core/util/snapshot/state/PartitionStateHolder.java:
+ * 43-48: aggregators, output rate limiters) is the match's key's even when one push carries many keys.
+ *
+ * Clock (queries with an absent state): the runtime registers a TimeChangeListener with the app's
+ * TimestampGenerator, as the query's Scheduler does (Scheduler.java:71-103), so a playback send on
+ * ANY stream and the @app:playback(idle.time) heartbeat (TimestampGeneratorImpl.java:105-121,
+ * 165-185) reach the engine: SYNC fires the due timers at once (shp_advance_clock, before the event
+ * that moved the clock), DEFERRED appends a clock-only row to the batch.  In live mode it keeps one
+ * wall-clock wake-up on the app's ScheduledExecutorService at the engine's earliest due time
+ * (shp_engine_next_due), as Scheduler.schedule / EventCaller.run do (:129-155, :287-326).
+ *
  * Match records come back in the engine's compact layout (SHP_LAYOUT_COMPACT through
  * shp_push_batch_compact: PAIRS32 on the sweep path, CHAIN32 on the count-sequence path, FULL on
  * the others) and are decoded here against the batch's own rows; the rows are kept by sequence
@@ -45,6 +60,7 @@
  */
 package io.siddhi.core.query.input.stream.state.gpu;
 
+import io.siddhi.core.config.SiddhiAppContext;
 import io.siddhi.core.config.SiddhiQueryContext;
 import io.siddhi.core.event.ComplexEvent;
 import io.siddhi.core.event.ComplexEventChunk;
@@ -116,6 +132,12 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
     // DEFERRED: a push that failed on the flusher thread, rethrown to the next caller (append,
     // flush, advanceClock, snapshot) so the sender sees it; the flusher keeps running
     private volatile RuntimeException deferredFailure;
+    private final boolean partitioned;             // matches are emitted inside their key's flow
+    private final boolean timers;                  // an absent state: the query listens to the app clock
+    private final SiddhiAppContext appContext;
+    private ScheduledFuture<?> wake;               // live mode: the wall-clock wake-up at the next due time
+    private long wakeAt = Long.MAX_VALUE;
+    private volatile boolean closed;
 
     /**
      * The Java host's entry point: the library lowers the query from the app text
@@ -208,6 +230,9 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         this.chainM = Math.max(1, info.countMax);
         this.strings = strings;
         this.policy = policy;
+        this.partitioned = info.partitioned;
+        this.timers = info.timers;
+        this.appContext = queryContext.getSiddhiAppContext();
         this.outputDataSize = metaStateEvent.getOutputDataAttributes() == null ? 0
                 : metaStateEvent.getOutputDataAttributes().size();
         NativeDictionary keyDict = null;
@@ -309,6 +334,11 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         } else {
             flusher = null;
             flushTask = null;
+        }
+        if (timers) {
+            // Scheduler.java:71-72: the query hears every move of the app clock -- a playback send
+            // on any stream (InputHandler.java:59-92) and the idle.time heartbeat
+            appContext.getTimestampGenerator().addTimeChangeListener(this::onTimeChange);
         }
     }
 
@@ -415,6 +445,7 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
             long seq0 = batch.commit();
             deliver(seq0, pushed);
             batch.maybeTrim(this::oldestLiveSeq);
+            scheduleWake();
         } finally {
             lock.unlock();
         }
@@ -436,6 +467,85 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         }
     }
 
+    /** The query's TimeChangeListener (Scheduler.java:71-103): the app clock moved to `now` -- a
+     * playback send on any stream (before its event reaches a receiver) or the idle heartbeat.  SYNC
+     * fires the timers due by `now` at once, as the Scheduler does inside onTimeChange; DEFERRED adds
+     * a clock-only row to the batch (absorbed by the event that follows when the send is this
+     * query's, ColumnarBatch.append), and its timer matches come with the push. */
+    void onTimeChange(long now) {
+        if (closed) {
+            return;
+        }
+        if (policy == FlushPolicy.SYNC) {
+            advanceClock(now);
+            return;
+        }
+        rethrowDeferred();
+        lock.lock();
+        try {
+            batch.appendClock(now);
+            if (batch.full()) {
+                flush();
+            }
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /** shp_engine_next_due: the earliest head of any key's timer queue, Long.MAX_VALUE when none. */
+    private long nextDue() {
+        try (Arena a = Arena.ofConfined()) {
+            MemorySegment out = a.allocate(JAVA_LONG);
+            int rc = (int) ShpNative.NEXT_DUE.invokeExact(engine, out);
+            if (rc < 0) {
+                throw new SiddhiAppRuntimeException("shp_engine_next_due: " + ShpNative.lastError(engine));
+            }
+            return rc == 1 ? out.get(JAVA_LONG, 0) : Long.MAX_VALUE;
+        } catch (RuntimeException e) {
+            throw e;
+        } catch (Throwable t) {
+            throw new SiddhiAppRuntimeException("shp_engine_next_due failed: " + t, t);
+        }
+    }
+
+    /** Live mode (not playback): keep one wake-up on the app's ScheduledExecutorService at the
+     * engine's earliest due time, as Scheduler.schedule arms the EventCaller for a queue head
+     * (Scheduler.java:129-155) and EventCaller.run re-arms for the next (:287-326).  The wake-up
+     * advances the engine to the wall clock, which fires every timer due by then.  Called under
+     * `lock` after every push. */
+    private void scheduleWake() {
+        if (!timers || closed || appContext.isPlayback()) {
+            return;
+        }
+        long due = nextDue();
+        if (due == Long.MAX_VALUE || (wake != null && !wake.isDone() && wakeAt <= due)) {
+            return;
+        }
+        if (wake != null) {
+            wake.cancel(false);
+        }
+        wakeAt = due;
+        long delay = Math.max(0, due - appContext.getTimestampGenerator().currentTime());
+        wake = appContext.getScheduledExecutorService().schedule(this::onWake, delay, TimeUnit.MILLISECONDS);
+    }
+
+    private void onWake() {
+        lock.lock();
+        try {
+            wake = null;               // this wake-up has run: advanceClock arms the next one
+            wakeAt = Long.MAX_VALUE;
+        } finally {
+            lock.unlock();
+        }
+        try {
+            if (!closed && !appContext.isPlayback()) {
+                advanceClock(appContext.getTimestampGenerator().currentTime());
+            }
+        } catch (RuntimeException e) {
+            deferredFailure = e;       // no caller on the executor's thread: the next one sees it
+        }
+    }
+
     /** TimestampGeneratorImpl.setCurrentTimestamp with no event (absent-state timers). */
     void advanceClock(long now) {
         rethrowDeferred();
@@ -452,8 +562,33 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
                 throw new SiddhiAppRuntimeException("shp_advance_clock: " + ShpNative.lastError(engine));
             }
             deliverFull();   // a clock-only event: FULL records (timer matches), no new rows
+            scheduleWake();
         } finally {
             lock.unlock();
+        }
+    }
+
+    /** One match into the QuerySelector, inside its key's partition flow (the only call of
+     * selector.process): PartitionStreamReceiver.send (:262-272) runs event matches under
+     * SiddhiAppContext.startPartitionFlow(key) and the Scheduler timer matches the same way
+     * (Scheduler.java:88-97), so the selector's per-key state is looked up under the match's key.
+     * The caller's flow (a sender's PartitionStreamReceiver.send of another key, in a batched push
+     * or when key A's timer fires on key B's event) is restored after it. */
+    private void emit(int keyId, StateEvent se) {
+        if (!partitioned) {
+            selector.process(new ComplexEventChunk<>(se, se));
+            return;
+        }
+        String prev = SiddhiAppContext.getPartitionFlowId();
+        SiddhiAppContext.startPartitionFlow(keys.string(keyId));
+        try {
+            selector.process(new ComplexEventChunk<>(se, se));
+        } finally {
+            if (prev == null) {
+                SiddhiAppContext.stopPartitionFlow();
+            } else {
+                SiddhiAppContext.startPartitionFlow(prev);
+            }
         }
     }
 
@@ -495,7 +630,7 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
             se.setType(ComplexEvent.Type.CURRENT);
             se.addEvent(0, batch.event(e1, out0));
             se.addEvent(1, batch.event(e2, out1));
-            selector.process(new ComplexEventChunk<>(se, se));
+            emit(batch.keyAt(idx), se);
         }
     }
 
@@ -541,7 +676,7 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
                     se.addEvent(0, batch.event(ring[base + t], out0));   // the count state's chain, in order
                 }
                 se.addEvent(1, batch.event(seq0 + i, out1));
-                selector.process(new ComplexEventChunk<>(se, se));
+                emit(k, se);
             }
             if (have == chainM) {
                 System.arraycopy(ring, base + 1, ring, base, chainM - 1);
@@ -559,6 +694,7 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         if (m == 0) {
             return;
         }
+        MemorySegment key = ShpNative.matchesPtr(matches, "key", m * 4);
         MemorySegment ts = ShpNative.matchesPtr(matches, "ts", m * 8);
         MemorySegment type = ShpNative.matchesPtr(matches, "type", m);
         MemorySegment refOff = ShpNative.matchesPtr(matches, "ref_off", m * 8);
@@ -584,7 +720,7 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
                     }
                 }
             }
-            selector.process(new ComplexEventChunk<>(se, se));
+            emit(key.getAtIndex(JAVA_INT, i), se);
         }
     }
 
@@ -651,8 +787,15 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         }
     }
 
-    /** State.restore(): the engine blob, then the rows and rings that travelled with it. */
+    /** State.restore(): the engine blob, then the rows and rings that travelled with it.  A state
+     * without the rows (a snapshot of an older build: GpuEngineSnapshot / StateByKey only) is refused
+     * before the engine is touched, so engine and row history never disagree. */
     void restoreFrom(Map<String, Object> m) {
+        if (!(m.get("GpuEngineSnapshot") instanceof byte[]) || !(m.get("LiveRows") instanceof Object[])
+                || !(m.get("NextSeq") instanceof Long)) {
+            throw new SiddhiAppRuntimeException("GPU state snapshot without GpuEngineSnapshot / LiveRows / NextSeq "
+                    + "(taken by an older build?): the rows its partials name are missing, not restored");
+        }
         lock.lock();
         try {
             restore((byte[]) m.get("GpuEngineSnapshot"));
@@ -690,6 +833,15 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
 
     /** SiddhiAppRuntime.shutdown for the query. */
     public void shutdown() {
+        closed = true;                 // the app clock's listener and the wake-up become no-ops
+        lock.lock();
+        try {
+            if (wake != null) {
+                wake.cancel(false);
+            }
+        } finally {
+            lock.unlock();
+        }
         if (flushTask != null) {
             flushTask.cancel(false);
             flusher.shutdown();

@@ -27,6 +27,7 @@ final class NativeDictionary implements AutoCloseable {
 
     private final MemorySegment dict;   // shp_dict*
     private final ConcurrentHashMap<String, Integer> cache = new ConcurrentHashMap<>();
+    private final ConcurrentHashMap<Integer, String> names = new ConcurrentHashMap<>();
     private final String what;
 
     /** maxIds > 0: at most that many distinct strings (a partition-key dictionary: cfg.max_keys). */
@@ -61,7 +62,33 @@ final class NativeDictionary implements AutoCloseable {
                     + " (more distinct values than the engine was created for)");
         }
         cache.putIfAbsent(s, id);
+        names.putIfAbsent(id, s);
         return id;
+    }
+
+    /** The string of id `id` (a match's partition key: the flow it is delivered in).  Ids this
+     * process interned are cached; any other comes from the library (shp_dict_string). */
+    String string(int id) {
+        String s = names.get(id);
+        if (s != null) {
+            return s;
+        }
+        try (Arena a = Arena.ofConfined()) {
+            long len = (long) ShpNative.DICT_STRING.invokeExact(dict, id, MemorySegment.NULL, 0L);
+            if (len < 0) {
+                throw new SiddhiAppRuntimeException(what + ": no string for id " + id + " ("
+                        + ShpNative.codeName((int) len) + ")");
+            }
+            MemorySegment out = a.allocate(len + 1);
+            long got = (long) ShpNative.DICT_STRING.invokeExact(dict, id, out, len + 1);
+            s = new String(out.asSlice(0, len).toArray(JAVA_BYTE), StandardCharsets.UTF_8);
+        } catch (RuntimeException e) {
+            throw e;
+        } catch (Throwable t) {
+            throw new SiddhiAppRuntimeException("shp_dict_string failed: " + t, t);
+        }
+        names.putIfAbsent(id, s);
+        return s;
     }
 
     @Override

@@ -24,9 +24,10 @@ final class ProgramInfo {
     final String[] stateRef;        // per state id: the reference id (e1, ...), null when none
     final boolean[] stateMulti;     // per state id: a count state (multi-valued slot)
     final int countMax;             // the largest <min:max> bound (CHAIN32: a chain's longest length)
+    final boolean timers;           // an absent state (`not S for T`): the query has a Scheduler
 
     private ProgramInfo(String[] streams, ColumnarBatch.Column[] columns, boolean partitioned, int[] stateStream,
-                        String[] stateRef, boolean[] stateMulti, int countMax) {
+                        String[] stateRef, boolean[] stateMulti, int countMax, boolean timers) {
         this.streams = streams;
         this.columns = columns;
         this.partitioned = partitioned;
@@ -34,6 +35,7 @@ final class ProgramInfo {
         this.stateRef = stateRef;
         this.stateMulti = stateMulti;
         this.countMax = countMax;
+        this.timers = timers;
     }
 
     @SuppressWarnings("unchecked")
@@ -58,14 +60,17 @@ final class ProgramInfo {
         int[] sst = new int[st.size()];
         String[] sref = new String[st.size()];
         boolean[] smulti = new boolean[st.size()];
+        boolean timers = false;
         for (Object o : st) {
             Map<String, Object> m = (Map<String, Object>) o;
             int id = ((Number) m.get("id")).intValue();
             sst[id] = ((Number) m.get("stream")).intValue();
             sref[id] = (String) m.get("ref");
+            timers |= Boolean.TRUE.equals(m.get("absent"));
         }
         int cmax = markCounts(p.get("tree"), smulti);
-        return new ProgramInfo(names, cols, Boolean.TRUE.equals(p.get("partitioned")), sst, sref, smulti, cmax);
+        return new ProgramInfo(names, cols, Boolean.TRUE.equals(p.get("partitioned")), sst, sref, smulti, cmax,
+                timers);
     }
 
     // the states under a "count" node of program["tree"] (CountStateElement: multiValue = true);

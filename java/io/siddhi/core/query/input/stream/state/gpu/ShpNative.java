@@ -82,6 +82,8 @@ final class ShpNative {
     static final MethodHandle PUSH_BATCH_COMPACT = fn("shp_push_batch_compact", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
     // the oldest event an open partial still holds: the rows below it may be dropped (ColumnarBatch.trim)
     static final MethodHandle OLDEST_LIVE_SEQ = fn("shp_engine_oldest_live_seq", JAVA_INT, ADDRESS, ADDRESS);
+    // the earliest head of any key's timer queue: a live-mode runtime's wall-clock wake-up (Scheduler.schedule)
+    static final MethodHandle NEXT_DUE = fn("shp_engine_next_due", JAVA_INT, ADDRESS, ADDRESS);
     static final MethodHandle FETCH_MATCHES = fn("shp_fetch_matches", JAVA_INT, ADDRESS, ADDRESS);
     static final MethodHandle ADVANCE_CLOCK = fn("shp_advance_clock", JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS);
     static final MethodHandle SNAPSHOT = fn("shp_snapshot", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
@@ -100,6 +102,7 @@ final class ShpNative {
     static final MethodHandle DICT_CREATE = fn("shp_dict_create", ADDRESS, JAVA_INT);
     static final MethodHandle DICT_INTERN = fn("shp_dict_intern", JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG);
     static final MethodHandle DICT_SIZE = fn("shp_dict_size", JAVA_INT, ADDRESS);
+    static final MethodHandle DICT_STRING = fn("shp_dict_string", JAVA_LONG, ADDRESS, JAVA_INT, ADDRESS, JAVA_LONG);
     static final MethodHandle DICT_DESTROY = fnVoid("shp_dict_destroy", ADDRESS);
     static final MethodHandle COMPILE_SIDDHIQL = fn("shp_compile_siddhiql", JAVA_LONG, ADDRESS, ADDRESS, ADDRESS,
             ADDRESS, JAVA_LONG);

@@ -1712,6 +1712,20 @@ int64_t oracle_oldest_live_seq(void* hp) {
   return ne > 0 ? e.ev_gseq[ne - 1] + 1 : 0;
 }
 
+// The earliest head of any key's Scheduler queue (Scheduler.java:113-127: a FIFO; the live
+// EventCaller is scheduled at the head's due time, :129-155): 1 and *out, or 0 when none is pending.
+// The checker of shp_engine_next_due.
+int oracle_next_due(void* hp, int64_t* out) {
+  Engine& e = ((OracleHandle*)hp)->e;
+  int64_t best = INT64_MAX;
+  for (auto& k : e.keys)
+    for (size_t s = 0; s < e.schedulers.size(); s++)
+      if (!k->sched[s].queue.empty()) best = std::min(best, k->sched[s].queue.front());
+  if (best == INT64_MAX) return 0;
+  *out = best;
+  return 1;
+}
+
 // Debugging aid (tests only): key `key`'s timer queue of scheduler 0 into out[0..cap), then the
 // absent processor's lastScheduledTime; returns the queue length (or -1: no such key)
 int64_t oracle_debug_queue(void* hp, int32_t key, int64_t* out, int64_t cap) {

@@ -38,6 +38,7 @@ def lib():
                   "oracle_oldest_live_seq"):
             getattr(L, f).restype = ctypes.c_int64
             getattr(L, f).argtypes = [ctypes.c_void_p]
+        L.oracle_next_due.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
         L.oracle_num_states.argtypes = [ctypes.c_void_p]
         L.oracle_fetch.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 6
         L.oracle_destroy.argtypes = [ctypes.c_void_p]
@@ -87,6 +88,11 @@ class OracleEngine:
 
     def dropped_returns(self):
         return lib().oracle_dropped_returns(self.h)
+
+    def next_due(self):
+        """The earliest head of any key's timer queue (oracle_next_due), or None."""
+        v = ctypes.c_int64()
+        return int(v.value) if lib().oracle_next_due(self.h, ctypes.byref(v)) == 1 else None
 
     def oldest_live_seq(self):
         """The oldest event any open partial holds (oracle_oldest_live_seq)."""

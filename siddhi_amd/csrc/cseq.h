@@ -926,7 +926,9 @@ struct CseqState {
     return s.every ? (s.minc <= 1 ? CS_EVERY1 : CS_EVERYN) : (s.minc <= 1 ? CS_ONCE1 : CS_ONCEN);
   }
   bool own_plan(int M, int mode, int32_t nk) {
-    if (M > CO_MAXM || (mode == CS_ONCE1 && M + 1 > CO_MAXM)) return false;  // (k_co_run's 8-byte tables)
+    // without `every` (CS_ONCE1 and CS_ONCEN) a used once-armed start is the dead state D = M + 1,
+    // which k_co_run's 8-byte tables hold only for M + 1 <= CO_MAXM
+    if (M > CO_MAXM || ((mode == CS_ONCE1 || mode == CS_ONCEN) && M + 1 > CO_MAXM)) return false;
     const int per = 8 + 4 * M;  // value, L / null / ring head / ring fill, the ring
     int kmax = 1;
     while (kmax * 2 <= CO_KPO_MAX && kmax * 2 * per <= CO_KEY_LDS) kmax *= 2;

@@ -1096,7 +1096,9 @@ struct shp_engine {
         o += "},\"scheduler0\":{\"ToNotifyQueue\":[";
         for (int i = 0; i < s.ne; i++) {
           if (i) o += ",";
-          jnum(o, fq[(int64_t)k * wcap + ((s.eh + i) & (wcap - 1))].t);
+          const int64_t t = fq[(int64_t)k * wcap + ((s.eh + i) & (wcap - 1))].t;
+          if (due_min && i == 0 && t < *due_min) *due_min = t;  // the key's FIFO head
+          jnum(o, t);
         }
         o += "]}}";
       }
@@ -1284,7 +1286,9 @@ struct shp_engine {
           const int hd = i16(Yb.o_qhead, s, k), n = i16(Yb.o_qlen, s, k);
           for (int i = 0; i < n; i++) {
             if (i) o += ",";
-            jnum(o, i64(Yb.o_q, (int64_t)s * Yb.qcap + (hd + i) % Yb.qcap, k));
+            const int64_t t = i64(Yb.o_q, (int64_t)s * Yb.qcap + (hd + i) % Yb.qcap, k);
+            if (due_min && i == 0 && t < *due_min) *due_min = t;  // the key's FIFO head
+            jnum(o, t);
           }
           o += "]}";
         }
@@ -1316,6 +1320,29 @@ struct shp_engine {
       throw;
     }
     live_min = nullptr;
+    return m;
+  }
+
+  // ---- the earliest due time of any key's timer queue (shp_engine_next_due): the head of each
+  // key's Scheduler FIFO (Scheduler.java:113-127, 332) -- the EventCaller of a live-mode Scheduler
+  // is scheduled at the head's due time (Scheduler.schedule :129-155, EventCaller.run :287-326).
+  // INT64_MAX when no timer is pending (the 2-state, count-sequence paths have none).
+  int64_t* due_min = nullptr;
+  int64_t next_due() {
+    if (fast != 0 && fast != 4) return INT64_MAX;
+    if (fast == 0 && comp.P.nsched == 0) return INT64_MAX;
+    void* b = nullptr;
+    size_t n = 0;
+    snapshot_into(live_snap, &b, &n);
+    int64_t m = INT64_MAX;
+    due_min = &m;
+    try {
+      (void)describe(b, n);
+    } catch (...) {
+      due_min = nullptr;
+      throw;
+    }
+    due_min = nullptr;
     return m;
   }
 
@@ -1627,6 +1654,16 @@ int shp_engine_oldest_live_seq(shp_engine* e, int64_t* out) {
   return guarded(e, [&]() {
     *out = e->oldest_live_seq();
     return SHP_OK;
+  });
+}
+
+int shp_engine_next_due(shp_engine* e, int64_t* out) {
+  if (!e || !out) return SHP_ERR_ARG;
+  return guarded(e, [&]() {
+    const int64_t t = e->next_due();
+    if (t == INT64_MAX) return 0;
+    *out = t;
+    return 1;
   });
 }
 

@@ -23,6 +23,7 @@ SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACIT
               -4: "SHP_ERR_OUTPUT", -5: "SHP_ERR_DEVICE", -6: "SHP_ERR_KEYS"}
 
 SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches", "shp_push_batch_compact", "shp_engine_oldest_live_seq",
+           "shp_engine_next_due",
            "shp_advance_clock", "shp_engine_num_states", "shp_engine_state_stream", "shp_engine_path", "shp_last_kernel_ms", "shp_engine_stat",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
            "shp_dev_to_host", "shp_host_alloc", "shp_host_free", "shp_host_register",
@@ -81,6 +82,7 @@ def lib():
         L.shp_fetch_matches.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpMatches)]
         L.shp_push_batch_compact.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpBatch), ctypes.POINTER(ShpMatches)]
         L.shp_engine_oldest_live_seq.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+        L.shp_engine_next_due.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
         L.shp_advance_clock.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ShpMatches)]
         L.shp_engine_num_states.argtypes = [ctypes.c_void_p]
         L.shp_engine_state_stream.argtypes = [ctypes.c_void_p, ctypes.c_int32]
@@ -348,6 +350,14 @@ class HipEngine:
         v = ctypes.c_int64()
         self._check(lib().shp_engine_oldest_live_seq(self.h, ctypes.byref(v)))
         return int(v.value)
+
+    def next_due(self):
+        """shp_engine_next_due: the earliest due time of any key's timer queue, or None."""
+        v = ctypes.c_int64()
+        rc = lib().shp_engine_next_due(self.h, ctypes.byref(v))
+        if rc < 0:
+            self._check(rc)
+        return int(v.value) if rc == 1 else None
 
     def advance(self, now):
         mt = ShpMatches()

@@ -16,6 +16,8 @@ from typing import Any, Dict, List, Optional
 
 import numpy as np
 
+from ..flow import get_partition_flow_id
+
 NUM_RANK = {"int": 0, "long": 1, "float": 2, "double": 3}
 
 
@@ -112,8 +114,11 @@ class Selector:
         self.partitioned = compiled.partition_keys is not None
         self.aggs: Dict[Any, List[Aggregator]] = {}
 
-    def _aggs_for(self, key):
-        k = key if self.partitioned else 0
+    def _aggs_for(self):
+        """The aggregators of the current partition flow (PartitionStateHolder.getState,
+        core/util/snapshot/state/PartitionStateHolder.java:43-48): the host delivers each match
+        inside its key's flow (siddhi_amd.flow), the selector is never handed a key."""
+        k = get_partition_flow_id() if self.partitioned else 0
         if k not in self.aggs:
             lst = []
             self._collect_aggs(self.cq.select, lst)
@@ -188,9 +193,9 @@ class Selector:
             return args[0] is None
         raise ValueError(op)
 
-    def select(self, key, ts, etype, slots):
+    def select(self, ts, etype, slots):
         """Return the output row, or None when the event is not emitted (expired)."""
-        aggs = self._aggs_for(key)
+        aggs = self._aggs_for()
         agg_i = [0]
         remove = etype == 1
         row = [self._eval(it, slots, aggs, agg_i, remove) for it in self.cq.select]

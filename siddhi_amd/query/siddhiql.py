@@ -150,6 +150,24 @@ class App:
     streams: dict
     queries: List[Query]
     playback: bool
+    idle_time: int = -1   # @app:playback(idle.time = '...'): the heartbeat's idle time (ms), -1 = none
+    increment: int = 0    # @app:playback(increment = '...'): the heartbeat's clock step (ms)
+
+
+def playback_time(text: str) -> int:
+    """'10 milliseconds' / '1 sec' of an @app:playback property, in ms (SiddhiAppParser reads them with
+    the time grammar: core/util/parser/SiddhiAppParser.java)."""
+    parts = text.split()
+    total, i = 0, 0
+    while i + 1 < len(parts):
+        unit = parts[i + 1].lower()
+        if unit not in TIME_UNITS:
+            raise SiddhiParserException(f"bad time {text!r}")
+        total += int(float(parts[i]) * TIME_UNITS[unit])
+        i += 2
+    if i != len(parts):
+        raise SiddhiParserException(f"bad time {text!r}")
+    return total
 
 
 # --------------------------------------------------------------------------
@@ -196,6 +214,7 @@ class Parser:
         streams = {}
         queries: List[Query] = []
         playback = False
+        idle_time, increment = -1, 0
         pending_info = None
         while self.peek().kind != "eof":
             if self.at("@"):
@@ -203,6 +222,9 @@ class Parser:
                 lname = name.lower()
                 if lname in ("app:playback",):
                     playback = True
+                    if props.get("idle.time") is not None:
+                        idle_time = playback_time(props["idle.time"])
+                        increment = playback_time(props.get("increment") or "0 ms")
                 elif lname == "info":
                     pending_info = props.get("name")
                 continue
@@ -223,7 +245,7 @@ class Parser:
                 pending_info = None
                 continue
             raise SiddhiParserException(f"unsupported construct at {self.peek().pos}: {self.peek().text!r}")
-        return App(streams, queries, playback)
+        return App(streams, queries, playback, idle_time, increment)
 
     def annotation(self):
         self.eat("@")

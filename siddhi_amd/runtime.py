@@ -22,6 +22,7 @@ from typing import Callable, Dict, List, Optional
 
 import numpy as np
 
+from .flow import TimestampGenerator, in_partition_flow
 from .query.compiler import Dictionary, compile_app
 from .history import ChainRings, RowHistory, decode_pairs32
 from .query.selector import Selector
@@ -68,14 +69,24 @@ class InputHandler:
         return self.stream
 
     def send(self, *args):
-        """send(Object[]) | send(long timestamp, Object[]) | send(Event) | send(Event[])."""
+        """send(Object[]) | send(long timestamp, Object[]) | send(Event) | send(Event[]).
+        In playback the app clock is set from the event before it enters any junction
+        (InputHandler.java:59-92; send(Event[]): from the last event), which is what fires absent
+        timers on a send to any stream; send(Object[]) stamps wall-clock time and sets nothing."""
+        tg = self.rt.timestamp_generator
         if len(args) == 2:
+            if tg.playback:
+                tg.set_current_timestamp(int(args[0]))
             self.rt._enqueue(self.stream, int(args[0]), list(args[1]))
             return
         (a,) = args
         if isinstance(a, Event):
+            if tg.playback:
+                tg.set_current_timestamp(int(a.timestamp))
             self.rt._enqueue(self.stream, int(a.timestamp), list(a.data))
         elif isinstance(a, (list, tuple)) and a and isinstance(a[0], Event):
+            if tg.playback:
+                tg.set_current_timestamp(int(a[-1].timestamp))
             for ev in a:
                 self.rt._enqueue(self.stream, int(ev.timestamp), list(ev.data))
         else:
@@ -109,6 +120,8 @@ class _QueryRun:
         self.layout = engine.stat("match_layout") if self.compact else 0
         self.rings = ChainRings(_count_max(cq.program["tree"])) if self.layout == 4 else None
         self.retain = rt.retain and hasattr(engine, "oldest_live_seq")
+        # absent states: the query's Scheduler listens to the app clock (Scheduler.java:71-103)
+        self.timers = any(st.get("absent") for st in cq.program["states"])
 
 
 class SiddhiAppRuntime:
@@ -135,7 +148,10 @@ class SiddhiAppRuntime:
             self.strings = Dictionary()
         self.keydict = Dictionary()
         self.app, self.compiled, _ = compile_app(text, self.strings)
-        self._events: List[tuple] = []  # events not yet pushed: (stream idx, ts, data)
+        self.timestamp_generator = TimestampGenerator(self.app.playback, self.app.idle_time, self.app.increment)
+        # rows not yet pushed: (stream idx, ts, data, query) -- stream -1 with a query name is that
+        # query's clock-only row (its Scheduler heard the app clock move, under DEFERRED batching)
+        self._events: List[tuple] = []
         self._pending: List[int] = []
         self._start_clock = start_clock
         self._engine_factory = engine_factory
@@ -184,22 +200,75 @@ class SiddhiAppRuntime:
                     raise AssertionError(f"native lowering of {cq.name} differs from query.compiler")
             else:
                 eng = self._engine_factory(cq.program_json(), start, **kw)
-            self.queries[cq.name] = _QueryRun(self, cq, eng, self.min_trim)
+            qr = _QueryRun(self, cq, eng, self.min_trim)
+            self.queries[cq.name] = qr
+            if qr.timers:
+                self.timestamp_generator.add_time_change_listener(
+                    lambda now, qr=qr: self._on_time_change(qr, now))
 
     def _enqueue(self, stream: str, ts: int, data: list):
         self._ensure_queries()
         sidx = list(self.app.streams.keys()).index(stream)
-        self._events.append((sidx, ts, tuple(data)))
+        # a query's clock-only row at this ts just before its own stream's event: the event carries
+        # the same clock (ColumnarBatch.append absorbs it the same way)
+        ev = self._events
+        j = len(ev)
+        while j > 0 and ev[j - 1][0] < 0 and ev[j - 1][1] == ts:
+            j -= 1
+        for i in range(len(ev) - 1, j - 1, -1):
+            if stream in self.queries[ev[i][3]].streams:
+                del ev[i]
+                self._pending.pop()
+        ev.append((sidx, ts, tuple(data), None))
+        self._pending.append(len(ev) - 1)
+        if len(self._pending) >= self._batch_size:
+            self.flush()
+
+    def _on_time_change(self, qr: _QueryRun, now: int):
+        """The query's TimeChangeListener (Scheduler.java:71-103; GpuStateStreamRuntime.onTimeChange):
+        one push per send (batch_size 1, FlushPolicy.SYNC) fires the due timers at once, before the
+        event that moved the clock; batched (DEFERRED) a clock-only row joins the batch."""
+        self._ensure_queries()
+        if self._batch_size == 1:
+            self.flush()
+            qr.engine.advance(int(now))
+            self._drain(qr)
+            self._trim(qr)
+            return
+        self._events.append((-1, int(now), (), qr.cq.name))
         self._pending.append(len(self._events) - 1)
         if len(self._pending) >= self._batch_size:
             self.flush()
 
     def advance_time(self, now: int):
-        """Advance the event-time clock (playback heartbeat / live scheduler emulation)."""
+        """Time passes to `now` with no event (a test's Thread.sleep).  Playback: an injected clock
+        move (the idle heartbeat's setCurrentTimestamp), heard by the timer queries' listeners.  Live:
+        each timer query's wall-clock wake-up (Scheduler.schedule / EventCaller.run,
+        Scheduler.java:129-155, 287-326; GpuStateStreamRuntime.scheduleWake) runs at every due time
+        shp_engine_next_due reports up to `now`, and fires the timers due then."""
+        self._ensure_queries()
         self.flush()
+        if self.app.playback:
+            self.timestamp_generator.set_current_timestamp(int(now))
+            self.flush()
+            return
         for qr in self.queries.values():
-            qr.engine.advance(int(now))
-            self._drain(qr)
+            if not qr.timers:
+                continue
+            while True:
+                due = qr.engine.next_due() if hasattr(qr.engine, "next_due") else None
+                if due is None or due > now:
+                    break
+                qr.engine.advance(due)
+                self._drain(qr)
+            self._trim(qr)
+
+    def heartbeat(self, wall_ms: int):
+        """The playback idle heartbeat (TimestampGeneratorImpl.TimeInjector) at wall-clock wall_ms."""
+        self._ensure_queries()
+        self.flush()
+        if self.timestamp_generator.heartbeat(int(wall_ms)):
+            self.flush()
 
     # ---------------------------------------------------------------- flush
     def flush(self):
@@ -212,16 +281,12 @@ class SiddhiAppRuntime:
         ids = [i - ids[0] for i in ids]
         stream_names = list(self.app.streams.keys())
         for qr in self.queries.values():
-            if self.app.playback:
-                # the playback clock is the app's: a send on any stream sets it before anything
-                # else (InputHandler.java:59-64), so a stream this query does not read still
-                # fires its timers -- pushed as clock-only events (stream -1)
-                sel = list(ids)
-            else:
-                sel = [i for i in ids if stream_names[events[i][0]] in qr.streams]
+            # the query's own streams' events and its own clock-only rows (the listener's)
+            sel = [i for i in ids if (events[i][3] == qr.cq.name if events[i][0] < 0
+                                      else stream_names[events[i][0]] in qr.streams)]
             if not sel:
                 continue
-            self._push(qr, [events[i] for i in sel], stream_names)
+            self._push(qr, [events[i][:3] for i in sel], stream_names)
 
     def _push(self, qr: _QueryRun, evs: List[tuple], stream_names):
         n = len(evs)
@@ -238,10 +303,9 @@ class SiddhiAppRuntime:
             s, t, data = ev
             ts[j] = t
             stream[j] = s
+            if s < 0:  # clock-only: no key, no values (the kernels never read a stream -1 row's
+                continue  # values, so its null flags stay 0)
             sname = stream_names[s]
-            if sname not in qr.streams:  # clock-only (playback): no key, no values (the kernels never
-                stream[j] = -1          # read a stream -1 row's values, so its null flags stay 0)
-                continue
             if pk is not None:
                 attr = pk[sname]
                 ai = [x[0] for x in self.app.streams[sname].attrs].index(attr)
@@ -273,11 +337,24 @@ class SiddhiAppRuntime:
                 self._deliver(qr, int(key[i]), int(ts[i]), 0, slots)
         else:
             self._drain(qr, res)
+        self._trim(qr)
+
+    def _trim(self, qr: _QueryRun):
         if qr.retain:
             qr.history.maybe_trim(qr.engine.oldest_live_seq)
 
     def _deliver(self, qr: _QueryRun, key: int, ts: int, etype: int, slots):
-        row = qr.selector.select(key, ts, etype, slots)
+        """One match into the selector inside its key's partition flow, as the reference emits it
+        (PartitionStreamReceiver.send :262-272 for event matches, Scheduler.java:88-97 for timer
+        matches): the selector's per-key state is looked up under the flow (PartitionStateHolder)."""
+        flow = self.keydict.strings[key] if qr.cq.partition_keys is not None else None
+        if flow is None:
+            return self._select(qr, ts, etype, slots)
+        with in_partition_flow(flow):
+            self._select(qr, ts, etype, slots)
+
+    def _select(self, qr: _QueryRun, ts: int, etype: int, slots):
+        row = qr.selector.select(ts, etype, slots)
         if row is None:
             return
         qr.rows.append((ts, row))

@@ -260,6 +260,32 @@ def test_cseq_every_min_max_vs_oracle(every, mn, M, op, layout):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mn,M,layout", [(2, 7, 4), (2, 7, 0), (1, 7, 4), (2, 6, 4)])
+def test_cseq_once_dead_state_oldest_live_vs_oracle(mn, M, layout):
+    """No `every`: a used once-armed start is the dead state D = M + 1.  At M = 7 that is past the
+    owner kernel's 8-byte tables, so the engine must keep such shapes off the owner path:
+    matches, the oldest live event and the described chain lengths agree with the oracle per push."""
+    from siddhi_amd.native import HipEngine
+    rng = np.random.default_rng(M * 31 + mn)
+    ts, key, v = _stream(rng, 60_000, 500)
+    cq = _cq(_app(M, "<", every=False, mn=mn))
+    o = OracleEngine(cq.program_json(), 0)
+    eng = HipEngine(cq.program_json(), 0, max_keys=500, max_batch=1 << 15, match_layout=layout)
+    assert eng.path == 3
+    st = np.zeros(len(ts), np.int32)
+    for lo in range(0, len(ts), 15_013):
+        hi = min(len(ts), lo + 15_013)
+        args = (ts[lo:hi], key[lo:hi], st[lo:hi], [v[lo:hi]], [None])
+        o.push(*args)
+        eng.push(*args)
+        want, got = per_key(o.fetch()), per_key(eng.fetch())
+        assert compare(want, got) is None, (lo, compare(want, got))
+        assert eng.oldest_live_seq() == o.oldest_live_seq(), lo
+        d = eng.describe(eng.snapshot())
+        assert all(0 <= s["e1"]["Count"] <= M for s in d["keys"].values())
+
+
+@pytest.mark.gpu
 def test_cseq_nulls_vs_oracle():
     rng = np.random.default_rng(4)
     ts, key, v = _stream(rng, 120_000, 500, nan=0.0)

@@ -365,3 +365,75 @@ def test_runtime_pushes_compact_and_trims_by_oldest_live_seq():
     assert "void maybeTrim(LongSupplier oldestLive)" in cb and "void trim(long lo)" in cb
     src = _java("ShpNative.java")
     assert re.search(r"LAYOUT_COMPACT = 5;", src)
+
+
+def _method(src, sig):
+    """The body of the method whose declaration contains `sig` (brace-matched)."""
+    i = src.index(sig)
+    j = src.index("{", i)
+    depth = 0
+    for k in range(j, len(src)):
+        depth += {"{": 1, "}": -1}.get(src[k], 0)
+        if depth == 0:
+            return src[j:k + 1]
+    raise AssertionError(sig)
+
+
+def test_every_match_reaches_the_selector_inside_its_partition_flow():
+    """Egress as the reference: PartitionStreamReceiver.send (:262-272) and the Scheduler's timer loop
+    (Scheduler.java:88-97) run a match under SiddhiAppContext.startPartitionFlow(key), and the selector's
+    per-key state is looked up under it (PartitionStateHolder.java:43-48).  selector.process appears only
+    inside emit(), which sets the match key's flow and restores the caller's in a finally; each decoder
+    hands emit the key of its record (PAIRS32 / CHAIN32: the batch's key column, FULL: the records')."""
+    rt = _java("GpuStateStreamRuntime.java")
+    code = re.sub(r"/\*.*?\*/|//[^\n]*", "", rt, flags=re.S)
+    emit = _method(code, "private void emit(int keyId, StateEvent se)")
+    assert code.count("selector.process(") == emit.count("selector.process(") == 2
+    assert "SiddhiAppContext.startPartitionFlow(keys.string(keyId))" in emit
+    fin = emit[emit.index("finally"):]
+    assert "SiddhiAppContext.startPartitionFlow(prev)" in fin and "SiddhiAppContext.stopPartitionFlow()" in fin
+    assert emit.index("SiddhiAppContext.getPartitionFlowId()") < emit.index("startPartitionFlow(keys.string")
+    assert "emit(batch.keyAt(idx), se)" in _method(code, "private void deliverPairs32(")
+    assert "emit(k, se)" in _method(code, "private void deliverChain32(")
+    full = _method(code, "private void deliverFull(")
+    assert 'matchesPtr(matches, "key", m * 4)' in full and "emit(key.getAtIndex(JAVA_INT, i), se)" in full
+    nd = _java("NativeDictionary.java")
+    assert "String string(int id)" in nd and "ShpNative.DICT_STRING.invokeExact" in nd
+
+
+def test_the_app_clock_reaches_the_engine():
+    """Clock as the reference's Scheduler hears it: a TimeChangeListener on the app's TimestampGenerator
+    (Scheduler.java:71-72) for queries with an absent state -- SYNC advances the engine at once, DEFERRED
+    appends a clock-only row that the following event of the same send absorbs; live mode keeps one
+    wall-clock wake-up at shp_engine_next_due (Scheduler.java:129-155) that advances to the wall clock."""
+    rt = re.sub(r"/\*.*?\*/|//[^\n]*", "", _java("GpuStateStreamRuntime.java"), flags=re.S)
+    assert "getTimestampGenerator().addTimeChangeListener(this::onTimeChange)" in rt
+    ctor = rt[rt.index("GpuStateStreamRuntime(String appText"):rt.index("private void rethrowDeferred()")]
+    assert "if (timers)" in ctor and "addTimeChangeListener" in ctor
+    otc = _method(rt, "void onTimeChange(long now)")
+    assert "advanceClock(now)" in otc and "batch.appendClock(now)" in otc
+    assert otc.index("FlushPolicy.SYNC") < otc.index("advanceClock(now)") < otc.index("batch.appendClock(now)")
+    wake = _method(rt, "private void scheduleWake()")
+    assert "appContext.isPlayback()" in wake and "nextDue()" in wake
+    assert "getScheduledExecutorService().schedule(this::onWake" in wake
+    assert "ShpNative.NEXT_DUE.invokeExact(engine, out)" in _method(rt, "private long nextDue()")
+    assert "advanceClock(appContext.getTimestampGenerator().currentTime())" in _method(rt, "private void onWake()")
+    for m in ("void flush()", "void advanceClock(long now)"):
+        assert "scheduleWake();" in _method(rt, m), m
+    pi = _java("ProgramInfo.java")
+    assert 'timers |= Boolean.TRUE.equals(m.get("absent"))' in pi
+    cb = re.sub(r"/\*.*?\*/|//[^\n]*", "", _java("ColumnarBatch.java"), flags=re.S)
+    app = _method(cb, "void append(long timestamp, int keyId, int streamIndex, Object[] data)")
+    assert "streamIndex >= 0 && n > 0 && streamAt(n - 1) < 0 && rowTs.get((int) n - 1) == timestamp" in app
+    assert "append(now, 0, -1, null)" in _method(cb, "void appendClock(long now)")
+
+
+def test_columnar_batch_finds_rows_by_bisection_and_restore_validates():
+    """event() bisects the kept blocks by seq0 (history is unbounded, trimmed only to the
+    engine's oldest live seq); restoreFrom refuses a snapshot without the rows before touching the engine."""
+    cb = re.sub(r"/\*.*?\*/|//[^\n]*", "", _java("ColumnarBatch.java"), flags=re.S)
+    ev = _method(cb, "StreamEvent event(long seq, int outputDataSize)")
+    assert "(lo + hi) >>> 1" in ev and "descendingIterator" not in ev
+    rt = re.sub(r"/\*.*?\*/|//[^\n]*", "", _java("GpuStateStreamRuntime.java"), flags=re.S)
+    rf = _method(rt, "void restoreFrom(Map<String, Object> m)")
+    assert rf.index('m.get("LiveRows") instanceof Object[]') < rf.index("restore((byte[])")
