@@ -91,6 +91,10 @@ def parse():
                          "takes such pushes; a measurement of that path, not the headline)")
     ap.add_argument("--cseq-layout", choices=["chain32", "full"], default="chain32",
                     help="match payload of the count-sequence path (C3'): 4-byte CHAIN32 words (default) or FULL")
+    ap.add_argument("--e2e-steps", type=int, default=3,
+                    help="SURVEY §8d(b) end-to-end host ingest: steps of N events from page-locked host columns "
+                         "through shp_stage_batch / shp_run_staged (records back to host memory); 0: skip")
+    ap.add_argument("--e2e-batch", type=int, default=12_500_000, help="events per staged host batch")
     return ap.parse_args()
 
 
@@ -278,6 +282,13 @@ def main():
         latency = batch_latency(eng, L, native, spec, K, layout, a.latency_events, a.latency_batches,
                                 (a.warmup + a.steps + 1) * N)
 
+    e2e = None
+    if rank == 0 and G == 1 and a.e2e_steps > 0 and layout != "full" and a.disorder == 0:
+        del batches
+        torch.cuda.empty_cache()
+        e2e = end_to_end(cq, L, native, spec, K, a.e2e_batch, N, a.e2e_steps, (a.warmup + 2 * a.steps + 4) * N,
+                         force, mlay, layout, local)
+
     if rank == 0:
         value = ev_total / elapsed
         dom = max(kernel_ms, key=lambda k: kernel_ms[k])
@@ -342,6 +353,9 @@ def main():
                 "p99_batch_ms": float(np.percentile(lat, 99)),
                 "match_layout": layout,
                 "latency": latency,
+                # host columns in, match records in host memory out (what the Java host
+                # drives), beside the device-resident `value`
+                "end_to_end": e2e,
                 # the compact words are not self-contained (a CHAIN32 word names its e2 event; the
                 # chain needs the batch's key column and the engine's pre-push history): the same
                 # path with each push's words expanded to FULL rows in HBM, timed the same way
@@ -499,6 +513,123 @@ def batch_latency(eng, L, native, spec, K, layout, n, batches, start):
             "host_buffer": "page-locked (shp_host_alloc)",
             "pageable_p50_ms": float(np.percentile(pg, 50)), "pageable_p99_ms": float(np.percentile(pg, 99)),
             "what": "shp_push_batch_device entry -> match payload in host memory"}
+
+
+def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout, device):
+    """the step's N events from page-locked host SoA columns (the Java host's
+    ColumnarBatch segments, pinned with shp_host_register) to match records in host memory, in
+    batches of nb events: (1) serial -- shp_push_batch_compact per batch, the copy, the run and the
+    records' copy back one after the other; (2) pipelined -- shp_stage_batch of batch i+1 (H2D on the
+    engine's copy stream) while shp_run_staged runs batch i; (3) the same with the narrow ingest form
+    (shp_stage_batch_ts32: 4-byte ts offsets, 12 B/event).  Fresh events every step (the stream goes
+    on); each form on its own engine, one untimed warm-up step each.  Achieved PCIe GB/s counts the
+    H2D input bytes plus the D2H record bytes over the wall time."""
+    import torch
+    nsub = -(-N // nb)
+    per = BYTES_PER_MATCH[layout]
+    total_steps = 1 + steps
+    # page-locked host input for every step: generated in HBM, copied down untimed
+    host = []
+    for s in range(total_steps):
+        ts = torch.empty(N, dtype=torch.int64, pin_memory=True)
+        key = torch.empty(N, dtype=torch.int32, pin_memory=True)
+        price = torch.empty(N, dtype=torch.float32, pin_memory=True)
+        ts32 = torch.empty(N, dtype=torch.int32, pin_memory=True)
+        dts = torch.empty(N, dtype=torch.int64, device="cuda")
+        dkey = torch.empty(N, dtype=torch.int32, device="cuda")
+        dpr = torch.empty(N, dtype=torch.float32, device="cuda")
+        assert L.shp_synth_fill(spec.config, start + s * N, N, K, 1, int(spec.dense), dts.data_ptr(), dkey.data_ptr(),
+                                dpr.data_ptr(), None, None, None) == 0
+        torch.cuda.synchronize()
+        base = torch.empty(nsub, dtype=torch.int64)
+        d32 = torch.empty(N, dtype=torch.int32, device="cuda")
+        for j in range(nsub):
+            lo, hi = j * nb, min(N, (j + 1) * nb)
+            b0 = dts[lo]
+            d32[lo:hi] = (dts[lo:hi] - b0).to(torch.int32)
+            base[j] = b0.item()
+        ts.copy_(dts)
+        key.copy_(dkey)
+        price.copy_(dpr)
+        ts32.copy_(d32)
+        host.append((ts, key, price, ts32, base))
+        del dts, dkey, dpr, d32
+    torch.cuda.synchronize()
+
+    def batch(s, j):
+        ts, key, price, ts32, base = host[s]
+        lo, hi = j * nb, min(N, (j + 1) * nb)
+        colp = (ctypes.c_void_p * 1)(price.data_ptr() + lo * 4)
+        b = native.ShpBatch(hi - lo, ts.data_ptr() + lo * 8, key.data_ptr() + lo * 4, None,
+                            ctypes.cast(colp, ctypes.c_void_p), None)
+        return b, colp, ts32.data_ptr() + lo * 4, int(base[j])
+
+    def check(rc, e):
+        if rc != 0:
+            raise native.ShpError(rc, L.shp_last_error(e.h).decode())
+
+    res = {}
+    for mode in ("serial", "pipelined", "pipelined_ts32"):
+        e = native.HipEngine(cq.program_json(), 0, max_keys=K, max_batch=nb, max_matches=int(nb * 1.1) + 4096,
+                             device=device, force_general=force, match_layout=native.LAYOUT_COMPACT)
+        try:
+            def stage(s, j):
+                b, colp, p32, b0 = batch(s, j)
+                if mode == "pipelined_ts32":
+                    check(L.shp_stage_batch_ts32(e.h, ctypes.byref(b), b0, p32), e)
+                else:
+                    check(L.shp_stage_batch(e.h, ctypes.byref(b)), e)
+
+            def one_step(s):
+                m = 0
+                mt = native.ShpMatches()
+                if mode == "serial":
+                    for j in range(nsub):
+                        b, colp, _, _ = batch(s, j)
+                        check(L.shp_push_batch_compact(e.h, ctypes.byref(b), ctypes.byref(mt)), e)
+                        m += mt.m
+                    return m
+                for j in range(nsub):
+                    if j + 1 < nsub:
+                        stage(s, j + 1)  # batch j+1's copies run while batch j runs
+                    elif s + 1 < total_steps:
+                        stage(s + 1, 0)  # the next step's first batch
+                    check(L.shp_run_staged(e.h, ctypes.byref(mt)), e)
+                    m += mt.m
+                return m
+            if mode != "serial":
+                stage(0, 0)
+            one_step(0)  # warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            m = 0
+            for s in range(1, total_steps):
+                m += one_step(s)
+            el = time.perf_counter() - t0
+            inb = 12 if mode == "pipelined_ts32" else 16
+            ev = N * steps
+            res[mode] = {"value": ev / el, "ms_per_step": el / steps * 1e3, "matches_per_s": m / el,
+                         "h2d_bytes_per_event": inb, "d2h_bytes_per_match": per,
+                         "pcie_gbs": (ev * inb + m * per) / el / 1e9}
+        finally:
+            e.close()
+    # the host link alone: one page-locked 1 GiB H2D copy (torch), for scale
+    hb = torch.empty(1 << 28, dtype=torch.float32, pin_memory=True)
+    db = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
+    db.copy_(hb, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(4):
+        db.copy_(hb, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = 4 * (1 << 30) / (time.perf_counter() - t0) / 1e9
+    del hb, db, host
+    best = max(("pipelined", "pipelined_ts32"), key=lambda k: res[k]["value"])
+    return {"value": res[best]["value"], "unit": "events/s", "ms_per_step": res[best]["ms_per_step"],
+            "mode": best, "batch_events": nb, "batches_per_step": nsub, "steps": steps, "forms": res,
+            "h2d_copy_gbs": h2d,
+            "what": "page-locked host SoA columns -> shp_stage_batch[_ts32] / shp_run_staged -> compact records in "
+                    "page-locked host memory; serial = shp_push_batch_compact per batch"}
 
 
 def _lib_sha16(path):

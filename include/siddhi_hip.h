@@ -187,6 +187,19 @@ int shp_push_batch_device(shp_engine* e, const shp_batch* in, shp_matches* out);
  * e2's batch index (the reference emits at e2's arrival, PatternSingleProcessStreamReceiver).
  * The Java binding's push (GpuStateStreamRuntime.flush). */
 int shp_push_batch_compact(shp_engine* e, const shp_batch* in, shp_matches* out);
+/* Pipelined host ingest: the host copy of batch i+1 overlaps the engine's run of
+ * batch i.  shp_stage_batch enqueues the H2D copies of a host batch into one of two device slots on a
+ * copy stream and returns at once (the host columns must stay valid and unchanged until the
+ * shp_run_staged that consumes them returns; page-locked memory -- shp_host_alloc / shp_host_register
+ * -- makes the copies asynchronous).  At most two batches are staged (a third: SHP_ERR_CAPACITY).
+ * shp_run_staged runs the oldest staged batch as shp_push_batch_compact would (same state, same
+ * records, in the engine's compact layout) and copies the records into page-locked memory owned by
+ * the engine (valid until the next call).  Order: stage(0), stage(1), run -> 0, stage(2), run -> 1, ...
+ * shp_stage_batch_ts32 is the narrow form: ts[i] = ts_base + ts_delta[i] (in->ts is ignored), 12
+ * instead of 16 bytes per event for a float column -- the host keeps a batch's ts span below 2^31 ms. */
+int shp_stage_batch(shp_engine* e, const shp_batch* in);
+int shp_stage_batch_ts32(shp_engine* e, const shp_batch* in, int64_t ts_base, const int32_t* ts_delta);
+int shp_run_staged(shp_engine* e, shp_matches* out);
 /* The oldest event sequence number the engine's committed state still names: an event of any open
  * partial (pending / new-and-every lists, count chains, logical slots, pairs waiting on an absent
  * timer, sweep carry).  Every later match names events >= this or of later pushes, so a host that

@@ -82,6 +82,11 @@ final class ShpNative {
     static final MethodHandle PUSH_BATCH_COMPACT = fn("shp_push_batch_compact", JAVA_INT, ADDRESS, ADDRESS, ADDRESS);
     // the oldest event an open partial still holds: the rows below it may be dropped (ColumnarBatch.trim)
     static final MethodHandle OLDEST_LIVE_SEQ = fn("shp_engine_oldest_live_seq", JAVA_INT, ADDRESS, ADDRESS);
+    // pipelined host ingest: H2D of the next batch on the engine's copy stream while it runs the staged one
+    static final MethodHandle STAGE_BATCH = fn("shp_stage_batch", JAVA_INT, ADDRESS, ADDRESS);
+    static final MethodHandle STAGE_BATCH_TS32 = fn("shp_stage_batch_ts32", JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG,
+            ADDRESS);
+    static final MethodHandle RUN_STAGED = fn("shp_run_staged", JAVA_INT, ADDRESS, ADDRESS);
     // the earliest head of any key's timer queue: a live-mode runtime's wall-clock wake-up (Scheduler.schedule)
     static final MethodHandle NEXT_DUE = fn("shp_engine_next_due", JAVA_INT, ADDRESS, ADDRESS);
     static final MethodHandle FETCH_MATCHES = fn("shp_fetch_matches", JAVA_INT, ADDRESS, ADDRESS);

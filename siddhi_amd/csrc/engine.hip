@@ -141,6 +141,13 @@ __global__ void k_clamp_clock(int64_t* rmax, int64_t n, int64_t clock0) {
     if (rmax[i] < clock0) rmax[i] = clock0;
 }
 
+// shp_stage_batch_ts32: the narrow ingest form (4-byte ts offsets from the batch's base) widened
+// in HBM before the run -- 4 B read + 8 B written per event, against 4 B saved on the host link
+__global__ void k_widen_ts(const int32_t* __restrict__ d, int64_t base, int64_t* __restrict__ ts, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) ts[i] = base + d[i];
+}
+
 // Capacity growth: the committed arena of layout Ys (tier t) into layout Yd (tier >= t), every
 // lane.  Fields keep their order and element sizes across tiers; element indices that embed a
 // capacity are re-indexed: list items ((which * MAXP + p) * LCAP + i) and the timer rings
@@ -280,6 +287,31 @@ struct shp_engine {
   int64_t win_pushes = 0, win_fallbacks = 0, r16_reruns = 0;
   int64_t spill_reruns = 0;
 
+  // ---- pipelined host ingest (shp_stage_batch / shp_run_staged): two device slots
+  // filled from host columns on a copy stream while the compute stream runs the previous batch, and
+  // the compact records copied back into page-locked memory.  Allocated at the first stage.
+  struct Slot {
+    int64_t n = 0;
+    int64_t* ts = nullptr;
+    int32_t* ts32 = nullptr;  // shp_stage_batch_ts32: ts = ts_base + ts32[i], widened on the device
+    int64_t ts_base = 0;
+    bool narrow = false;
+    int32_t* key = nullptr;
+    int32_t* strm = nullptr;
+    int64_t *clk = nullptr, *sq = nullptr;
+    void* cols[MAXCOL] = {};
+    uint8_t* nulls[MAXCOL] = {};
+    bool has_stream = false, has_clk = false, has_seq = false, has_null[MAXCOL] = {};
+    hipEvent_t ready = nullptr;     // its H2D copies are done (copy stream)
+    hipEvent_t consumed = nullptr;  // the run that read it is done (compute stream)
+  };
+  Slot slots[2];
+  int slot_head = 0, slot_count = 0;
+  bool slots_ready = false;
+  hipStream_t cstream = nullptr;
+  uint32_t* h_wpin = nullptr;  // page-locked compact records of the last shp_run_staged
+  int64_t h_wpin_words = 0;
+
   ~shp_engine() { release(); }
 
   void release() {
@@ -324,6 +356,22 @@ struct shp_engine {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (ev2) (void)hipEventDestroy(ev2);
+    for (Slot& sl : slots) {
+      F(sl.ts);
+      F(sl.ts32);
+      F(sl.key);
+      F(sl.strm);
+      F(sl.clk);
+      F(sl.sq);
+      for (int c = 0; c < MAXCOL; c++) {
+        F(sl.cols[c]);
+        F(sl.nulls[c]);
+      }
+      if (sl.ready) (void)hipEventDestroy(sl.ready);
+      if (sl.consumed) (void)hipEventDestroy(sl.consumed);
+    }
+    if (h_wpin) (void)hipHostFree(h_wpin);
+    if (cstream) (void)hipStreamDestroy(cstream);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -1385,6 +1433,116 @@ struct shp_engine {
     }
   }
 
+  // ---- pipelined host ingest
+  void slots_alloc() {
+    if (slots_ready) return;
+    const DevProg& P = comp.P;
+    HIP_OK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    for (Slot& sl : slots) {
+      alloc(sl.ts, cap);
+      alloc(sl.ts32, cap);
+      alloc(sl.key, cap);
+      alloc(sl.strm, cap);
+      alloc(sl.clk, cap);
+      alloc(sl.sq, cap);
+      for (int c = 0; c < P.ncol; c++) {
+        HIP_OK(hipMalloc(&sl.cols[c], std::max<int64_t>(cap, 1) * colBytes(P.colTag[c])));
+        alloc(sl.nulls[c], cap);
+      }
+      HIP_OK(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&sl.consumed, hipEventDisableTiming));
+      HIP_OK(hipEventRecord(sl.consumed, stream));
+    }
+    slots_ready = true;
+  }
+
+  // H2D of one host batch into the next free slot on the copy stream; returns once enqueued
+  int stage_slot(const shp_batch* in, const int32_t* ts32, int64_t ts_base) {
+    const DevProg& P = comp.P;
+    if (in->n > cfg.max_batch) return fail(SHP_ERR_ARG, "batch larger than max_batch");
+    if (in->n > 0 && !ts32 && !in->ts) return fail(SHP_ERR_ARG, "no ts column");
+    if (P.partitioned && in->n > 0 && !in->key) return fail(SHP_ERR_ARG, "no key column");
+    if (slot_count == 2) return fail(SHP_ERR_CAPACITY, "two batches staged: run one first (shp_run_staged)");
+    slots_alloc();
+    Slot& sl = slots[(slot_head + slot_count) % 2];
+    const int64_t n = in->n;
+    const hipMemcpyKind k = hipMemcpyHostToDevice;
+    HIP_OK(hipStreamWaitEvent(cstream, sl.consumed, 0));  // the run that read this slot is done
+    sl.n = n;
+    sl.narrow = ts32 != nullptr;
+    sl.ts_base = ts_base;
+    if (n > 0) {
+      if (ts32) HIP_OK(hipMemcpyAsync(sl.ts32, ts32, n * 4, k, cstream));
+      else HIP_OK(hipMemcpyAsync(sl.ts, in->ts, n * 8, k, cstream));
+      if (P.partitioned) HIP_OK(hipMemcpyAsync(sl.key, in->key, n * 4, k, cstream));
+      sl.has_stream = in->stream != nullptr;
+      if (sl.has_stream) HIP_OK(hipMemcpyAsync(sl.strm, in->stream, n * 4, k, cstream));
+      sl.has_clk = in->clock != nullptr;
+      if (sl.has_clk) HIP_OK(hipMemcpyAsync(sl.clk, in->clock, n * 8, k, cstream));
+      sl.has_seq = in->seq != nullptr;
+      if (sl.has_seq) HIP_OK(hipMemcpyAsync(sl.sq, in->seq, n * 8, k, cstream));
+      for (int c = 0; c < P.ncol; c++) {
+        HIP_OK(hipMemcpyAsync(sl.cols[c], in->cols[c], n * colBytes(P.colTag[c]), k, cstream));
+        sl.has_null[c] = in->nulls && in->nulls[c];
+        if (sl.has_null[c]) HIP_OK(hipMemcpyAsync(sl.nulls[c], in->nulls[c], n, k, cstream));
+      }
+    }
+    HIP_OK(hipEventRecord(sl.ready, cstream));
+    slot_count++;
+    return SHP_OK;
+  }
+
+  // the oldest staged batch through the engine; compact records to page-locked host memory
+  int run_slot(shp_matches* out) {
+    if (slot_count == 0) return fail(SHP_ERR_ARG, "no staged batch (shp_stage_batch first)");
+    const DevProg& P = comp.P;
+    Slot& sl = slots[slot_head];
+    slot_head = (slot_head + 1) % 2;
+    slot_count--;
+    HIP_OK(hipStreamWaitEvent(stream, sl.ready, 0));
+    const int64_t n = sl.n;
+    if (sl.narrow && n > 0) {
+      const int gb = (int)std::min<int64_t>((n + 255) / 256, 8192);
+      k_widen_ts<<<gb, 256, 0, stream>>>(sl.ts32, sl.ts_base, sl.ts, n);
+    }
+    const void* cp[MAXCOL];
+    const uint8_t* np[MAXCOL];
+    for (int c = 0; c < P.ncol; c++) {
+      cp[c] = sl.cols[c];
+      np[c] = sl.has_null[c] ? sl.nulls[c] : nullptr;
+    }
+    shp_batch b{n, sl.ts, sl.key, sl.has_stream ? sl.strm : nullptr, cp, np, sl.has_clk ? sl.clk : nullptr,
+                sl.has_seq ? sl.sq : nullptr};
+    const int rc = run(n, false, &b);
+    HIP_OK(hipEventRecord(sl.consumed, stream));
+    if (rc != SHP_OK) return rc;
+    const int lay = cfg.match_layout;
+    const bool compact = !expanded && ((fast == 2 && (lay == SHP_LAYOUT_PAIRS32 || lay == SHP_LAYOUT_PAIRS)) ||
+                                       (fast == 3 && lay == SHP_LAYOUT_CHAIN32));
+    if (!compact) {
+      fetch(out);
+      return SHP_OK;
+    }
+    const int64_t m = last_m;
+    const int64_t words = lay == SHP_LAYOUT_PAIRS ? 4 * m : (lay == SHP_LAYOUT_PAIRS32 ? 2 * m : m);
+    if (words > h_wpin_words) {
+      if (h_wpin) HIP_OK(hipHostFree(h_wpin));
+      h_wpin = nullptr;
+      h_wpin_words = std::max<int64_t>(words, h_wpin_words * 2);
+      HIP_OK(hipHostMalloc((void**)&h_wpin, (size_t)h_wpin_words * 4, hipHostMallocDefault));
+    }
+    if (m) {
+      HIP_OK(hipMemcpyAsync(h_wpin, d_refs, (size_t)words * 4, hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+    }
+    *out = shp_matches{};
+    out->layout = lay;
+    out->m = m;
+    out->num_states = P.nstates;
+    out->refs = (int64_t*)h_wpin;
+    return SHP_OK;
+  }
+
   void fill_device(shp_matches* out) {
     out->agg = nullptr;
     if (cfg.match_layout == SHP_LAYOUT_AGG) {
@@ -1676,6 +1834,21 @@ int shp_push_batch_compact(shp_engine* e, const shp_batch* in, shp_matches* out)
     if (rc != SHP_OK) return rc;
     return e->fetch_compact(out);
   });
+}
+
+int shp_stage_batch(shp_engine* e, const shp_batch* in) {
+  if (!e || !in) return SHP_ERR_ARG;
+  return guarded(e, [&]() { return e->stage_slot(in, nullptr, 0); });
+}
+
+int shp_stage_batch_ts32(shp_engine* e, const shp_batch* in, int64_t ts_base, const int32_t* ts_delta) {
+  if (!e || !in || (in->n > 0 && !ts_delta)) return SHP_ERR_ARG;
+  return guarded(e, [&]() { return e->stage_slot(in, ts_delta, ts_base); });
+}
+
+int shp_run_staged(shp_engine* e, shp_matches* out) {
+  if (!e || !out) return SHP_ERR_ARG;
+  return guarded(e, [&]() { return e->run_slot(out); });
 }
 
 int shp_fetch_matches(shp_engine* e, shp_matches* out) {

@@ -84,14 +84,16 @@ struct __attribute__((aligned(8))) LaWait {
 // push completes at most ceil(cnt / 2) pairs, and at most 64 were waiting before it)
 struct __attribute__((aligned(8))) LaRec {
   int64_t due, xseq, yseq;
-  uint32_t flo, fhi;  // the fire event is the first batch index in [flo, fhi] whose clock reaches due
+  uint32_t flo, fhi;  // the fire event is the first batch index in [flo, fhi] whose clock reaches thr
+  int64_t thr;        // (due for the ordered formulation's records; a record of an exactly stepped block
+                      // fires where an earlier entry of the same window crossed, or at flo: thr = INT64_MIN)
 };
 
 // one timer entry of the key's Scheduler queue (ToNotifyQueue, a FIFO: Scheduler.java:113-127, 332)
 struct __attribute__((aligned(8))) LaEnt {
   int64_t t;    // notify time
   int32_t i0;   // the first batch index of the current push it may fire at (0 for carried entries)
-  int32_t pad;
+  int32_t pad;  // (k_labs_w's exact blocks keep their entries in registers, with the same fields)
 };
 
 struct LaPend {
@@ -843,6 +845,8 @@ constexpr int LA_SEG_MAXKEYS = 4096;   // segments only while keys are this few
 struct LaSnap {
   int64_t xseq, xts, yseq, yts, last, lsched, lo;
   uint32_t xv, yv, fl, hxy, nal, nef;
+  uint32_t xm, xnae;   // exact mode (round 6): its new-and-every count
+  uint64_t qat;        // exact mode: the entries already reached when queued
   LaWait A[64];
   int64_t ed[64];
   int64_t qe[64];
@@ -900,10 +904,11 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   const int64_t Wb = useW ? Wn : (1ll << 60);  // D = min slot ts + Wb
   int nal = s0.nw;
   int nef = s0.ne;
-  {  // the ordered formulation must hold from this state and for this push (else k_labs)
-    bool slow = nal > 64 || nef > LA_WF || !s0.reg;
+  const int64_t mstep = (int64_t)*D.maxstep;  // the push's largest clock step after its first send
+  {  // capacity and the push's clock steps (else k_labs re-runs the push)
+    bool slow = nal > 64 || nef > LA_WF;
     if (!slow && nef > 0 && B.n > 0 && B.rmax[0] - B.clock0 > Tw) slow = true;  // a step at the first send
-    if (!slow && *D.maxstep > (unsigned long long)Tw) slow = true;             // a step at a later send
+    if (!slow && mstep > Tw) slow = true;                                       // a step at a later send
     if (slow) {
       if (lane == 0) {
         D.cm[ks] = 0;  // k_labs_out runs before the host sees LA_SLOW
@@ -913,26 +918,26 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     }
   }
   int64_t qe = lane < nef ? D.fq[rd][(int64_t)k * cap + ((s0.eh + lane) & msk)].t : INT64_MAX;  // the queue
+  // Exact blocks (round 6).  A block the ordered formulation does not cover (a key's ts going back, an
+  // event lagging the clock by T) runs the exact rule of k_labs instead, event by event on the whole wave:
+  // the pairs stay in A[] in list order (the last xnae on new-and-every), the Scheduler FIFO in qe (entry
+  // j in lane j, unsorted) with, per entry, its first batch index Qi0 and whether the clock had already
+  // reached it when it was queued (Qat: it fires at the next send that sets the clock).  After each such
+  // block the state goes back to the ordered formulation when it is regular there (to_wave), so only
+  // the disordered stretches of a key pay for the exact rule.  A firing's send is kept as a window and
+  // a clock threshold (the first send from plo on whose clock reaches pthr) and found by k_labs_out, as
+  // for the ordered blocks' records; it is searched here only when the clock at it decides
+  // lastScheduledTime.  The carried state starts here too and converts when regular.
+  int32_t Qi0 = 0;
+  bool Qat = lane < nef && qe <= B.clock0;
+  int xnae = s0.nae;
+  bool xm = true;      // exact mode (wave-uniform)
+  bool xover = false;  // exact mode outgrew 64 pairs or entries: the push re-runs on k_labs
   Ec[lane] = 0;
   if (lane < nal) {
     const LaWait w = D.wq[rd][(int64_t)k * cap + ((s0.wh + lane) & msk)];
     A[lane] = w;
     Ac[lane] = -1;
-    Anae[lane] = lane >= nal - s0.nae ? 1 : 0;
-  }
-  {  // a carried pair's E_D: the first queued entry past D (every entry is past the clock; its own due is one)
-    int64_t dd = INT64_MAX, due = INT64_MAX;
-    if (lane < nal) {
-      const LaWait& w = A[lane];
-      dd = min(w.xts, w.yts) + Wb;
-      due = w.due;
-    }
-    int64_t ed = due;
-    for (int i = 0; i < nef; i++) {
-      const int64_t t = la_rl64(qe, i);
-      if (t > dd) ed = min(ed, t);
-    }
-    if (lane < nal) Aed[lane] = ed;
   }
   __syncthreads();
   LaRec* rec = D.rec + la_region(beg + s_beg, ks);
@@ -948,6 +953,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   int64_t last = s0.last;
   int64_t lsched = s0.lst;  // lastScheduledTime
   int64_t lo = 0;  // first batch index a timer can fire at (after the key's previous event)
+  int64_t lclk = B.clock0;  // the clock at the key's previous event
   // the pairs (one per lane) leave (left: in [flo, fhi]) -- emitted when within W of their due
   // time -- or are killed; the survivors are compacted in order
   auto settle = [&](bool left, bool killed, bool tonae, int64_t flo, int64_t fhi, LaWait w, int64_t ed)
@@ -963,6 +969,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       r.yseq = w.yseq;
       r.flo = (uint32_t)flo;
       r.fhi = (uint32_t)fhi;
+      r.thr = w.due;
       rec[nm + (uint32_t)__popcll(em & lt)] = r;
     }
     nm += (uint32_t)__popcll(em);
@@ -997,6 +1004,316 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   do {                 \
   } while (0)
 #endif
+  // ---- exact blocks: conversions between the two forms and the exact rule (k_labs) on the wave
+  // the exact state -> the ordered formulation's, when regular after the key's event at clock clkl
+  // (la_regular's conditions, every entry past the clock, every pair's E_D past it)
+  auto to_wave = [&](int64_t clkl) __attribute__((always_inline)) {
+    LaWait w{};
+    if (lane < nal) w = A[lane];
+    const int64_t qp = __shfl_up(qe, 1, 64);
+    bool bad = lane >= 1 && lane < nef && qe < qp;   // the queue sorted
+    bad |= lane < nef && (qe <= clkl || Qat);          // every entry the clock reached has fired
+    const int64_t dp = __shfl_up(w.due, 1, 64);
+    bad |= lane >= 1 && lane < nal && w.due < dp;      // the pairs by due, each completed by the last event
+    bad |= lane < nal && w.due - Tw > last;
+    const int64_t dd = min(w.xts, w.yts) + Wb;
+    const int64_t ddp = __shfl_up(dd, 1, 64);
+    bad |= lane >= 1 && lane < nal - xnae && dd < ddp; // the pending pairs' expiry bounds in list order
+    int64_t sl = lane < nal ? max(w.xts, w.yts) : INT64_MIN;
+    for (int o = 32; o > 0; o >>= 1) sl = max(sl, (int64_t)__shfl_xor(sl, o, 64));
+    bool ubad = false;
+    if (nef > 0) {
+      const int64_t tmax = la_rl64(qe, nef - 1);
+      ubad = last == INT64_MIN || tmax > last + Tw || lsched < tmax;
+    }
+    ubad |= hx && (xts > last || xts < sl);
+    ubad |= hy && (yts > last || yts < sl);
+    int64_t ed = w.due;  // E_D: the first queued entry past D
+    for (int i = 0; i < nef; i++) {
+      const int64_t t = la_rl64(qe, i);
+      if (t > dd) ed = min(ed, t);
+    }
+    bad |= lane < nal && ed <= clkl;
+    if (ubad || __ballot(bad)) return;
+    if (lane < nal) {
+      Aed[lane] = ed;
+      Anae[lane] = lane >= nal - xnae ? 1 : 0;
+      Ac[lane] = -1;
+    }
+    __syncthreads();
+    xm = false;
+  };
+  // the ordered formulation's state -> the exact rule's (its entries all past the clock)
+  auto to_exact = [&]() __attribute__((always_inline)) {
+    const uint64_t m = __ballot(lane < nal && Anae[lane]);
+    const uint64_t all = nal >= 64 ? ~0ull : ((1ull << nal) - 1ull);
+    const uint64_t notq = all & ~m;
+    xnae = notq ? nal - 1 - (63 - __builtin_clzll(notq)) : nal;
+    Qi0 = (int32_t)lo;
+    Qat = false;
+    xm = true;
+  };
+  auto xcompact = [&](uint64_t keep) __attribute__((always_inline)) {
+    LaWait w{};
+    if (lane < nal) w = A[lane];
+    __syncthreads();
+    if ((keep >> lane) & 1ull) A[__popcll(keep & lt)] = w;
+    nal = __popcll(keep);
+    __syncthreads();
+  };
+  // updateState: the new-and-every pairs, stably sorted by due, join the pending list
+  auto xmove_nae = [&]() __attribute__((always_inline)) {
+    if (xnae > 1) {
+      const int b0 = nal - xnae;
+      LaWait w{};
+      if (lane < nal) w = A[lane];
+      const bool in = lane >= b0 && lane < nal;
+      int r = b0;
+      for (int j = b0; j < nal; j++) {
+        const int64_t dj = la_rl64(w.due, j);
+        if (in && (dj < w.due || (dj == w.due && j < lane))) r++;
+      }
+      __syncthreads();
+      if (in) A[r] = w;
+      __syncthreads();
+    }
+    xnae = 0;
+  };
+  auto xpush = [&](int64_t t, int64_t i0, bool at) __attribute__((always_inline)) {
+    if (nef >= LA_WF) {
+      xover = true;
+      return;
+    }
+    if (lane == nef) {
+      qe = t;
+      Qi0 = (int32_t)i0;
+      Qat = at;
+    }
+    nef++;
+  };
+  auto xpop = [&]() __attribute__((always_inline)) {
+    qe = __shfl_down(qe, 1, 64);
+    Qi0 = __shfl_down(Qi0, 1, 64);
+    Qat = __shfl_down((int)Qat, 1, 64) != 0;
+    nef--;
+    if (lane >= nef) {
+      qe = INT64_MAX;
+      Qat = false;
+    }
+  };
+  // the first batch index in [a, b] whose clock reaches thr (64 lanes over the coarse clock, then over
+  // the block's clocks)
+  auto xresolve = [&](int64_t a, int64_t b, int64_t thr) __attribute__((always_inline)) -> int64_t {
+    int64_t jb = a >> 6;
+    const int64_t je = b >> 6;
+    for (;;) {
+      const int64_t j = jb + lane;
+      const uint64_t m = __ballot(j <= je && D.rc[j] >= thr);
+      if (m) {
+        jb += __builtin_ctzll(m);
+        break;
+      }
+      jb += 64;
+      if (jb > je) {
+        jb = je;
+        break;
+      }
+    }
+    const int64_t i = (jb << 6) + lane;
+    const uint64_t m = __ballot(i >= a && i <= b && B.rmax[i] >= thr);
+    return m ? (jb << 6) + __builtin_ctzll(m) : b;
+  };
+  // AbsentStreamPreStateProcessor.process for the timer of entry et, at the firing send: a known
+  // one (pex: pidx, its clock pclk) or the first send from plo on whose clock reaches pthr (<= upto)
+  auto xprocess = [&](int64_t et, bool pex, int64_t pidx, int64_t pclk, int64_t plo, int64_t pthr, int64_t upto)
+                      __attribute__((always_inline)) {
+    xmove_nae();
+    LaWait w{};
+    if (lane < nal) w = A[lane];
+    const bool in = lane < nal;
+    const bool ex = in && la_expired(w.xts, w.yts, et, Wn);
+    const bool emt = in && !ex && et >= w.due;
+    const uint64_t em = __ballot(emt);
+    if (emit_on && em) {
+      const uint32_t c = (uint32_t)__popcll(em);
+      if (nm + c > rcap) {
+        e |= LA_BOUND;
+      } else if (emt) {
+        LaRec r;
+        r.due = et;  // the match's ts: the timer's time
+        r.xseq = w.xseq;
+        r.yseq = w.yseq;
+        r.flo = (uint32_t)(pex ? pidx : plo);
+        r.fhi = (uint32_t)(pex ? pidx : upto);
+        r.thr = pex ? INT64_MIN : pthr;
+        rec[nm + (uint32_t)__popcll(em & lt)] = r;
+      }
+      nm += c;
+    }
+    const uint64_t keep = __ballot(in && !ex && !emt);
+    if (__popcll(keep) != nal) xcompact(keep);
+    if (pex && pclk > Tw + et) lsched = pclk + Tw;
+    if (!em && lsched < et) {  // the re-arm
+      lsched = et + Tw;
+      xpush(et + Tw, pex ? pidx : plo, false);
+    }
+  };
+  // the queue's heads that fire at a send in the window [lo, upto] (the clock at upto: clk_upto), in
+  // FIFO order: an entry fires at the first send that sets the clock to or past it, behind the entries
+  // ahead of it (Scheduler.sendTimerEvents; k_labs' fire / la_fire_at)
+  auto xfire = [&](int64_t upto, int64_t clk_upto) __attribute__((always_inline)) {
+    bool hp = false, pex = false;
+    int64_t pidx = 0, pclk = 0, plo = 0, pthr = 0;
+    while (nef > 0 && !xover) {
+      const int64_t t = la_rl64(qe, 0);
+      const bool at = __builtin_amdgcn_readlane((int)Qat, 0) != 0;
+      bool cex = pex;
+      int64_t cidx = pidx, cclk = pclk, clo = plo, cthr = pthr;
+      if (at) {  // reached when queued: the next send that sets the clock (or the previous firing's)
+        if (!hp) {
+          int64_t a = -1;
+          for (int64_t c0 = lo; c0 <= upto && a < 0; c0 += 64) {
+            const int64_t i = c0 + lane;
+            const uint64_t m = __ballot(i <= upto && B.tclk[i] == B.rmax[i]);
+            if (m) a = c0 + __builtin_ctzll(m);
+          }
+          if (a < 0) break;
+          cex = true;
+          cidx = a;
+          cclk = B.rmax[a];
+        }
+      } else {
+        if (!hp) {
+          cex = false;
+          clo = lo;
+          cthr = t;
+        } else if (pex) {
+          if (pclk < t) {
+            cex = false;
+            clo = pidx + 1;
+            cthr = t;
+          }
+        } else if (t > pthr) {
+          cthr = t;
+        }
+        if (!cex && clk_upto < cthr) break;
+      }
+      xpop();
+      hp = true;
+      pex = cex;
+      pidx = cidx;
+      pclk = cclk;
+      plo = clo;
+      pthr = cthr;
+      if (!pex && pthr + mstep > t + Tw) {  // the clock at the send may pass t + T: find the send
+        pidx = xresolve(plo, upto, pthr);
+        pclk = B.rmax[pidx];
+        pex = true;
+      }
+      xprocess(t, pex, pidx, pclk, plo, pthr, upto);
+    }
+  };
+  // one key event q of the block (lane q's registers) by the exact rule (k_labs' step)
+  auto xstep = [&](int q, int64_t ts_, int64_t clk_, uint32_t g_, uint32_t v_, int role_, bool en_, bool qf_)
+                   __attribute__((always_inline)) {
+    const int64_t t = la_rl64(ts_, q), xc = la_rl64(clk_, q);
+    const uint32_t xg = (uint32_t)__builtin_amdgcn_readlane((int)g_, q);
+    const uint32_t xv_ = (uint32_t)__builtin_amdgcn_readlane((int)v_, q);
+    const int xr = __builtin_amdgcn_readlane(role_, q);
+    const bool xen = __builtin_amdgcn_readlane((int)en_, q) != 0;
+    const bool xqf = __builtin_amdgcn_readlane((int)qf_, q) != 0;
+    xfire((int64_t)xg, xc);
+    lo = (int64_t)xg + 1;
+    lclk = xc;
+    last = t;
+    if (xover) return;
+    // expireEvents: the partial; the pending list's expired head, every expired new-and-every pair
+    if (useW && ((hx && llabs(xts - t) > Wn) || (hy && llabs(yts - t) > Wn))) {
+      hx = hy = false;
+      xseq = yseq = -1;
+      fl = 0;
+    }
+    if (useW && nal > 0) {
+      LaWait w{};
+      if (lane < nal) w = A[lane];
+      const uint64_t exm = __ballot(lane < nal && la_expired(w.xts, w.yts, t, Wn));
+      if (exm) {
+        const int np = nal - xnae;
+        const uint64_t pm = np >= 64 ? ~0ull : ((1ull << np) - 1ull);
+        const uint64_t all = nal >= 64 ? ~0ull : ((1ull << nal) - 1ull);
+        const uint64_t live = ~exm & pm;
+        const int nh = live ? __builtin_ctzll(live) : np;
+        const uint64_t drop = (nh >= 64 ? ~0ull : ((1ull << nh) - 1ull)) | (exm & all & ~pm);
+        const uint64_t keep = all & ~drop;
+        if (keep != all) {
+          const int nk = __popcll(keep & ~pm);
+          xcompact(keep);
+          xnae = nk;
+        }
+      }
+    }
+    if (xr < 0) return;
+    if (xr == 2) {  // Z: new-and-every -> pending, then each pending pair fz matches is dropped
+      xmove_nae();
+      LaWait w{};
+      if (lane < nal) w = A[lane];
+      const LaVals V{w.xv, w.yv, xv_, (w.fl & 1u) != 0, (w.fl & 2u) != 0, xen, t0g, t1g, t2g};
+      const uint64_t km = __ballot(lane < nal && la_pred(D.fz, V));
+      if (km) {
+        lsched = t + Tw;
+        for (int i = __popcll(km); i > 0; i--) xpush(t + Tw, (int64_t)xg + 1, xc >= t + Tw);
+        const uint64_t all = nal >= 64 ? ~0ull : ((1ull << nal) - 1ull);
+        xcompact(all & ~km);
+      }
+      return;
+    }
+    if (!xqf) return;  // X / Y: its own filter (la_pack_q)
+    const int64_t sq = bseq(B, (int64_t)xg);
+    const bool en1 = xen;
+    if (xr == 0 && !hx) {
+      hx = true;
+      xseq = sq;
+      xts = t;
+      xv = xv_;
+      fl = (fl & ~1u) | (en1 ? 1u : 0u);
+    } else if (xr == 1 && !hy) {
+      hy = true;
+      yseq = sq;
+      yts = t;
+      yv = xv_;
+      fl = (fl & ~2u) | (en1 ? 2u : 0u);
+    } else {
+      return;  // the slot is taken: the partial waits for its partner
+    }
+    if (hx && hy) {  // the pair completes: new-and-every of the absent state, an entry t + T
+      if (nal >= 64) {
+        xover = true;
+        return;
+      }
+      if (lane == nal) {
+        LaWait w;
+        w.due = t + Tw;
+        w.xseq = xseq;
+        w.xts = xts;
+        w.yseq = yseq;
+        w.yts = yts;
+        w.xv = xv;
+        w.yv = yv;
+        w.fl = fl;
+        w.pad = 0;
+        A[nal] = w;
+      }
+      __syncthreads();
+      nal++;
+      xnae++;
+      lsched = t + Tw;
+      xpush(t + Tw, (int64_t)xg + 1, xc >= t + Tw);
+      hx = hy = false;
+      xseq = yseq = -1;
+      fl = 0;
+    }
+  };
+  to_wave(B.clock0);  // the carried state: the ordered formulation's when regular
   // the key's events 64 at a time; the next block's loads are issued before this one is worked
   int64_t n_ts = 0, n_clk = 0;
   uint32_t n_g = 0, n_v = 0, n_n = 1;
@@ -1028,17 +1345,22 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       sp->lo = lo;
       sp->nal = (uint32_t)nal;
       sp->nef = (uint32_t)nef;
+      sp->xm = xm ? 1u : 0u;
+      sp->xnae = xm ? (uint32_t)xnae : 0u;
     }
+    const uint64_t qa = __ballot(xm && lane < nef && Qat);
+    if (lane == 0) sp->qat = qa;
     if (lane < nal) {
       sp->A[lane] = A[lane];
-      sp->ed[lane] = Aed[lane];
-      sp->nae[lane] = Anae[lane];
+      sp->ed[lane] = xm ? 0 : Aed[lane];
+      sp->nae[lane] = xm ? 0 : Anae[lane];
     }
     if (lane < nef) sp->qe[lane] = qe;
   };
   fetch(w_beg);
   for (uint32_t j0 = w_beg; j0 < s_end; j0 += 64) {
     if (j0 == s_beg && h > 0) {  // the cut: the state the warm-up reached
+      if (xm) to_wave(lclk);
       dump(D.snap[0] + ks);
       emit_on = true;
     }
@@ -1051,16 +1373,24 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     const bool qf = (n_n & 2u) != 0;  // its own filter (la_pack_q)
     if (j0 + 64 < s_end) fetch(j0 + 64);
     {  // the ordered formulation: timestamps do not decrease within the key, and no event lags the
-       // clock by T or more (an entry queued then could fire at a send far past it)
+       // clock by T or more (an entry queued then could fire at a send far past it); a block that
+       // breaks it runs the exact rule
       const int64_t tp = __shfl_up(ts, 1, 64);
       const int64_t prev = lane == 0 ? last : tp;
-      if (__ballot(valid && ((prev != INT64_MIN && ts < prev) || clk - ts >= Tw))) {
+      if (!xm && __ballot(valid && ((prev != INT64_MIN && ts < prev) || clk - ts >= Tw))) to_exact();
+    }
+    if (xm) {
+#pragma unroll 1
+      for (int q = 0; q < nv && !xover; q++) xstep(q, ts, clk, g, v, role, en, qf);
+      if (xover) {
         if (lane == 0) {
           D.cm[ks] = 0;
           atomicOr(err, LA_SLOW);
         }
         return;
       }
+      to_wave(lclk);  // (still exact after it: the next block runs the exact rule too)
+      continue;
     }
     const int64_t seqg = bseq(B, g);
     const uint64_t QX = __ballot(valid && role == 0 && qf);
@@ -1439,6 +1769,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     LA_STAMP(5);
     lo = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)g, nv - 1) + 1;
     last = la_rl64(ts, nv - 1);
+    lclk = clkl;
     __syncthreads();
   }
   auto stamps_out = [&]() {
@@ -1450,6 +1781,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   };
   if (!lastseg) {  // the state this segment ends with, for the next one's check; no push-end settle
     stamps_out();
+    if (xm) to_wave(lclk);
     dump(D.snap[1] + ks + 1);
     if (lane == 0) D.cm[ks] = min(nm, rcap);
     if (e) atomicOr(err, e);
@@ -1457,6 +1789,51 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   }
   // the timers the push's last clock reaches
   const int64_t lastclk = B.n > 0 ? B.rmax[B.n - 1] : B.clock0;
+  if (xm) {  // the exact rule's push end (k_labs): the timers the last clock reaches, then its state
+    if (B.n > 0) xfire(B.n - 1, lastclk);
+    if (xover) {
+      if (lane == 0) {
+        D.cm[ks] = 0;
+        atomicOr(err, LA_SLOW);
+      }
+      return;
+    }
+    stamps_out();
+    if (nal > cap || nef > cap) {
+      e |= E_LIST;
+    } else {
+      if (lane < nal) D.wq[wr][(int64_t)k * cap + lane] = A[lane];
+      if (lane < nef) {
+        LaEnt y;
+        y.t = qe;
+        y.i0 = 0;
+        y.pad = 0;
+        D.fq[wr][(int64_t)k * cap + lane] = y;
+      }
+    }
+    if (lane == 0) {
+      D.cm[ks] = min(nm, rcap);
+      LaPend s{};
+      s.xseq = hx ? xseq : -1;
+      s.yseq = hy ? yseq : -1;
+      s.xts = xts;
+      s.yts = yts;
+      s.xv = xv;
+      s.yv = yv;
+      s.fl = fl;
+      s.nw = nal;
+      s.wh = 0;
+      s.nae = xnae;
+      s.last = last;
+      s.lst = lsched;
+      s.ne = nef;
+      s.eh = 0;
+      s.reg = 0;  // (k_labs_w decides from the state itself: to_wave)
+      D.pend[wr][k] = s;
+    }
+    if (e) atomicOr(err, e);
+    return;
+  }
   const bool flushed = __ballot(lane < nef && qe <= lastclk) != 0;  // a firing after every event of the key
   if (nal > 0) {
     LaWait w{};
@@ -1547,11 +1924,12 @@ static __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B,
     }
     const LaRec x = rec[r];
     int64_t a = x.flo, b = min((int64_t)x.fhi, B.n - 1);
-    if (D.rc && a < b) {  // the 64-event block first reaching due (rc: each block's last clock), then within it
+    if (x.thr == INT64_MIN) b = a;  // (an exact block's firing at a known send)
+    if (D.rc && a < b) {  // the 64-event block first reaching thr (rc: each block's last clock), then within it
       int64_t ja = a >> 6, jb = b >> 6;
       while (ja < jb) {
         const int64_t mid = ja + ((jb - ja) >> 1);
-        if (D.rc[mid] >= x.due) jb = mid;
+        if (D.rc[mid] >= x.thr) jb = mid;
         else ja = mid + 1;
       }
       a = max(a, ja << 6);
@@ -1559,7 +1937,7 @@ static __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B,
     }
     while (a < b) {
       const int64_t mid = a + ((b - a) >> 1);
-      if (B.rmax[mid] >= x.due) b = mid;
+      if (B.rmax[mid] >= x.thr) b = mid;
       else a = mid + 1;
     }
     O.key[m] = B.partitioned ? k : 0;
@@ -1592,7 +1970,7 @@ static __global__ __launch_bounds__(64) void k_labs_segcheck(LabsDev D, const ui
   if (lane == 0)
     bad = a.xseq != b.xseq || a.yseq != b.yseq || a.xts != b.xts || a.yts != b.yts || a.xv != b.xv || a.yv != b.yv ||
           a.fl != b.fl || a.hxy != b.hxy || a.last != b.last || a.lsched != b.lsched || a.lo != b.lo ||
-          a.nal != b.nal || a.nef != b.nef;
+          a.nal != b.nal || a.nef != b.nef || a.xm != b.xm || a.xnae != b.xnae || a.qat != b.qat;
   const uint32_t nal = min(a.nal, 64u), nef = min(a.nef, 64u);
   if ((uint32_t)lane < nal && (uint32_t)lane < b.nal) {
     const LaWait& x = a.A[lane];
@@ -1774,6 +2152,8 @@ struct LabsState {
         (void)hipMemsetAsync(D.maxstep, 0, sizeof(unsigned long long), s);
         if (B.n > 1) k_labs_steps<<<1024, 256, 0, s>>>(B.rmax, B.n, D.maxstep);
       }
+      // the coarse clock (each 64-event block's last) for k_labs_w's exact blocks and k_labs_out
+      if (D.rc && B.n > 0) k_labs_coarse<<<(unsigned)(((B.n + 63) / 64 + 255) / 256), 256, 0, s>>>(B.rmax, B.n, D.rc);
       kt.mark("labs", s);
       const int H = noseg ? 1 : D.seg;
       const unsigned gs = (unsigned)(D.nk * D.seg);
@@ -1787,7 +2167,6 @@ struct LabsState {
       size_t tb = tmp_bytes;
       (void)rocprim::exclusive_scan(tmp, tb, D.cm, D.om, 0u, (size_t)gs, rocprim::plus<uint32_t>(), s);
       kt.mark("labs_out", s);
-      if (D.rc && B.n > 0) k_labs_coarse<<<(unsigned)(((B.n + 63) / 64 + 255) / 256), 256, 0, s>>>(B.rmax, B.n, D.rc);
       k_labs_out<<<(gs + 3) / 4, 256, 0, s>>>(D, B, O, kbeg, kcnt, H, err);
       kt.mark(nullptr, s);
       return;

@@ -88,7 +88,7 @@ def loop_waits(text: str):
     return res
 
 
-TOOLS = ("llvm-objcopy", "clang-offload-bundler", "llvm-objdump", "llvm-cxxfilt")
+TOOLS = ("llvm-objcopy", "clang-offload-bundler", "llvm-objdump")  # (c++filt stands in for llvm-cxxfilt)
 
 
 def collect():
