@@ -32,6 +32,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 BYTES_PER_EVENT = 16    # ts 8 + key 4 + price 4
+# SURVEY.md §8d per config: C4 reads the stream id too (17 B/event: ts 8 + key 4 + stream 1 + price 4)
+BYTES_PER_EVENT_CFG = {"4": 17}
 BYTES_PER_MATCH = {"pairs32": 8,  # (e2 batch index, e2 seq - e1 seq) as two u32 (SHP_LAYOUT_PAIRS32)
                    "pairs": 16,  # one (e1 seq, e2 seq) pair of int64 (SHP_LAYOUT_PAIRS)
                    "agg": 12,    # (key u32, aggregate f64) per match (SHP_LAYOUT_AGG, C5)
@@ -296,7 +298,8 @@ def main():
         # per launch of the dominant kernel on rank 0's (first local) engine: the events it received
         ev_per_launch = ev_total / G / a.steps
         m_per_launch = m_total / G / a.steps
-        alg_bytes = BYTES_PER_EVENT * ev_per_launch + BYTES_PER_MATCH[layout] * m_per_launch
+        bpe = BYTES_PER_EVENT_CFG.get(str(cfg_id), BYTES_PER_EVENT)
+        alg_bytes = bpe * ev_per_launch + BYTES_PER_MATCH[layout] * m_per_launch
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
         traffic = step_traffic = None
         pmc_src = None
@@ -306,6 +309,7 @@ def main():
                 # PMC passes are of one bench command (tools/pmc_run.sh) on one library build: used
                 # only for that config, key count and build (the same .so as this run loaded)
                 if (str(pm.get("config", "2")) == str(cfg_id) and int(pm.get("keys", K)) == K and G == 1
+                        and float(pm.get("disorder", 0.0)) == a.disorder
                         and pm.get("lib_sha16") == _lib_sha16(native.LIB_PATH)):
                     ks = pm.get("kernels", {})
                     traffic = ks.get(dom, {}).get("hbm_bytes_per_launch")
@@ -370,7 +374,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": alg_bytes,
-                "bytes_per_event": BYTES_PER_EVENT,
+                "bytes_per_event": bpe,
                 "bytes_per_match": BYTES_PER_MATCH[layout],
                 "kernel_ms_per_launch": {k: v / a.steps for k, v in sorted(kernel_ms.items()) if v > 0},
                 # the same algorithmic bytes over the whole step (every kernel of the push, plus the

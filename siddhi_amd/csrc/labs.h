@@ -17,14 +17,19 @@
 // at least T old (ts = the entry), drops the expired ones, and re-arms when it emitted nothing.
 // k_labs_w runs the ordered special case (a key's events do not go back in time, no event lags the
 // clock by T, no clock step beyond T: then the queue stays sorted and a pair fires at its due time)
-// a wave per key, 64 events a step, and leaves the same state; anything else raises LA_SLOW and
-// k_labs re-runs the push from the committed state.  Cross-key ties of the playback scheduler's
+// a wave per key segment, 64 events a step, and leaves the same state.  Since round 6 a block of a
+// key that breaks the ordered case (a ts going back, an event lagging the clock by T) runs the exact
+// rule inside k_labs_w, on the whole wave, and the key returns to the ordered formulation once its
+// state is regular again; only more than 64 pairs / entries or a clock step beyond T raise LA_SLOW
+// (k_labs re-runs the push from the committed state).  Cross-key ties of the playback scheduler's
 // TreeMultimap (one state per due time per onTimeChange) are not modelled, as on the general lanes
 // (parity-unpinned).  The rings (pairs, queue) start at 8 per key and grow x16 per
 // tier in HBM when a push overflows them (the push then re-runs from the committed state).
 //
-// Batch order: the events are packed into 16-byte records and sorted with their keys (k_labs_pack2
-// + one rocPRIM radix sort), so each key's events are contiguous.
+// Batch order: since round 5 a stable multisplit by key (k_la_ms_count, one scan, k_la_ms_scatter:
+// one wave per 16k-event segment writes each event's 16-byte record at its key-order position), so
+// each key's events are contiguous; up to 4096 keys (LA_MS_BINS), else the 16-byte records are
+// sorted with their keys (k_labs_pack2 + one rocPRIM radix sort).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -865,7 +870,13 @@ __host__ __device__ __forceinline__ uint32_t la_segb(uint32_t cnt, int hk, int i
 __host__ __device__ inline bool la_fz1(const LaPredD& p) {
   return p.n == 1 && ((p.t[0].ak == 3) != (p.t[0].bk == 3));
 }
-template <bool FZ1>
+// XB: the exact blocks (round 6) are a second variant of the kernel, so the ordered formulation's
+// variant keeps its registers: it marks a (key, segment) whose blocks break the formulation
+// (cm = LA_XMARK) and stops there; the XB variant, launched after it, re-runs only the marked ones
+// from the committed state, the broken blocks by the exact rule (the records and state of the others
+// stand).
+constexpr uint32_t LA_XMARK = 0xFFFFFFFFu;
+template <bool FZ1, bool XB>
 static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
                                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                                int H, int* err) {
@@ -878,6 +889,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   const int S = D.seg;  // slot stride
   const int k = blockIdx.x / S, h = blockIdx.x % S, ks = blockIdx.x;
   if (k >= D.nk) return;
+  if (XB && D.cm[ks] != LA_XMARK) return;  // (the ordered variant ran this one through)
   const int lane = (int)threadIdx.x;
   const uint32_t beg = kbeg[k], cnt = kcnt[k];
   const int hk = la_nseg(cnt, H);
@@ -930,6 +942,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   // lastScheduledTime.  The carried state starts here too and converts when regular.
   int32_t Qi0 = 0;
   bool Qat = lane < nef && qe <= B.clock0;
+  LaWait P{};          // exact mode: pair `lane` of the absent state's lists (list order), in registers
   int xnae = s0.nae;
   bool xm = true;      // exact mode (wave-uniform)
   bool xover = false;  // exact mode outgrew 64 pairs or entries: the push re-runs on k_labs
@@ -938,6 +951,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     const LaWait w = D.wq[rd][(int64_t)k * cap + ((s0.wh + lane) & msk)];
     A[lane] = w;
     Ac[lane] = -1;
+    P = w;
   }
   __syncthreads();
   LaRec* rec = D.rec + la_region(beg + s_beg, ks);
@@ -1008,8 +1022,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   // the exact state -> the ordered formulation's, when regular after the key's event at clock clkl
   // (la_regular's conditions, every entry past the clock, every pair's E_D past it)
   auto to_wave = [&](int64_t clkl) __attribute__((always_inline)) {
-    LaWait w{};
-    if (lane < nal) w = A[lane];
+    const LaWait w = P;
     const int64_t qp = __shfl_up(qe, 1, 64);
     bool bad = lane >= 1 && lane < nef && qe < qp;   // the queue sorted
     bad |= lane < nef && (qe <= clkl || Qat);          // every entry the clock reached has fired
@@ -1036,6 +1049,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     bad |= lane < nal && ed <= clkl;
     if (ubad || __ballot(bad)) return;
     if (lane < nal) {
+      A[lane] = w;
       Aed[lane] = ed;
       Anae[lane] = lane >= nal - xnae ? 1 : 0;
       Ac[lane] = -1;
@@ -1051,31 +1065,33 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     xnae = notq ? nal - 1 - (63 - __builtin_clzll(notq)) : nal;
     Qi0 = (int32_t)lo;
     Qat = false;
+    P = lane < nal ? A[lane] : LaWait{};
     xm = true;
   };
+  // the pairs in registers move between lanes through A[] (a scratch in exact mode)
   auto xcompact = [&](uint64_t keep) __attribute__((always_inline)) {
-    LaWait w{};
-    if (lane < nal) w = A[lane];
     __syncthreads();
-    if ((keep >> lane) & 1ull) A[__popcll(keep & lt)] = w;
+    if ((keep >> lane) & 1ull) A[__popcll(keep & lt)] = P;
     nal = __popcll(keep);
     __syncthreads();
+    P = lane < nal ? A[lane] : LaWait{};
   };
   // updateState: the new-and-every pairs, stably sorted by due, join the pending list
   auto xmove_nae = [&]() __attribute__((always_inline)) {
     if (xnae > 1) {
       const int b0 = nal - xnae;
-      LaWait w{};
-      if (lane < nal) w = A[lane];
       const bool in = lane >= b0 && lane < nal;
       int r = b0;
       for (int j = b0; j < nal; j++) {
-        const int64_t dj = la_rl64(w.due, j);
-        if (in && (dj < w.due || (dj == w.due && j < lane))) r++;
+        const int64_t dj = la_rl64(P.due, j);
+        if (in && (dj < P.due || (dj == P.due && j < lane))) r++;
       }
-      __syncthreads();
-      if (in) A[r] = w;
-      __syncthreads();
+      if (__ballot(in && r != (int)lane)) {  // (already in order: nothing moves)
+        __syncthreads();
+        if (in) A[r] = P;
+        __syncthreads();
+        if (in) P = A[lane];
+      }
     }
     xnae = 0;
   };
@@ -1128,8 +1144,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   auto xprocess = [&](int64_t et, bool pex, int64_t pidx, int64_t pclk, int64_t plo, int64_t pthr, int64_t upto)
                       __attribute__((always_inline)) {
     xmove_nae();
-    LaWait w{};
-    if (lane < nal) w = A[lane];
+    const LaWait w = P;
     const bool in = lane < nal;
     const bool ex = in && la_expired(w.xts, w.yts, et, Wn);
     const bool emt = in && !ex && et >= w.due;
@@ -1234,9 +1249,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       fl = 0;
     }
     if (useW && nal > 0) {
-      LaWait w{};
-      if (lane < nal) w = A[lane];
-      const uint64_t exm = __ballot(lane < nal && la_expired(w.xts, w.yts, t, Wn));
+      const uint64_t exm = __ballot(lane < nal && la_expired(P.xts, P.yts, t, Wn));
       if (exm) {
         const int np = nal - xnae;
         const uint64_t pm = np >= 64 ? ~0ull : ((1ull << np) - 1ull);
@@ -1255,9 +1268,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     if (xr < 0) return;
     if (xr == 2) {  // Z: new-and-every -> pending, then each pending pair fz matches is dropped
       xmove_nae();
-      LaWait w{};
-      if (lane < nal) w = A[lane];
-      const LaVals V{w.xv, w.yv, xv_, (w.fl & 1u) != 0, (w.fl & 2u) != 0, xen, t0g, t1g, t2g};
+      const LaVals V{P.xv, P.yv, xv_, (P.fl & 1u) != 0, (P.fl & 2u) != 0, xen, t0g, t1g, t2g};
       const uint64_t km = __ballot(lane < nal && la_pred(D.fz, V));
       if (km) {
         lsched = t + Tw;
@@ -1291,19 +1302,16 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
         return;
       }
       if (lane == nal) {
-        LaWait w;
-        w.due = t + Tw;
-        w.xseq = xseq;
-        w.xts = xts;
-        w.yseq = yseq;
-        w.yts = yts;
-        w.xv = xv;
-        w.yv = yv;
-        w.fl = fl;
-        w.pad = 0;
-        A[nal] = w;
+        P.due = t + Tw;
+        P.xseq = xseq;
+        P.xts = xts;
+        P.yseq = yseq;
+        P.yts = yts;
+        P.xv = xv;
+        P.yv = yv;
+        P.fl = fl;
+        P.pad = 0;
       }
-      __syncthreads();
       nal++;
       xnae++;
       lsched = t + Tw;
@@ -1314,6 +1322,10 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     }
   };
   to_wave(B.clock0);  // the carried state: the ordered formulation's when regular
+  if (!XB && xm) {  // (the exact variant takes this one)
+    if (lane == 0) D.cm[ks] = LA_XMARK;
+    return;
+  }
   // the key's events 64 at a time; the next block's loads are issued before this one is worked
   int64_t n_ts = 0, n_clk = 0;
   uint32_t n_g = 0, n_v = 0, n_n = 1;
@@ -1351,37 +1363,63 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     const uint64_t qa = __ballot(xm && lane < nef && Qat);
     if (lane == 0) sp->qat = qa;
     if (lane < nal) {
-      sp->A[lane] = A[lane];
+      sp->A[lane] = xm ? P : A[lane];
       sp->ed[lane] = xm ? 0 : Aed[lane];
       sp->nae[lane] = xm ? 0 : Anae[lane];
     }
     if (lane < nef) sp->qe[lane] = qe;
   };
   fetch(w_beg);
-  for (uint32_t j0 = w_beg; j0 < s_end; j0 += 64) {
+  uint32_t adv = 64;  // events this step took (exact stretches hand the rest of a block back early)
+  for (uint32_t j0 = w_beg; j0 < s_end; j0 += adv) {
     if (j0 == s_beg && h > 0) {  // the cut: the state the warm-up reached
-      if (xm) to_wave(lclk);
+      if (XB && xm) to_wave(lclk);
       dump(D.snap[0] + ks);
       emit_on = true;
     }
-    const int nv = (int)min(64u, s_end - j0);
+    const uint32_t jend = (h > 0 && j0 < s_beg) ? s_beg : s_end;  // (a step never crosses the cut)
+    const int nv = (int)min(64u, jend - j0);
+    adv = (uint32_t)nv;
     const bool valid = lane < nv;
     const int64_t ts = n_ts, clk = n_clk;
     const uint32_t g = n_g, v = n_v;
     const int role = valid ? n_st : -1;
     const bool en = (n_n & 1u) != 0;
     const bool qf = (n_n & 2u) != 0;  // its own filter (la_pack_q)
-    if (j0 + 64 < s_end) fetch(j0 + 64);
+    if (j0 + nv < s_end) fetch(j0 + nv);
+    uint64_t brk;
     {  // the ordered formulation: timestamps do not decrease within the key, and no event lags the
        // clock by T or more (an entry queued then could fire at a send far past it); a block that
        // breaks it runs the exact rule
       const int64_t tp = __shfl_up(ts, 1, 64);
       const int64_t prev = lane == 0 ? last : tp;
-      if (!xm && __ballot(valid && ((prev != INT64_MIN && ts < prev) || clk - ts >= Tw))) to_exact();
+      brk = __ballot(valid && ((prev != INT64_MIN && ts < prev) || clk - ts >= Tw));
+      if (!xm && brk) {
+        if constexpr (!XB) {  // the exact variant re-runs this (key, segment)
+          if (lane == 0) D.cm[ks] = LA_XMARK;
+          return;
+        }
+        to_exact();
+      }
     }
-    if (xm) {
+    if (XB && xm) {
+      // the exact rule through the event after the block's last break (or 8 events when the block
+      // has none: a carried irregular state), then back to the ordered formulation when the state is
+      // regular there -- its next step starts after that event -- else the block's rest exactly
+      const int E = brk ? min(64 - __builtin_clzll(brk), nv - 1) : min(7, nv - 1);
+      int q = 0;
 #pragma unroll 1
-      for (int q = 0; q < nv && !xover; q++) xstep(q, ts, clk, g, v, role, en, qf);
+      for (; q <= E && !xover; q++) xstep(q, ts, clk, g, v, role, en, qf);
+      if (!xover && q < nv) {
+        to_wave(lclk);
+        if (!xm) {
+          adv = (uint32_t)q;
+          fetch(j0 + adv);  // (the prefetch above read the step after this block)
+          continue;
+        }
+#pragma unroll 1
+        for (; q < nv && !xover; q++) xstep(q, ts, clk, g, v, role, en, qf);
+      }
       if (xover) {
         if (lane == 0) {
           D.cm[ks] = 0;
@@ -1781,7 +1819,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   };
   if (!lastseg) {  // the state this segment ends with, for the next one's check; no push-end settle
     stamps_out();
-    if (xm) to_wave(lclk);
+    if (XB && xm) to_wave(lclk);
     dump(D.snap[1] + ks + 1);
     if (lane == 0) D.cm[ks] = min(nm, rcap);
     if (e) atomicOr(err, e);
@@ -1789,7 +1827,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   }
   // the timers the push's last clock reaches
   const int64_t lastclk = B.n > 0 ? B.rmax[B.n - 1] : B.clock0;
-  if (xm) {  // the exact rule's push end (k_labs): the timers the last clock reaches, then its state
+  if (XB && xm) {  // the exact rule's push end (k_labs): the timers the last clock reaches, then its state
     if (B.n > 0) xfire(B.n - 1, lastclk);
     if (xover) {
       if (lane == 0) {
@@ -1802,7 +1840,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     if (nal > cap || nef > cap) {
       e |= E_LIST;
     } else {
-      if (lane < nal) D.wq[wr][(int64_t)k * cap + lane] = A[lane];
+      if (lane < nal) D.wq[wr][(int64_t)k * cap + lane] = P;
       if (lane < nef) {
         LaEnt y;
         y.t = qe;
@@ -2157,8 +2195,13 @@ struct LabsState {
       kt.mark("labs", s);
       const int H = noseg ? 1 : D.seg;
       const unsigned gs = (unsigned)(D.nk * D.seg);
-      if (la_fz1(D.fz)) k_labs_w<true><<<gs, 64, 0, s>>>(D, B, perm, kbeg, kcnt, H, err);
-      else k_labs_w<false><<<gs, 64, 0, s>>>(D, B, perm, kbeg, kcnt, H, err);
+      if (la_fz1(D.fz)) {
+        k_labs_w<true, false><<<gs, 64, 0, s>>>(D, B, perm, kbeg, kcnt, H, err);
+        k_labs_w<true, true><<<gs, 64, 0, s>>>(D, B, perm, kbeg, kcnt, H, err);  // (the marked ones only)
+      } else {
+        k_labs_w<false, false><<<gs, 64, 0, s>>>(D, B, perm, kbeg, kcnt, H, err);
+        k_labs_w<false, true><<<gs, 64, 0, s>>>(D, B, perm, kbeg, kcnt, H, err);
+      }
       if (H > 1) {
         kt.mark("labs_segcheck", s);
         k_labs_segcheck<<<gs, 64, 0, s>>>(D, kcnt, H, err);

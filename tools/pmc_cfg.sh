@@ -10,7 +10,7 @@ OUT=gpurun_out/pmc_$CFG
 mkdir -p $OUT
 A="SQ_WAVES SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_LDS"
 B="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
-ARGS="--config $CFG --steps 2 --warmup 1 --no-cpu-baseline --latency-batches 0 ${BENCH_ARGS}"
+ARGS="--config $CFG --steps 2 --warmup 1 --no-cpu-baseline --latency-batches 0 --e2e-steps 0 ${BENCH_ARGS}"
 if [ -z "$NO_LV" ]; then
   timeout -s KILL 200 rocprofv3 --pmc $A --output-format csv -d $OUT/w_a -o p -- python3 -u bench.py $ARGS > $OUT/w_a.log 2>&1 || exit $?
   timeout -s KILL 200 rocprofv3 --pmc $B --output-format csv -d $OUT/w_b -o p -- python3 -u bench.py $ARGS > $OUT/w_b.log 2>&1 || exit $?

@@ -5,7 +5,7 @@
 # bench.py uses the traffic only for the same config and key count).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --latency-batches 0 ${BENCH_ARGS}"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --latency-batches 0 --e2e-steps 0 ${BENCH_ARGS}"
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats -o run -- python3 -u bench.py $ARGS > gpurun_out/stats.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o p -- python3 -u bench.py $ARGS > gpurun_out/pmc_fetch.log 2>&1 || exit $?

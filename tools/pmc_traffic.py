@@ -51,6 +51,7 @@ def main():
     out = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
                      "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 read correction)",
            "config": os.environ.get("PMC_CONFIG", "2"), "keys": int(os.environ.get("PMC_KEYS", "10000")),
+           "disorder": float(os.environ.get("PMC_DISORDER", "0")),
            "lib_sha16": lib_sha16(), "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f, w = fetch.get(k, 0.0), write.get(k, 0.0)
