@@ -351,6 +351,10 @@ def main():
                 "keys": K,
                 "parallelism": par,
                 "engine_path": _path_desc(eng, layout),
+                # monitoring counters since create (shp_engine_stat): hand-backs and re-runs of the push
+                "engine_stats": ({k: native_stat(eng, k) for k in ("pushes", "lean_fallbacks", "labs_fallbacks",
+                                                                 "labs_segmiss", "sweep_r16_reruns", "spill_reruns")}
+                                 if G == 1 else None),
                 "matches_per_s": m_total / elapsed,
                 "matches_per_step_gpu0": m_per_launch,
                 "p50_batch_ms": float(np.percentile(lat, 50)),

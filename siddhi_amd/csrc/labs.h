@@ -831,7 +831,8 @@ __device__ __forceinline__ bool la_kill(const LaPredD& p, const LaKill& K, doubl
 // per event lane (a completion, or the pairs a Z event kills), all at that event's ts + T.
 constexpr int LA_WF = 64;  // queue entries k_labs_w holds (one per lane)
 // diagnostic build (SHP_SW_STAMPS): per key, phase cycles 0 load, 1 partial, 2 doomed E_D, 3 leave
-// search, 4 settle, 5 queue, 8 Z kills, 9 firings; counts 6 pairs, 7 events, 10 kill rounds, 11 Z events
+// search, 4 settle, 5 queue, 8 Z kills, 9 firings, 13 exact blocks (15: their timer firings); counts
+// 6 pairs, 7 events, 10 kill rounds, 11 Z events, 12 events by the exact rule, 14 run by the exact variant
 constexpr int LA_NSTAMP = 16;
 
 // Segments (round 5).  With few keys (one wave each cannot fill the CUs) a key's events are cut into
@@ -1068,12 +1069,14 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     P = lane < nal ? A[lane] : LaWait{};
     xm = true;
   };
-  // the pairs in registers move between lanes through A[] (a scratch in exact mode)
+  // the pairs in registers move between lanes through A[] (a scratch in exact mode).  The workgroup is
+  // one wave, whose LDS operations complete in order: a wave-scope fence between the stores and the
+  // loads is the whole synchronisation (as in sl_expand_block)
   auto xcompact = [&](uint64_t keep) __attribute__((always_inline)) {
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if ((keep >> lane) & 1ull) A[__popcll(keep & lt)] = P;
     nal = __popcll(keep);
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     P = lane < nal ? A[lane] : LaWait{};
   };
   // updateState: the new-and-every pairs, stably sorted by due, join the pending list
@@ -1087,9 +1090,9 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
         if (in && (dj < P.due || (dj == P.due && j < lane))) r++;
       }
       if (__ballot(in && r != (int)lane)) {  // (already in order: nothing moves)
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (in) A[r] = P;
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (in) P = A[lane];
       }
     }
@@ -1237,7 +1240,9 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
     const int xr = __builtin_amdgcn_readlane(role_, q);
     const bool xen = __builtin_amdgcn_readlane((int)en_, q) != 0;
     const bool xqf = __builtin_amdgcn_readlane((int)qf_, q) != 0;
+    LA_STAMP(13);
     xfire((int64_t)xg, xc);
+    LA_STAMP(15);
     lo = (int64_t)xg + 1;
     lclk = xc;
     last = t;
@@ -1378,48 +1383,59 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
       emit_on = true;
     }
     const uint32_t jend = (h > 0 && j0 < s_beg) ? s_beg : s_end;  // (a step never crosses the cut)
-    const int nv = (int)min(64u, jend - j0);
-    adv = (uint32_t)nv;
-    const bool valid = lane < nv;
+    const int nv0 = (int)min(64u, jend - j0);
     const int64_t ts = n_ts, clk = n_clk;
     const uint32_t g = n_g, v = n_v;
-    const int role = valid ? n_st : -1;
+    const int st0 = n_st;
     const bool en = (n_n & 1u) != 0;
     const bool qf = (n_n & 2u) != 0;  // its own filter (la_pack_q)
-    if (j0 + nv < s_end) fetch(j0 + nv);
     uint64_t brk;
+    int nv = nv0;
     {  // the ordered formulation: timestamps do not decrease within the key, and no event lags the
        // clock by T or more (an entry queued then could fire at a send far past it); a block that
-       // breaks it runs the exact rule
+       // breaks it runs the exact rule from its first break on (the events before it are this step)
       const int64_t tp = __shfl_up(ts, 1, 64);
       const int64_t prev = lane == 0 ? last : tp;
-      brk = __ballot(valid && ((prev != INT64_MIN && ts < prev) || clk - ts >= Tw));
+      brk = __ballot((int)lane < nv0 && ((prev != INT64_MIN && ts < prev) || clk - ts >= Tw));
       if (!xm && brk) {
         if constexpr (!XB) {  // the exact variant re-runs this (key, segment)
           if (lane == 0) D.cm[ks] = LA_XMARK;
           return;
         }
-        to_exact();
+        const int F = __builtin_ctzll(brk);
+        if (F > 0) nv = F;
+        else to_exact();
       }
     }
+    adv = (uint32_t)nv;
+    if (j0 + nv < s_end) fetch(j0 + nv);
+    const bool valid = lane < nv;
+    const int role = valid ? st0 : -1;
     if (XB && xm) {
       // the exact rule through the event after the block's last break (or 8 events when the block
       // has none: a carried irregular state), then back to the ordered formulation when the state is
       // regular there -- its next step starts after that event -- else the block's rest exactly
       const int E = brk ? min(64 - __builtin_clzll(brk), nv - 1) : min(7, nv - 1);
       int q = 0;
+      LA_STAMP(0);
+      int qe_ = E;  // the next event after which the state is checked (then every 4 events)
 #pragma unroll 1
-      for (; q <= E && !xover; q++) xstep(q, ts, clk, g, v, role, en, qf);
-      if (!xover && q < nv) {
+      while (q < nv && !xover) {
+        for (; q <= qe_ && !xover; q++) xstep(q, ts, clk, g, v, role, en, qf);
+        if (xover || q >= nv) break;
         to_wave(lclk);
-        if (!xm) {
-          adv = (uint32_t)q;
-          fetch(j0 + adv);  // (the prefetch above read the step after this block)
-          continue;
-        }
-#pragma unroll 1
-        for (; q < nv && !xover; q++) xstep(q, ts, clk, g, v, role, en, qf);
+        if (!xm) break;
+        qe_ = min(q + 3, nv - 1);
       }
+      if (!xover && q < nv) {  // regular again before the block's end: the next step starts at q
+        LA_COUNT(12, q);
+        LA_STAMP(13);
+        adv = (uint32_t)q;
+        fetch(j0 + adv);  // (the prefetch above read the step after this block)
+        continue;
+      }
+      LA_COUNT(12, q);
+      LA_STAMP(13);
       if (xover) {
         if (lane == 0) {
           D.cm[ks] = 0;
@@ -1813,6 +1829,7 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   auto stamps_out = [&]() {
 #ifdef SHP_SW_STAMPS
     LA_COUNT(7, s_end - w_beg);
+    LA_COUNT(14, XB ? 1 : 0);
     if (lane == 0 && D.stamps)
       for (int x = 0; x < LA_NSTAMP; x++) D.stamps[(int64_t)ks * LA_NSTAMP + x] = lst[x];
 #endif

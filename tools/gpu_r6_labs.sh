@@ -12,5 +12,5 @@ for m in c4 c4d; do
   extra=""; [ $m = c4d ] && extra="--disorder 0.01"
   timeout -k 10 300 python -u bench.py --config 4 --steps 3 --warmup 1 --no-cpu-baseline --latency-batches 0 \
     --e2e-steps 0 $extra > gpurun_out/r6_bench_$m.json 2> gpurun_out/r6_bench_$m.err || { tail -5 gpurun_out/r6_bench_$m.err; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/r6_bench_$m.json'));print('$m', d['value']/1e9, 'G', d['ms_per_step'], 'ms', {k:round(v,3) for k,v in d['roofline']['kernel_ms_per_launch'].items()})"
+  python -c "import json;d=json.load(open('gpurun_out/r6_bench_$m.json'));print('$m', d['value']/1e9, 'G', d['ms_per_step'], 'ms', {k:round(v,3) for k,v in d['roofline']['kernel_ms_per_launch'].items()}, d['config'].get('engine_stats'))"
 done

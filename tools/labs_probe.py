@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--events", type=int, default=100_000_000)
     ap.add_argument("--keys", type=int, default=1_000)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--disorder", type=float, default=0.0, help="as bench.py --disorder")
     a = ap.parse_args()
     import torch
     from siddhi_amd import native, synth
@@ -38,6 +39,10 @@ def main():
         stream = torch.empty(N, dtype=torch.int32, device="cuda")
         assert L.shp_synth_fill(4, rep * N, N, K, 3, 1, ts.data_ptr(), key.data_ptr(), price.data_ptr(), None,
                                 stream.data_ptr(), None) == 0
+        if a.disorder > 0:  # (bench.py's disorder: events moved back by up to 8 s)
+            gg = torch.Generator(device="cuda").manual_seed(1000 + rep * N)
+            back = torch.rand(N, device="cuda", generator=gg) < a.disorder
+            ts -= back.to(torch.int64) * torch.randint(0, 8000, (N,), device="cuda", generator=gg)
         torch.cuda.synchronize()
         ncol = max(1, len(cq.columns))  # one pointer per program column (S1, S2, S3 price): all the price column
         colp = (ctypes.c_void_p * ncol)(*([price.data_ptr()] * ncol))
@@ -57,7 +62,7 @@ def main():
             nk = L.shp_debug_la_stamps(eng.h, buf, K * 4 * S)
             st = np.frombuffer(buf, dtype=np.uint64, count=nk * S).reshape(nk, S).astype(np.float64)
             phases = [(0, "load+filters"), (1, "partial"), (2, "doomed E_D"), (3, "leave search"), (8, "Z kills"),
-                      (9, "firings"), (4, "settle"), (5, "queue")]
+                      (9, "firings"), (4, "settle"), (5, "queue"), (13, "exact blocks"), (15, "exact firings")]
             tot = sum(st[:, x].sum() for x, _ in phases)
             blocks = st[:, 7].sum() / 64
             for x, name in phases:
@@ -65,6 +70,9 @@ def main():
             print(f"    waiting pairs/block {st[:, 6].sum() / blocks:.1f}  kill rounds/block {st[:, 10].sum() / blocks:.2f}"
                   f"  Z/block {st[:, 11].sum() / blocks:.1f}  events/key {st[:, 7].mean():.0f}"
                   f"  cycles/block {tot / blocks:.0f}")
+            print(f"    exact variant: {int(st[:, 14].sum())} of {nk} slots; events by the exact rule "
+                  f"{st[:, 12].sum() / st[:, 7].sum():.3f} of all, {(st[:, 13].sum() + st[:, 15].sum()) / max(1, st[:, 12].sum()):.0f} cycles each "
+                  f"({st[:, 15].sum() / max(1, st[:, 12].sum()):.0f} in the timer firings)")
 
 if __name__ == "__main__":
     main()
