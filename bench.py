@@ -543,6 +543,7 @@ def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout,
         key = torch.empty(N, dtype=torch.int32, pin_memory=True)
         price = torch.empty(N, dtype=torch.float32, pin_memory=True)
         ts32 = torch.empty(N, dtype=torch.int32, pin_memory=True)
+        key16 = torch.empty(N, dtype=torch.int16, pin_memory=True) if K <= 65536 else None
         dts = torch.empty(N, dtype=torch.int64, device="cuda")
         dkey = torch.empty(N, dtype=torch.int32, device="cuda")
         dpr = torch.empty(N, dtype=torch.float32, device="cuda")
@@ -560,30 +561,35 @@ def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout,
         key.copy_(dkey)
         price.copy_(dpr)
         ts32.copy_(d32)
-        host.append((ts, key, price, ts32, base))
+        if key16 is not None:
+            key16.copy_(dkey.to(torch.int16))  # (the ids as 16 bits: uint16 on the C side)
+        host.append((ts, key, price, ts32, base, key16))
         del dts, dkey, dpr, d32
     torch.cuda.synchronize()
 
     def batch(s, j):
-        ts, key, price, ts32, base = host[s]
+        ts, key, price, ts32, base, key16 = host[s]
         lo, hi = j * nb, min(N, (j + 1) * nb)
         colp = (ctypes.c_void_p * 1)(price.data_ptr() + lo * 4)
         b = native.ShpBatch(hi - lo, ts.data_ptr() + lo * 8, key.data_ptr() + lo * 4, None,
                             ctypes.cast(colp, ctypes.c_void_p), None)
-        return b, colp, ts32.data_ptr() + lo * 4, int(base[j])
+        return b, colp, ts32.data_ptr() + lo * 4, int(base[j]), (key16.data_ptr() + lo * 2 if key16 is not None else None)
 
     def check(rc, e):
         if rc != 0:
             raise native.ShpError(rc, L.shp_last_error(e.h).decode())
 
     res = {}
-    for mode in ("serial", "pipelined", "pipelined_ts32"):
+    modes = ("serial", "pipelined", "pipelined_ts32") + (("pipelined_narrow",) if K <= 65536 else ())
+    for mode in modes:
         e = native.HipEngine(cq.program_json(), 0, max_keys=K, max_batch=nb, max_matches=int(nb * 1.1) + 4096,
                              device=device, force_general=force, match_layout=native.LAYOUT_COMPACT)
         try:
             def stage(s, j):
-                b, colp, p32, b0 = batch(s, j)
-                if mode == "pipelined_ts32":
+                b, colp, p32, b0, p16 = batch(s, j)
+                if mode == "pipelined_narrow":
+                    check(L.shp_stage_batch_narrow(e.h, ctypes.byref(b), b0, p32, p16), e)
+                elif mode == "pipelined_ts32":
                     check(L.shp_stage_batch_ts32(e.h, ctypes.byref(b), b0, p32), e)
                 else:
                     check(L.shp_stage_batch(e.h, ctypes.byref(b)), e)
@@ -593,7 +599,7 @@ def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout,
                 mt = native.ShpMatches()
                 if mode == "serial":
                     for j in range(nsub):
-                        b, colp, _, _ = batch(s, j)
+                        b, colp, _, _, _ = batch(s, j)
                         check(L.shp_push_batch_compact(e.h, ctypes.byref(b), ctypes.byref(mt)), e)
                         m += mt.m
                     return m
@@ -614,7 +620,7 @@ def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout,
             for s in range(1, total_steps):
                 m += one_step(s)
             el = time.perf_counter() - t0
-            inb = 12 if mode == "pipelined_ts32" else 16
+            inb = {"pipelined_ts32": 12, "pipelined_narrow": 10}.get(mode, 16)
             ev = N * steps
             res[mode] = {"value": ev / el, "ms_per_step": el / steps * 1e3, "matches_per_s": m / el,
                          "h2d_bytes_per_event": inb, "d2h_bytes_per_match": per,
@@ -632,12 +638,13 @@ def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout,
     torch.cuda.synchronize()
     h2d = 4 * (1 << 30) / (time.perf_counter() - t0) / 1e9
     del hb, db, host
-    best = max(("pipelined", "pipelined_ts32"), key=lambda k: res[k]["value"])
+    best = max([m for m in modes if m != "serial"], key=lambda k: res[k]["value"])
     return {"value": res[best]["value"], "unit": "events/s", "ms_per_step": res[best]["ms_per_step"],
             "mode": best, "batch_events": nb, "batches_per_step": nsub, "steps": steps, "forms": res,
             "h2d_copy_gbs": h2d,
-            "what": "page-locked host SoA columns -> shp_stage_batch[_ts32] / shp_run_staged -> compact records in "
-                    "page-locked host memory; serial = shp_push_batch_compact per batch"}
+            "what": "page-locked host SoA columns -> shp_stage_batch[_ts32|_narrow] / shp_run_staged -> compact records "
+                    "in page-locked host memory; serial = shp_push_batch_compact per batch; ts32 = 4-byte ts offsets "
+                    "(12 B/event), narrow = also 2-byte key ids (10 B/event)"}
 
 
 def _lib_sha16(path):

@@ -199,6 +199,10 @@ int shp_push_batch_compact(shp_engine* e, const shp_batch* in, shp_matches* out)
  * instead of 16 bytes per event for a float column -- the host keeps a batch's ts span below 2^31 ms. */
 int shp_stage_batch(shp_engine* e, const shp_batch* in);
 int shp_stage_batch_ts32(shp_engine* e, const shp_batch* in, int64_t ts_base, const int32_t* ts_delta);
+/* The narrowest form: ts offsets as above and, with key16 != NULL, 2-byte partition key ids (in->key is
+ * ignored; needs max_keys <= 65536, else SHP_ERR_ARG): 10 bytes per event for one float column. */
+int shp_stage_batch_narrow(shp_engine* e, const shp_batch* in, int64_t ts_base, const int32_t* ts_delta,
+                           const uint16_t* key16);
 int shp_run_staged(shp_engine* e, shp_matches* out);
 /* The oldest event sequence number the engine's committed state still names: an event of any open
  * partial (pending / new-and-every lists, count chains, logical slots, pairs waiting on an absent

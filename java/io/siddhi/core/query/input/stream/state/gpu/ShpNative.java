@@ -86,6 +86,8 @@ final class ShpNative {
     static final MethodHandle STAGE_BATCH = fn("shp_stage_batch", JAVA_INT, ADDRESS, ADDRESS);
     static final MethodHandle STAGE_BATCH_TS32 = fn("shp_stage_batch_ts32", JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG,
             ADDRESS);
+    static final MethodHandle STAGE_BATCH_NARROW = fn("shp_stage_batch_narrow", JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG,
+            ADDRESS, ADDRESS);
     static final MethodHandle RUN_STAGED = fn("shp_run_staged", JAVA_INT, ADDRESS, ADDRESS);
     // the earliest head of any key's timer queue: a live-mode runtime's wall-clock wake-up (Scheduler.schedule)
     static final MethodHandle NEXT_DUE = fn("shp_engine_next_due", JAVA_INT, ADDRESS, ADDRESS);

@@ -148,6 +148,12 @@ __global__ void k_widen_ts(const int32_t* __restrict__ d, int64_t base, int64_t*
   for (; i < n; i += (int64_t)gridDim.x * blockDim.x) ts[i] = base + d[i];
 }
 
+// shp_stage_batch_narrow: 2-byte key ids (max_keys <= 65536) widened in HBM
+__global__ void k_widen_key(const uint16_t* __restrict__ d, int32_t* __restrict__ key, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) key[i] = (int32_t)d[i];
+}
+
 // Capacity growth: the committed arena of layout Ys (tier t) into layout Yd (tier >= t), every
 // lane.  Fields keep their order and element sizes across tiers; element indices that embed a
 // capacity are re-indexed: list items ((which * MAXP + p) * LCAP + i) and the timer rings
@@ -294,8 +300,9 @@ struct shp_engine {
     int64_t n = 0;
     int64_t* ts = nullptr;
     int32_t* ts32 = nullptr;  // shp_stage_batch_ts32: ts = ts_base + ts32[i], widened on the device
+    uint16_t* k16 = nullptr;  // shp_stage_batch_narrow: 2-byte key ids, widened on the device
     int64_t ts_base = 0;
-    bool narrow = false;
+    bool narrow = false, nkey = false;
     int32_t* key = nullptr;
     int32_t* strm = nullptr;
     int64_t *clk = nullptr, *sq = nullptr;
@@ -359,6 +366,7 @@ struct shp_engine {
     for (Slot& sl : slots) {
       F(sl.ts);
       F(sl.ts32);
+      F(sl.k16);
       F(sl.key);
       F(sl.strm);
       F(sl.clk);
@@ -1441,6 +1449,7 @@ struct shp_engine {
     for (Slot& sl : slots) {
       alloc(sl.ts, cap);
       alloc(sl.ts32, cap);
+      alloc(sl.k16, cap);
       alloc(sl.key, cap);
       alloc(sl.strm, cap);
       alloc(sl.clk, cap);
@@ -1457,11 +1466,12 @@ struct shp_engine {
   }
 
   // H2D of one host batch into the next free slot on the copy stream; returns once enqueued
-  int stage_slot(const shp_batch* in, const int32_t* ts32, int64_t ts_base) {
+  int stage_slot(const shp_batch* in, const int32_t* ts32, int64_t ts_base, const uint16_t* key16 = nullptr) {
     const DevProg& P = comp.P;
     if (in->n > cfg.max_batch) return fail(SHP_ERR_ARG, "batch larger than max_batch");
     if (in->n > 0 && !ts32 && !in->ts) return fail(SHP_ERR_ARG, "no ts column");
-    if (P.partitioned && in->n > 0 && !in->key) return fail(SHP_ERR_ARG, "no key column");
+    if (P.partitioned && in->n > 0 && !in->key && !key16) return fail(SHP_ERR_ARG, "no key column");
+    if (key16 && cfg.max_keys > 65536) return fail(SHP_ERR_ARG, "2-byte key ids need max_keys <= 65536");
     if (slot_count == 2) return fail(SHP_ERR_CAPACITY, "two batches staged: run one first (shp_run_staged)");
     slots_alloc();
     Slot& sl = slots[(slot_head + slot_count) % 2];
@@ -1470,11 +1480,13 @@ struct shp_engine {
     HIP_OK(hipStreamWaitEvent(cstream, sl.consumed, 0));  // the run that read this slot is done
     sl.n = n;
     sl.narrow = ts32 != nullptr;
+    sl.nkey = P.partitioned && key16 != nullptr;
     sl.ts_base = ts_base;
     if (n > 0) {
       if (ts32) HIP_OK(hipMemcpyAsync(sl.ts32, ts32, n * 4, k, cstream));
       else HIP_OK(hipMemcpyAsync(sl.ts, in->ts, n * 8, k, cstream));
-      if (P.partitioned) HIP_OK(hipMemcpyAsync(sl.key, in->key, n * 4, k, cstream));
+      if (sl.nkey) HIP_OK(hipMemcpyAsync(sl.k16, key16, n * 2, k, cstream));
+      else if (P.partitioned) HIP_OK(hipMemcpyAsync(sl.key, in->key, n * 4, k, cstream));
       sl.has_stream = in->stream != nullptr;
       if (sl.has_stream) HIP_OK(hipMemcpyAsync(sl.strm, in->stream, n * 4, k, cstream));
       sl.has_clk = in->clock != nullptr;
@@ -1504,6 +1516,10 @@ struct shp_engine {
     if (sl.narrow && n > 0) {
       const int gb = (int)std::min<int64_t>((n + 255) / 256, 8192);
       k_widen_ts<<<gb, 256, 0, stream>>>(sl.ts32, sl.ts_base, sl.ts, n);
+    }
+    if (sl.nkey && n > 0) {
+      const int gb = (int)std::min<int64_t>((n + 255) / 256, 8192);
+      k_widen_key<<<gb, 256, 0, stream>>>(sl.k16, sl.key, n);
     }
     const void* cp[MAXCOL];
     const uint8_t* np[MAXCOL];
@@ -1844,6 +1860,12 @@ int shp_stage_batch(shp_engine* e, const shp_batch* in) {
 int shp_stage_batch_ts32(shp_engine* e, const shp_batch* in, int64_t ts_base, const int32_t* ts_delta) {
   if (!e || !in || (in->n > 0 && !ts_delta)) return SHP_ERR_ARG;
   return guarded(e, [&]() { return e->stage_slot(in, ts_delta, ts_base); });
+}
+
+int shp_stage_batch_narrow(shp_engine* e, const shp_batch* in, int64_t ts_base, const int32_t* ts_delta,
+                           const uint16_t* key16) {
+  if (!e || !in || (in->n > 0 && !ts_delta)) return SHP_ERR_ARG;
+  return guarded(e, [&]() { return e->stage_slot(in, ts_delta, ts_base, key16); });
 }
 
 int shp_run_staged(shp_engine* e, shp_matches* out) {

@@ -23,7 +23,7 @@ SHP_ERRORS = {-1: "SHP_ERR_ARG", -2: "SHP_ERR_UNSUPPORTED", -3: "SHP_ERR_CAPACIT
               -4: "SHP_ERR_OUTPUT", -5: "SHP_ERR_DEVICE", -6: "SHP_ERR_KEYS"}
 
 SYMBOLS = ["shp_engine_create", "shp_push_batch", "shp_push_batch_device", "shp_fetch_matches", "shp_push_batch_compact", "shp_engine_oldest_live_seq",
-           "shp_engine_next_due", "shp_stage_batch", "shp_stage_batch_ts32", "shp_run_staged",
+           "shp_engine_next_due", "shp_stage_batch", "shp_stage_batch_ts32", "shp_stage_batch_narrow", "shp_run_staged",
            "shp_advance_clock", "shp_engine_num_states", "shp_engine_state_stream", "shp_engine_path", "shp_last_kernel_ms", "shp_engine_stat",
            "shp_last_error", "shp_engine_destroy", "shp_synth_fill", "shp_dev_alloc", "shp_dev_free",
            "shp_dev_to_host", "shp_host_alloc", "shp_host_free", "shp_host_register",
@@ -84,6 +84,8 @@ def lib():
         L.shp_engine_oldest_live_seq.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
         L.shp_stage_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpBatch)]
         L.shp_stage_batch_ts32.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpBatch), ctypes.c_int64, ctypes.c_void_p]
+        L.shp_stage_batch_narrow.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpBatch), ctypes.c_int64, ctypes.c_void_p,
+                                             ctypes.c_void_p]
         L.shp_run_staged.argtypes = [ctypes.c_void_p, ctypes.POINTER(ShpMatches)]
         L.shp_engine_next_due.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
         L.shp_advance_clock.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ShpMatches)]
@@ -348,16 +350,17 @@ class HipEngine:
         out["m"] = int(mt.m)
         return out
 
-    def stage(self, ts, key, stream, cols, nulls, clock=None, seq=None, ts32=None, ts_base=0):
-        """shp_stage_batch (or, with ts32 = int32 offsets from ts_base, shp_stage_batch_ts32): the H2D
-        copies of one host batch, enqueued on the engine's copy stream.  The arrays are held until the
-        shp_run_staged that consumes them (page-locked arrays make the copies asynchronous)."""
+    def stage(self, ts, key, stream, cols, nulls, clock=None, seq=None, ts32=None, ts_base=0, key16=None):
+        """shp_stage_batch (or, with ts32 = int32 offsets from ts_base, shp_stage_batch_ts32; with key16 =
+        uint16 key ids too, shp_stage_batch_narrow): the H2D copies of one host batch, enqueued on the
+        engine's copy stream.  The arrays are held until the shp_run_staged that consumes them
+        (page-locked arrays make the copies asynchronous)."""
         L = lib()
         n = len(ts) if ts32 is None else len(ts32)
         if n > self.max_batch:
             raise ValueError("stage: batch larger than max_batch")
-        keep = [np.ascontiguousarray(x) if x is not None else None for x in (ts, key, stream, clock, seq, ts32)]
-        t, k, s_, ck, sq, t32 = keep
+        keep = [np.ascontiguousarray(x) if x is not None else None for x in (ts, key, stream, clock, seq, ts32, key16)]
+        t, k, s_, ck, sq, t32, k16 = keep
         cs = [np.ascontiguousarray(c) for c in cols]
         ns = [None if m is None else np.ascontiguousarray(m, np.uint8) for m in nulls]
         _check_columns(cs, ns, self.col_bytes, n)
@@ -366,7 +369,9 @@ class HipEngine:
         ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
         b = ShpBatch(n, ptr(t), ptr(k), ptr(s_), ctypes.cast(colp, ctypes.c_void_p), ctypes.cast(nulp, ctypes.c_void_p),
                      ptr(ck), ptr(sq))
-        if t32 is None:
+        if k16 is not None:
+            self._check(L.shp_stage_batch_narrow(self.h, ctypes.byref(b), int(ts_base), ptr(t32), ptr(k16)))
+        elif t32 is None:
             self._check(L.shp_stage_batch(self.h, ctypes.byref(b)))
         else:
             self._check(L.shp_stage_batch_ts32(self.h, ctypes.byref(b), int(ts_base), ptr(t32)))

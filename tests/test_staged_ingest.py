@@ -46,8 +46,9 @@ def _same(a, b):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg,keys,n,step,layout,narrow", [
     (2, 10_000, 2_000_000, 300_007, 5, False), (2, 10_000, 2_000_000, 300_007, 5, True),
-    ("3b", 50_000, 1_500_000, 250_003, 5, True), (5, 100_000, 1_000_000, 200_003, 5, False),
-    (4, 1_000, 600_000, 100_003, 5, True)])
+    (2, 10_000, 2_000_000, 300_007, 5, "key16"), ("3b", 50_000, 1_500_000, 250_003, 5, True),
+    ("3b", 50_000, 1_500_000, 250_003, 5, "key16"), (5, 100_000, 1_000_000, 200_003, 5, False),
+    (4, 1_000, 600_000, 100_003, 5, True), (4, 1_000, 600_000, 100_003, 5, "key16")])
 def test_staged_pipeline_equals_compact_push(cfg, keys, n, step, layout, narrow):
     g = small_stream(cfg if cfg != "3b" else 3, n, keys)
     cq, a = _engine(cfg, keys, step, layout)
@@ -64,7 +65,8 @@ def test_staged_pipeline_equals_compact_push(cfg, keys, n, step, layout, narrow)
         args = (g["ts"][lo:hi], g["key"][lo:hi], g["stream"][lo:hi], [c[lo:hi] for c in cols], [None] * len(cols))
         if narrow:
             base = int(g["ts"][lo])
-            b.stage(None, *args[1:], ts32=(g["ts"][lo:hi] - base).astype(np.int32), ts_base=base)
+            k16 = g["key"][lo:hi].astype(np.uint16) if narrow == "key16" else None
+            b.stage(None, *args[1:], ts32=(g["ts"][lo:hi] - base).astype(np.int32), ts_base=base, key16=k16)
         else:
             b.stage(*args)
     got = []
@@ -99,3 +101,15 @@ def test_staged_capacity_and_empty_run_errors():
     for lo, r in ((0, r0), (10_000, r1)):
         _same(r, ref.push_compact(g["ts"][lo:lo + 10_000], g["key"][lo:lo + 10_000], g["stream"][lo:lo + 10_000],
                                   [c[lo:lo + 10_000] for c in cols], [None]))
+
+
+@pytest.mark.gpu
+def test_staged_narrow_keys_need_max_keys_16_bits():
+    from siddhi_amd.native import ShpError
+    g = small_stream(2, 1_000, 100_000)
+    cq, e = _engine(2, 100_000, 1_000, 5)
+    cols = columns_for(cq, g)
+    with pytest.raises(ShpError) as ei:
+        e.stage(None, g["key"], g["stream"], cols, [None], ts32=(g["ts"] - g["ts"][0]).astype(np.int32),
+                ts_base=int(g["ts"][0]), key16=g["key"].astype(np.uint16))
+    assert ei.value.code == -1  # SHP_ERR_ARG: 100k keys do not fit 2 bytes
