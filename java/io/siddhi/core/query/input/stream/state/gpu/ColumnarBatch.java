@@ -14,7 +14,13 @@
  * committed state holds): trim() drops everything below it, maybeTrim() asks the engine once the
  * kept rows have doubled since the last trim, so the query (a state snapshot) stays amortised.
  * The Python mirror of these rules is siddhi_amd/history.py (RowHistory), tested in
- * tests/test_retention.py.  Source only: no JDK in this repository's image (DESIGN.md §6).
+ * tests/test_retention.py.
+ *
+ * Pipelined ingest (FlushPolicy.PIPELINED): two column sets; a flush stages the filled set
+ * (shp_stage_batch: its H2D copies on the engine's copy stream, from page-locked segments) and
+ * runs the set staged before it (shp_run_staged), whose rows then join the history -- sequence
+ * numbers follow run order, which is stage order.  The mirror is SiddhiAppRuntime(pipelined=True)
+ * (siddhi_amd/runtime.py), tested in tests/test_flow_clock.py.  Source only: no JDK in this repository's image (DESIGN.md §6).
  */
 package io.siddhi.core.query.input.stream.state.gpu;
 
@@ -22,6 +28,7 @@ import io.siddhi.core.event.stream.StreamEvent;
 
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
+import java.util.ArrayDeque;
 import java.util.ArrayList;
 import java.util.Arrays;
 import java.util.List;
@@ -70,15 +77,58 @@ final class ColumnarBatch {
         }
     }
 
+    /** One set of host columns in shp_batch's layout with the rows appended into it.  A DEFERRED /
+     * SYNC batch has one; a PIPELINED batch two, so one set is being filled (or decoded) while the
+     * other's H2D copies (shp_stage_batch, on the engine's copy stream) are in flight. */
+    private final class Columns {
+        final MemorySegment ts, key, stream;
+        final MemorySegment[] cols, nulls;
+        final MemorySegment colPtrs, nullPtrs, descriptor;
+        final List<Object[]> rows = new ArrayList<>();
+        final List<Long> rowTs = new ArrayList<>();
+        long n;
+
+        Columns() {
+            ts = arena.allocate(JAVA_LONG, capacity);
+            key = arena.allocate(JAVA_INT, capacity);
+            stream = arena.allocate(JAVA_INT, capacity);
+            cols = new MemorySegment[columns.length];
+            nulls = new MemorySegment[columns.length];
+            colPtrs = arena.allocate(ADDRESS, Math.max(1, columns.length));
+            nullPtrs = arena.allocate(ADDRESS, Math.max(1, columns.length));
+            for (int c = 0; c < columns.length; c++) {
+                cols[c] = arena.allocate(columns[c].bytes() * capacity, 8);
+                nulls[c] = arena.allocate(JAVA_BYTE, capacity);
+                colPtrs.setAtIndex(ADDRESS, c, cols[c]);
+                nullPtrs.setAtIndex(ADDRESS, c, nulls[c]);
+            }
+            descriptor = arena.allocate(ShpNative.BATCH);
+        }
+
+        List<MemorySegment> segments() {
+            List<MemorySegment> l = new ArrayList<>(List.of(ts, key, stream));
+            l.addAll(Arrays.asList(cols));
+            l.addAll(Arrays.asList(nulls));
+            return l;
+        }
+
+        void clear() {
+            n = 0;
+            rows.clear();
+            rowTs.clear();
+        }
+    }
+
     private final Arena arena;
     private final long capacity;
     private final Column[] columns;
-    private final MemorySegment ts, key, stream;
-    private final MemorySegment[] cols, nulls;
-    private final MemorySegment colPtrs, nullPtrs, descriptor;
     private final NativeDictionary strings;           // string-attribute dictionary (shared with the filters)
-    private long n;
-    private long seq0;                                // sequence number of row 0 of the open batch
+    private Columns open;                             // the set appends go to (null only inside a flush)
+    private Columns decoded;                          // the set of the last committed push (keyAt / tsAt / streamAt)
+    private final ArrayDeque<Columns> staged = new ArrayDeque<>();  // PIPELINED: staged, oldest first
+    private final ArrayDeque<Columns> free = new ArrayDeque<>();
+    private final List<MemorySegment> pinned = new ArrayList<>();
+    private long seq0;                                // sequence number of the oldest row not yet committed
     // rows of committed pushes still named by open partials (or not yet trimmed), oldest first:
     // blocks [head, size) of the list, ordered by seq0, so a match slot's row is found by bisection
     private final ArrayList<Block> history = new ArrayList<>();
@@ -87,38 +137,55 @@ final class ColumnarBatch {
     private long floor;                               // every row below it was dropped
     private final long minTrim;
     private long trimAt;
-    private final List<Object[]> rows = new ArrayList<>();
-    private final List<Long> rowTs = new ArrayList<>();
 
-    ColumnarBatch(Arena arena, long capacity, Column[] columns, NativeDictionary strings, long minTrim) {
+    /** @param sets 1 (SYNC / DEFERRED) or 2 (PIPELINED: the second set fills while the first is staged) */
+    ColumnarBatch(Arena arena, long capacity, Column[] columns, NativeDictionary strings, long minTrim, int sets) {
         this.arena = arena;
         this.capacity = capacity;
         this.columns = columns;
         this.strings = strings;
         this.minTrim = Math.max(1, minTrim);
         this.trimAt = this.minTrim;
-        ts = arena.allocate(JAVA_LONG, capacity);
-        key = arena.allocate(JAVA_INT, capacity);
-        stream = arena.allocate(JAVA_INT, capacity);
-        cols = new MemorySegment[columns.length];
-        nulls = new MemorySegment[columns.length];
-        colPtrs = arena.allocate(ADDRESS, Math.max(1, columns.length));
-        nullPtrs = arena.allocate(ADDRESS, Math.max(1, columns.length));
-        for (int c = 0; c < columns.length; c++) {
-            cols[c] = arena.allocate(columns[c].bytes() * capacity, 8);
-            nulls[c] = arena.allocate(JAVA_BYTE, capacity);
-            colPtrs.setAtIndex(ADDRESS, c, cols[c]);
-            nullPtrs.setAtIndex(ADDRESS, c, nulls[c]);
+        open = new Columns();
+        decoded = open;
+        for (int i = 1; i < sets; i++) {
+            free.add(new Columns());
         }
-        descriptor = arena.allocate(ShpNative.BATCH);
+    }
+
+    ColumnarBatch(Arena arena, long capacity, Column[] columns, NativeDictionary strings, long minTrim) {
+        this(arena, capacity, columns, strings, minTrim, 1);
+    }
+
+    /** Page-locks every column segment (shp_host_register) so shp_stage_batch's copies run at DMA rate
+     * and asynchronously; undone by unpin() before the arena closes. */
+    void pin() throws Throwable {
+        List<Columns> all = new ArrayList<>(free);
+        all.add(open);
+        for (Columns c : all) {
+            for (MemorySegment m : c.segments()) {
+                int rc = (int) ShpNative.HOST_REGISTER.invokeExact(m, m.byteSize());
+                if (rc != ShpNative.OK) {
+                    throw new IllegalStateException("shp_host_register: " + ShpNative.codeName(rc));
+                }
+                pinned.add(m);
+            }
+        }
+    }
+
+    void unpin() throws Throwable {
+        for (MemorySegment m : pinned) {
+            int rc = (int) ShpNative.HOST_UNREGISTER.invokeExact(m);   // best effort at close
+        }
+        pinned.clear();
     }
 
     boolean full() {
-        return n >= capacity;
+        return open.n >= capacity;
     }
 
     long size() {
-        return n;
+        return open.n;
     }
 
     /** Appends one event (InputHandler.send -> Receiver.receive).  keyId: the partition-key
@@ -126,36 +193,40 @@ final class ColumnarBatch {
      * the query is not partitioned; streamIndex: -1 for a clock-only event (a send on a stream this
      * query does not read, which in playback still sets the app's clock). */
     void append(long timestamp, int keyId, int streamIndex, Object[] data) {
-        if (streamIndex >= 0 && n > 0 && streamAt(n - 1) < 0 && rowTs.get((int) n - 1) == timestamp) {
+        Columns o = open;
+        long n = o.n;
+        if (streamIndex >= 0 && n > 0 && o.stream.getAtIndex(JAVA_INT, n - 1) < 0
+                && o.rowTs.get((int) n - 1) == timestamp) {
             // the clock-only row the query's TimeChangeListener appended for this very send
             // (InputHandler.send sets the clock before the event reaches the receiver): the event
             // carries the same clock, so it takes the row's place
             n--;
-            rows.remove(rows.size() - 1);
-            rowTs.remove(rowTs.size() - 1);
+            o.rows.remove(o.rows.size() - 1);
+            o.rowTs.remove(o.rowTs.size() - 1);
         }
-        ts.setAtIndex(JAVA_LONG, n, timestamp);
-        key.setAtIndex(JAVA_INT, n, keyId);
-        stream.setAtIndex(JAVA_INT, n, streamIndex);
+        o.ts.setAtIndex(JAVA_LONG, n, timestamp);
+        o.key.setAtIndex(JAVA_INT, n, keyId);
+        o.stream.setAtIndex(JAVA_INT, n, streamIndex);
         for (int c = 0; c < columns.length; c++) {
             Column col = columns[c];
             Object v = (streamIndex == col.stream && data != null) ? data[col.attr] : null;
-            nulls[c].set(JAVA_BYTE, n, (byte) (v == null ? 1 : 0));
+            o.nulls[c].set(JAVA_BYTE, n, (byte) (v == null ? 1 : 0));
             if (v == null) {
                 continue;
             }
+            MemorySegment d = o.cols[c];
             switch (col.type) {
-                case 'i': cols[c].setAtIndex(JAVA_INT, n, ((Number) v).intValue()); break;
-                case 'l': cols[c].setAtIndex(JAVA_LONG, n, ((Number) v).longValue()); break;
-                case 'f': cols[c].setAtIndex(JAVA_FLOAT, n, ((Number) v).floatValue()); break;
-                case 'd': cols[c].setAtIndex(JAVA_DOUBLE, n, ((Number) v).doubleValue()); break;
-                case 'b': cols[c].set(JAVA_BYTE, n, (byte) (((Boolean) v) ? 1 : 0)); break;
-                default: cols[c].setAtIndex(JAVA_INT, n, strings.id(v.toString())); break;
+                case 'i': d.setAtIndex(JAVA_INT, n, ((Number) v).intValue()); break;
+                case 'l': d.setAtIndex(JAVA_LONG, n, ((Number) v).longValue()); break;
+                case 'f': d.setAtIndex(JAVA_FLOAT, n, ((Number) v).floatValue()); break;
+                case 'd': d.setAtIndex(JAVA_DOUBLE, n, ((Number) v).doubleValue()); break;
+                case 'b': d.set(JAVA_BYTE, n, (byte) (((Boolean) v) ? 1 : 0)); break;
+                default: d.setAtIndex(JAVA_INT, n, strings.id(v.toString())); break;
             }
         }
-        rows.add(data);
-        rowTs.add(timestamp);
-        n++;
+        o.rows.add(data);
+        o.rowTs.add(timestamp);
+        o.n = n + 1;
     }
 
     /** A clock-only row (stream -1, no key, no values): the app clock moved to `now` with no event of
@@ -165,25 +236,25 @@ final class ColumnarBatch {
         append(now, 0, -1, null);
     }
 
-    /** The shp_batch descriptor of the rows appended so far (host memory; shp_push_batch copies it). */
+    /** The shp_batch descriptor of the rows appended so far (host memory; shp_push_batch copies it,
+     * shp_stage_batch reads it until the shp_run_staged that consumes it). */
     MemorySegment descriptor() {
-        descriptor.set(JAVA_LONG, 0, n);
-        descriptor.set(ADDRESS, 8, ts);
-        descriptor.set(ADDRESS, 16, key);
-        descriptor.set(ADDRESS, 24, stream);
-        descriptor.set(ADDRESS, 32, colPtrs);
-        descriptor.set(ADDRESS, 40, nullPtrs);
-        descriptor.set(ADDRESS, 48, MemorySegment.NULL);  // clock: the events' own ts
-        descriptor.set(ADDRESS, 56, MemorySegment.NULL);  // seq: the engine's running count
-        return descriptor;
+        Columns o = open;
+        o.descriptor.set(JAVA_LONG, 0, o.n);
+        o.descriptor.set(ADDRESS, 8, o.ts);
+        o.descriptor.set(ADDRESS, 16, o.key);
+        o.descriptor.set(ADDRESS, 24, o.stream);
+        o.descriptor.set(ADDRESS, 32, o.colPtrs);
+        o.descriptor.set(ADDRESS, 40, o.nullPtrs);
+        o.descriptor.set(ADDRESS, 48, MemorySegment.NULL);  // clock: the events' own ts
+        o.descriptor.set(ADDRESS, 56, MemorySegment.NULL);  // seq: the engine's running count
+        return o.descriptor;
     }
 
-    /** After a failed push: the engine did not take the rows (its sequence counter did not move),
-     * so they are dropped and row 0 of the next batch keeps this batch's seq0. */
+    /** After a failed push or stage: the engine did not take the rows (its sequence counter did not
+     * move), so they are dropped and row 0 of the next batch keeps this batch's seq0. */
     void discard() {
-        n = 0;
-        rows.clear();
-        rowTs.clear();
+        open.clear();
     }
 
     /** After a successful push: the rows join the history (matches of this and later pushes name
@@ -191,32 +262,82 @@ final class ColumnarBatch {
      * (keyAt, tsAt, streamAt) until the next append: the compact records are decoded from them.
      * Returns the pushed rows' first sequence number. */
     long commit() {
-        long first = seq0;
-        if (n > 0) {
-            long[] t = new long[rowTs.size()];
-            for (int i = 0; i < t.length; i++) {
-                t[i] = rowTs.get(i);
-            }
-            history.add(new Block(seq0, rows.toArray(new Object[0][]), t));
-            kept += n;
-        }
-        seq0 += n;
-        n = 0;
-        rows.clear();
-        rowTs.clear();
+        decoded = open;
+        long first = commitRows(open);
+        open.clear();
         return first;
     }
 
+    private long commitRows(Columns c) {
+        long first = seq0;
+        if (c.n > 0) {
+            long[] t = new long[c.rowTs.size()];
+            for (int i = 0; i < t.length; i++) {
+                t[i] = c.rowTs.get(i);
+            }
+            history.add(new Block(seq0, c.rows.toArray(new Object[0][]), t));
+            kept += c.n;
+        }
+        seq0 += c.n;
+        return first;
+    }
+
+    // ---- PIPELINED (shp_stage_batch / shp_run_staged): descriptor() + shp_stage_batch, then markStaged();
+    // at the run, commitStaged() (or dropStaged() when the run failed)
+
+    /** The open set's H2D is enqueued: it waits for its run, appends go to the other set (none is
+     * free while two batches are staged: the caller runs the older one before the next append). */
+    void markStaged() {
+        staged.addLast(open);
+        open = free.pollFirst();
+    }
+
+    int stagedCount() {
+        return staged.size();
+    }
+
+    /** Rows of the oldest staged batch (the one shp_run_staged runs next). */
+    long stagedSize() {
+        return staged.isEmpty() ? 0 : staged.peekFirst().n;
+    }
+
+    /** The oldest staged batch ran: its rows join the history and its columns are the decoded ones
+     * until the next append; the set is then free for appends.  Returns its first sequence number. */
+    long commitStaged() {
+        Columns c = staged.pollFirst();
+        long first = commitRows(c);
+        decoded = c;
+        recycle(c);
+        return first;
+    }
+
+    /** The oldest staged batch's run failed: the engine left its counter as before, so its rows are
+     * dropped and the next staged batch takes its sequence numbers. */
+    void dropStaged() {
+        recycle(staged.pollFirst());
+    }
+
+    private void recycle(Columns c) {
+        // its key / ts / stream columns stay readable through `decoded` until the next append (no
+        // append runs while a flush decodes: both hold the runtime's lock)
+        c.clear();
+        if (open == null) {
+            open = c;
+        } else {
+            free.addLast(c);
+        }
+    }
+
     int keyAt(long i) {
-        return key.getAtIndex(JAVA_INT, i);
+        return decoded.key.getAtIndex(JAVA_INT, i);
     }
 
     long tsAt(long i) {
-        return ts.getAtIndex(JAVA_LONG, i);
+        return decoded.ts.getAtIndex(JAVA_LONG, i);
     }
 
     int streamAt(long i) {
-        return stream.getAtIndex(JAVA_INT, i);
+        return decoded.stream.getAtIndex(JAVA_INT, i);
     }
 
     /** Once the kept rows reach minTrim and have doubled since the last trim: ask the engine for its
@@ -286,6 +407,10 @@ final class ColumnarBatch {
     }
 
     long nextSeq() {
+        long n = open == null ? 0 : open.n;
+        for (Columns c : staged) {
+            n += c.n;
+        }
         return seq0 + n;
     }
 
@@ -331,6 +456,9 @@ final class ColumnarBatch {
             history.add(new Block(seqs[i], Arrays.copyOfRange(data, i, j), Arrays.copyOfRange(tss, i, j)));
             kept += j - i;
             i = j;
+        }
+        if (!staged.isEmpty()) {
+            throw new IllegalStateException("restore with staged batches: run them first");
         }
         discard();
         seq0 = nextSeq;

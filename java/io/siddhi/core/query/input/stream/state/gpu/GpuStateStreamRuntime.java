@@ -106,8 +106,13 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
      *   point that observes state (advanceClock, snapshot, shutdown); callbacks then fire on the
      *   flusher (or the filling sender's) thread, as with an @async junction
      *   (core/stream/StreamJunction.java:101-131).  Synchronous single-event senders then share one
-     *   push instead of paying a full push (sort, kernels, status read) per event. */
-    public enum FlushPolicy { SYNC, DEFERRED }
+     *   push instead of paying a full push (sort, kernels, status read) per event.
+     * PIPELINED: DEFERRED's flush points, with each flush staging its batch (shp_stage_batch: the H2D
+     *   copies from page-locked columns on the engine's copy stream) and running the batch staged
+     *   before it (shp_run_staged), so batch i+1's copies overlap batch i's kernels (bench.py
+     *   end_to_end "pipelined").  A batch's callbacks fire one flush later; a flush with nothing new
+     *   runs what is staged, and every point that observes state drains both first. */
+    public enum FlushPolicy { SYNC, DEFERRED, PIPELINED }
 
     private final Arena arena = Arena.ofShared();
     private final ReentrantLock lock = new ReentrantLock();
@@ -237,6 +242,7 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
                 : metaStateEvent.getOutputDataAttributes().size();
         NativeDictionary keyDict = null;
         MemorySegment eng = MemorySegment.NULL;
+        ColumnarBatch cb = null;
         try {
             keyDict = new NativeDictionary(maxKeys, "partition keys (max_keys = " + maxKeys + ")");
             MemorySegment cfg = arena.allocate(ShpNative.CONFIG);
@@ -298,8 +304,23 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
                 throw new SiddhiAppCreationException("shp_engine_stat failed", t);
             }
             matches = arena.allocate(ShpNative.MATCHES);
-            batch = new ColumnarBatch(arena, maxBatch, info.columns, strings, 1 << 12);
+            cb = new ColumnarBatch(arena, maxBatch, info.columns, strings, 1 << 12,
+                    policy == FlushPolicy.PIPELINED ? 2 : 1);
+            if (policy == FlushPolicy.PIPELINED) {
+                try {
+                    cb.pin();
+                } catch (Throwable t) {
+                    throw new SiddhiAppCreationException("shp_host_register of the batch columns failed: " + t, t);
+                }
+            }
         } catch (RuntimeException e) {
+            if (cb != null) {
+                try {
+                    cb.unpin();
+                } catch (Throwable ignored) {
+                    // the creation error is the one to report
+                }
+            }
             if (!eng.equals(MemorySegment.NULL)) {
                 try {
                     ShpNative.ENGINE_DESTROY.invokeExact(eng);
@@ -315,7 +336,8 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         }
         this.engine = eng;
         this.keys = keyDict;
-        if (policy == FlushPolicy.DEFERRED) {
+        this.batch = cb;
+        if (policy != FlushPolicy.SYNC) {
             flusher = Executors.newSingleThreadScheduledExecutor(r -> {
                 Thread t = new Thread(r, "siddhi-gpu-flush");
                 t.setDaemon(true);
@@ -419,10 +441,18 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
     }
 
     /** One shp_push_batch of the appended events, then one StateEvent per match into the
-     * selector, in record order (per key = the reference's emission order). */
+     * selector, in record order (per key = the reference's emission order).  PIPELINED: stage the
+     * appended events, then run the batch staged before them (or, with nothing new, what is staged). */
     void flush() {
         lock.lock();
         try {
+            if (policy == FlushPolicy.PIPELINED) {
+                boolean fresh = stageOpen();
+                if (batch.stagedCount() > (fresh ? 1 : 0)) {
+                    runStaged();
+                }
+                return;
+            }
             if (batch.size() == 0) {
                 return;
             }
@@ -449,6 +479,62 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         } finally {
             lock.unlock();
         }
+    }
+
+    /** Every appended and staged event through the engine (PIPELINED's drain before the clock moves,
+     * a snapshot or restore, shutdown); flush() otherwise. */
+    private void drain() {
+        lock.lock();
+        try {
+            flush();
+            while (batch.stagedCount() > 0) {
+                runStaged();
+            }
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /** PIPELINED: shp_stage_batch of the open rows (false when there are none). */
+    private boolean stageOpen() {
+        if (batch.size() == 0) {
+            return false;
+        }
+        int rc;
+        try {
+            rc = (int) ShpNative.STAGE_BATCH.invokeExact(engine, batch.descriptor());
+        } catch (Throwable t) {
+            batch.discard();
+            throw new SiddhiAppRuntimeException("shp_stage_batch failed: " + t, t);
+        }
+        if (rc != ShpNative.OK) {
+            batch.discard();   // not staged: the engine's counter and slots are as before
+            throw new SiddhiAppRuntimeException("shp_stage_batch: " + ShpNative.codeName(rc) + ": "
+                    + ShpNative.lastError(engine));
+        }
+        batch.markStaged();
+        return true;
+    }
+
+    /** PIPELINED: shp_run_staged of the oldest staged batch, then its records as a push's. */
+    private void runStaged() {
+        long pushed = batch.stagedSize();
+        int rc;
+        try {
+            rc = (int) ShpNative.RUN_STAGED.invokeExact(engine, matches);
+        } catch (Throwable t) {
+            batch.dropStaged();
+            throw new SiddhiAppRuntimeException("shp_run_staged failed: " + t, t);
+        }
+        if (rc != ShpNative.OK) {
+            batch.dropStaged();   // as a failed push: the engine's state and counter are as before
+            throw new SiddhiAppRuntimeException("shp_run_staged: " + ShpNative.codeName(rc) + ": "
+                    + ShpNative.lastError(engine));
+        }
+        long seq0 = batch.commitStaged();
+        deliver(seq0, pushed);
+        batch.maybeTrim(this::oldestLiveSeq);
+        scheduleWake();
     }
 
     /** shp_engine_oldest_live_seq: the oldest event an open partial of the committed state holds. */
@@ -551,7 +637,7 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         rethrowDeferred();
         lock.lock();
         try {
-            flush();
+            drain();
             int rc;
             try {
                 rc = (int) ShpNative.ADVANCE_CLOCK.invokeExact(engine, now, matches);
@@ -729,7 +815,7 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         rethrowDeferred();
         lock.lock();
         try {
-            flush();
+            drain();
             MemorySegment buf = arena.allocate(ADDRESS);
             MemorySegment len = arena.allocate(JAVA_LONG);
             int rc = (int) ShpNative.SNAPSHOT.invokeExact(engine, buf, len);
@@ -798,6 +884,9 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         }
         lock.lock();
         try {
+            while (batch.stagedCount() > 0) {
+                runStaged();   // PIPELINED: staged events were sent before the restore
+            }
             restore((byte[]) m.get("GpuEngineSnapshot"));
             Object[] rows = (Object[]) m.get("LiveRows");
             batch.restoreRows((long[]) rows[0], (long[]) rows[1], (Object[][]) rows[2], (Long) m.get("NextSeq"));
@@ -848,8 +937,9 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         }
         lock.lock();
         try {
-            flush();
+            drain();
             ShpNative.ENGINE_DESTROY.invokeExact(engine);
+            batch.unpin();
             keys.close();
             strings.close();
         } catch (Throwable t) {

@@ -122,12 +122,16 @@ class _QueryRun:
         self.retain = rt.retain and hasattr(engine, "oldest_live_seq")
         # absent states: the query's Scheduler listens to the app clock (Scheduler.java:71-103)
         self.timers = any(st.get("absent") for st in cq.program["states"])
+        # pipelined ingest (shp_stage_batch / shp_run_staged): the batch whose H2D is in flight while
+        # the next one is built -- (rows, ts, key, stream) -- run at the next push or at a drain point
+        self.pipelined = rt.pipelined and self.compact and hasattr(engine, "stage")
+        self.inflight = None
 
 
 class SiddhiAppRuntime:
     def __init__(self, text: str, engine_factory: Callable, start_clock: Optional[int] = None,
                  batch_size: int = 1 << 20, native_lowering: bool = False, compact: bool = False,
-                 retain: bool = True, min_trim: int = 4096):
+                 retain: bool = True, min_trim: int = 4096, pipelined: bool = False):
         """native_lowering: engines are created from the SiddhiQL text by the library
         (shp_engine_create_siddhiql), as the Java host does; string values then use the library's
         dictionary, shared with the lowering's filter constants.
@@ -135,7 +139,15 @@ class SiddhiAppRuntime:
         compact: engines made with SHP_LAYOUT_COMPACT and pushed with shp_push_batch_compact, the
         records decoded on the host (PAIRS32 / CHAIN32), as the Java binding does.
         retain / min_trim: keep the pushed rows only from the engine's oldest live sequence number on
-        (history.RowHistory), asking the engine once the kept rows reach min_trim and have doubled."""
+        (history.RowHistory), asking the engine once the kept rows reach min_trim and have doubled.
+        pipelined (with compact and batch_size > 1, GpuStateStreamRuntime's PIPELINED flush): each
+        flush stages its batch (shp_stage_batch: the H2D on the engine's copy stream) and runs the
+        batch staged before it (shp_run_staged), so batch i+1's copies overlap batch i's kernels; the
+        callbacks of a batch arrive one flush later, and every drain point
+        (shutdown, advance_time, heartbeat) runs the batch still staged first."""
+        if pipelined and batch_size == 1:
+            raise ValueError("pipelined ingest needs batched flushes (batch_size > 1)")
+        self.pipelined = pipelined
         self.compact = compact
         self.retain = retain
         self.min_trim = min_trim
@@ -184,6 +196,14 @@ class SiddhiAppRuntime:
 
     def shutdown(self):
         self.flush()
+        self._run_inflight()
+
+    def _run_inflight(self, qr: Optional[_QueryRun] = None):
+        """Drain point of the pipelined flush: the batch still staged runs before the clock moves or
+        results are read (its sequence numbers precede whatever the engine sees next)."""
+        for q in ([qr] if qr is not None else list(self.queries.values())):
+            if q.inflight is not None:
+                self._finish(q)
 
     def _now_ms(self):
         return int(time.time() * 1000)
@@ -231,6 +251,7 @@ class SiddhiAppRuntime:
         self._ensure_queries()
         if self._batch_size == 1:
             self.flush()
+            self._run_inflight(qr)
             qr.engine.advance(int(now))
             self._drain(qr)
             self._trim(qr)
@@ -251,7 +272,9 @@ class SiddhiAppRuntime:
         if self.app.playback:
             self.timestamp_generator.set_current_timestamp(int(now))
             self.flush()
+            self._run_inflight()
             return
+        self._run_inflight()
         for qr in self.queries.values():
             if not qr.timers:
                 continue
@@ -269,6 +292,7 @@ class SiddhiAppRuntime:
         self.flush()
         if self.timestamp_generator.heartbeat(int(wall_ms)):
             self.flush()
+        self._run_inflight()
 
     # ---------------------------------------------------------------- flush
     def flush(self):
@@ -322,13 +346,29 @@ class SiddhiAppRuntime:
                 else:
                     cols[c][j] = v
         null_ptrs = [m if m.any() else None for m in nulls]
+        if qr.pipelined:
+            # stage this batch, then run the one staged before it: its kernels overlap these copies
+            qr.engine.stage(ts, key, stream, cols, null_ptrs)
+            if qr.inflight is not None:
+                self._finish(qr)
+            qr.inflight = (list(evs), ts, key, stream)
+            return
         if qr.compact:
             res = qr.engine.push_compact(ts, key, stream, cols, null_ptrs)
         else:
             qr.engine.push(ts, key, stream, cols, null_ptrs)
             res = None
+        self._commit(qr, list(evs), ts, key, stream, res)
+
+    def _finish(self, qr: _QueryRun):
+        """shp_run_staged of the query's oldest staged batch, then its records as a push's."""
+        evs, ts, key, stream = qr.inflight
+        qr.inflight = None
+        self._commit(qr, evs, ts, key, stream, qr.engine.run_staged())
+
+    def _commit(self, qr: _QueryRun, evs, ts, key, stream, res):
         # the engine took the push (its sequence counter moved by n): the rows join the history
-        seq0 = qr.history.add_block(list(evs))
+        seq0 = qr.history.add_block(evs)
         if res is not None and res["layout"] == 3:  # PAIRS32
             for i, slots in decode_pairs32(res["words"], seq0):
                 self._deliver(qr, int(key[i]), int(ts[i]), 0, slots)

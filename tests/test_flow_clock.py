@@ -389,3 +389,108 @@ def test_engine_next_due_equals_oracle(app, start):
         assert e.next_due() == o.next_due(), lo
         seen += o.next_due() is not None
     assert seen > 5
+
+
+# ------------------------------------------- pipelined flush (shp_stage_batch / shp_run_staged)
+class _StagedOracle(OracleEngine):
+    """The oracle behind the staged-ingest interface (host-logic check of the pipelined flush on the
+    CPU): stage() holds a copy of the batch, run_staged() pushes the oldest one.  Like the engine it
+    refuses a third staged batch, and a clock move or due-time query with a batch still staged is the
+    host's ordering defect, so it fails."""
+
+    def __init__(self, program_json, start, **kw):
+        super().__init__(program_json, start)
+        self.staged = []
+        self.max_staged = 0
+
+    def stat(self, which):
+        assert which == "match_layout"
+        return 0  # FULL records
+
+    def push_compact(self, ts, key, stream, cols, nulls):
+        self.push(ts, key, stream, cols, nulls)
+        out = self.fetch()
+        out["layout"] = 0
+        return out
+
+    def stage(self, ts, key, stream, cols, nulls):
+        assert len(self.staged) < 2, "two batches staged: run one first"
+        self.staged.append(tuple(np.array(a, copy=True) for a in (ts, key, stream)) +
+                           ([np.array(c, copy=True) for c in cols], [None if m is None else m.copy() for m in nulls]))
+        self.max_staged = max(self.max_staged, len(self.staged))
+
+    def run_staged(self):
+        return self.push_compact(*self.staged.pop(0))
+
+    def advance(self, now):
+        assert not self.staged, "clock moved past a staged batch"
+        super().advance(now)
+
+    def next_due(self):
+        assert not self.staged, "due time read with a batch staged"
+        return super().next_due()
+
+
+def _staged_oracle_factory(program_json, start, **kw):
+    return _StagedOracle(program_json, start)
+
+
+def test_pipelined_flush_needs_batches():
+    with pytest.raises(ValueError):
+        SiddhiManager(_oracle_factory).createSiddhiAppRuntime(synth.QUERIES[5], batch_size=1, compact=True,
+                                                             pipelined=True)
+
+
+@pytest.mark.parametrize("case", ["c5", "c4", "live", "heartbeat"])
+def test_pipelined_flush_host_logic(case, c5_case, c4_case, live_case):
+    """The pipelined flush's ordering on the CPU: batch i runs after batch i+1 is staged, the rows join
+    the history in run order, and every clock move / drain point runs the staged batch first -- the
+    same rows as the unpipelined mirror and the Direct transcription."""
+    f = _staged_oracle_factory
+    if case == "c5":
+        sends, want = c5_case
+        q = _run_mirror(f, synth.QUERIES[5], sends, 4096, compact=True, pipelined=True)
+        _assert_rows_close(_by_key(q.rows), want)
+    elif case == "c4":
+        sends, want = c4_case
+        q = _run_mirror(f, C4_TIMER_APP, sends, 997, compact=True, pipelined=True)
+        assert _by_key(q.rows) == want
+    elif case == "live":
+        sends, adv, want = live_case
+        q = _run_mirror(f, LIVE_APP, sends, 500, compact=True, pipelined=True, advances=adv, start_clock=sends[0][1])
+        assert _by_key(q.rows) == want
+    else:
+        at_sends, rows, _ = _heartbeat_run(f, 64, compact=True, pipelined=True)
+        assert at_sends == []  # the sends' batch is still staged at the first read (one flush late)
+        assert [r for _, r in rows] == [["GOOG"], ["WSO2"], ["GOOG"]]
+        q = None
+    if q is not None:
+        # (live mode's Thread.sleep every 97 sends drains before a 500-row batch fills)
+        assert q.pipelined and q.inflight is None and q.engine.max_staged == (1 if case == "live" else 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["c5", "c4", "live", "heartbeat"])
+def test_pipelined_flush_hip(case, c5_case, c4_case, live_case):
+    """The mirror's pipelined flush through shp_stage_batch / shp_run_staged on the GPU: the same rows
+    as the oracle (PAIRS32 for C5, the labs path's FULL records for C4, the lanes for live mode)."""
+    if case == "c5":
+        sends, want = c5_case
+        q = _run_mirror(_hip_factory(C5_KEYS), synth.QUERIES[5], sends, 4096, compact=True, pipelined=True)
+        assert q.layout == 3 and q.pipelined
+        _assert_rows_close(_by_key(q.rows), want)
+    elif case == "c4":
+        sends, want = c4_case
+        q = _run_mirror(_hip_factory(64), C4_TIMER_APP, sends, 997, compact=True, pipelined=True)
+        assert q.engine.path == 4 and q.pipelined
+        assert _by_key(q.rows) == want
+    elif case == "live":
+        sends, adv, want = live_case
+        q = _run_mirror(_hip_factory(64), LIVE_APP, sends, 500, compact=True, pipelined=True, advances=adv,
+                        start_clock=sends[0][1])
+        assert q.pipelined
+        assert _by_key(q.rows) == want
+    else:
+        at_sends, rows, _ = _heartbeat_run(_hip_factory(256), 64, compact=True, pipelined=True)
+        assert [r for _, r in rows] == [["GOOG"], ["WSO2"], ["GOOG"]]
+        assert [t for t, _ in rows] == [1544512386100, 1544512386800, 1544512387200]

@@ -424,7 +424,8 @@ def test_the_app_clock_reaches_the_engine():
     assert 'timers |= Boolean.TRUE.equals(m.get("absent"))' in pi
     cb = re.sub(r"/\*.*?\*/|//[^\n]*", "", _java("ColumnarBatch.java"), flags=re.S)
     app = _method(cb, "void append(long timestamp, int keyId, int streamIndex, Object[] data)")
-    assert "streamIndex >= 0 && n > 0 && streamAt(n - 1) < 0 && rowTs.get((int) n - 1) == timestamp" in app
+    assert ("streamIndex >= 0 && n > 0 && o.stream.getAtIndex(JAVA_INT, n - 1) < 0" in app
+            and "o.rowTs.get((int) n - 1) == timestamp" in app)
     assert "append(now, 0, -1, null)" in _method(cb, "void appendClock(long now)")
 
 
@@ -437,3 +438,36 @@ def test_columnar_batch_finds_rows_by_bisection_and_restore_validates():
     rt = re.sub(r"/\*.*?\*/|//[^\n]*", "", _java("GpuStateStreamRuntime.java"), flags=re.S)
     rf = _method(rt, "void restoreFrom(Map<String, Object> m)")
     assert rf.index('m.get("LiveRows") instanceof Object[]') < rf.index("restore((byte[])")
+
+
+def test_pipelined_flush_stages_then_runs_the_older_batch():
+    """FlushPolicy.PIPELINED (the mirror: SiddhiAppRuntime(pipelined=True), tests/test_flow_clock.py):
+    flush stages the open rows (shp_stage_batch from page-locked column sets) and runs the batch staged
+    before them (shp_run_staged), committing its rows in run order; every point that observes state
+    (advanceClock, snapshot, restore, shutdown) drains the staged batches first."""
+    rt = re.sub(r"/\*.*?\*/|//[^\n]*", "", _java("GpuStateStreamRuntime.java"), flags=re.S)
+    assert "enum FlushPolicy { SYNC, DEFERRED, PIPELINED }" in rt
+    fl = _method(rt, "void flush()")
+    assert fl.index("stageOpen()") < fl.index("runStaged()") < fl.index("PUSH_BATCH_COMPACT")
+    assert "batch.stagedCount() > (fresh ? 1 : 0)" in fl
+    st = _method(rt, "private boolean stageOpen()")
+    assert "ShpNative.STAGE_BATCH.invokeExact(engine, batch.descriptor())" in st
+    assert st.index("invokeExact") < st.index("batch.markStaged()")
+    run = _method(rt, "private void runStaged()")
+    assert run.index("batch.stagedSize()") < run.index("ShpNative.RUN_STAGED.invokeExact(engine, matches)")
+    assert run.index("RUN_STAGED") < run.index("batch.commitStaged()") < run.index("deliver(seq0, pushed)")
+    assert run.count("batch.dropStaged()") == 2
+    dr = _method(rt, "private void drain()")
+    assert "while (batch.stagedCount() > 0)" in dr
+    for m in ("void advanceClock(long now)", "byte[] snapshot()", "public void shutdown()"):
+        assert "drain();" in _method(rt, m), m
+    assert "runStaged()" in _method(rt, "void restoreFrom(Map<String, Object> m)")
+    assert "cb.pin()" in rt and "batch.unpin()" in _method(rt, "public void shutdown()")
+    cb = re.sub(r"/\*.*?\*/|//[^\n]*", "", _java("ColumnarBatch.java"), flags=re.S)
+    assert "ShpNative.HOST_REGISTER.invokeExact(m, m.byteSize())" in cb
+    ms = _method(cb, "void markStaged()")
+    assert "staged.addLast(open)" in ms and "open = free.pollFirst()" in ms
+    cs = _method(cb, "long commitStaged()")
+    assert cs.index("staged.pollFirst()") < cs.index("commitRows(c)") < cs.index("decoded = c")
+    for getter in ("int keyAt(long i)", "long tsAt(long i)", "int streamAt(long i)"):
+        assert "decoded." in _method(cb, getter)
