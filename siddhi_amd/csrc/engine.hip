@@ -605,9 +605,12 @@ struct shp_engine {
     } else {
       int gb = (int)std::min<int64_t>((n + 255) / 256, 2048);
       if (gb < 1) gb = 1;
-      // 1. clock (the count-sequence path has no timers: its kernel keeps the push's max ts)
+      // 1. clock (the count-sequence path has no timers: its kernel keeps the push's max ts; the
+      // logical-absent multisplit computes it in its own passes, labs.h k_la_seg_clock)
       size_t tb = tmp_bytes;
-      if (fast != 3) {
+      la.fuse_clock = fast == 4 && !labs_v1 && n > 0 && la.fuses_clock();
+      la.rmax_out = d_rmax;
+      if (fast != 3 && !la.fuse_clock) {
         kt.mark("clock_scan", stream);
         HIP_OK(rocprim::inclusive_scan(d_tmp, tb, B.tclk, d_rmax, (size_t)n, rocprim::maximum<int64_t>(), stream));
         kt.mark("clamp_clock", stream);

@@ -142,6 +142,8 @@ struct LabsDev {
   uint32_t warm;     // warm-up events before a cut (LA_WARM; SHP_LABS_WARM for tests)
   struct LaSnap* snap[2];  // segment boundary states: [0] warmed-up start of segment h, [1] end of h - 1
   int64_t* rc;             // the push's clock at the end of each 64-event block (k_labs_out's coarse search)
+  int64_t* segclk;         // multisplit segments: [0, nseg) each one's max clock column, [nseg, 2 nseg) the
+                           // clock before it (k_la_seg_clock) -- the fused clock scan
   int32_t pad2;
   unsigned long long* stamps;  // diagnostic build (SHP_SW_STAMPS): k_labs_w phase cycles per key
   LaRec* rec;        // k_labs_w's records, per key region (la_region)
@@ -245,26 +247,111 @@ __device__ __forceinline__ uint32_t la_bin(const BatchView& B, const int32_t* __
   }
   return (uint32_t)x;
 }
+// FC (the fused clock): the segment's running clock from its own events (segment-local: without the
+// clock carried in from earlier segments) to rmax, and its last value to segmax[seg] for
+// k_la_seg_clock.  Event g = lo + 1024 r + 256 w + 64 u + lane (round r, wave w, chunk u): lane-
+// contiguous loads, a DPP max-scan per chunk, the waves' totals combined through LDS.
+template <bool FC>
 static __global__ __launch_bounds__(256) void k_la_ms_count(BatchView B, const int32_t* __restrict__ key, int64_t n,
                                                             uint32_t nokey, int32_t nseg, uint32_t* __restrict__ cnt,
-                                                            int* err) {
+                                                            int* err, int64_t* __restrict__ segmax,
+                                                            int64_t* __restrict__ rloc) {
   __shared__ uint32_t h[LA_MS_BINS];
+  __shared__ int64_t wtot[4];
   const uint32_t nb = nokey + 1u;
   for (uint32_t b = threadIdx.x; b < nb; b += 256) h[b] = 0;
   __syncthreads();
   int e = 0;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  int64_t carry = INT64_MIN;  // FC: the segment's clock before this round
   const int64_t lo = (int64_t)blockIdx.x * LA_MS_SEG, hi = min(n, lo + LA_MS_SEG);
-  for (int64_t g = lo + threadIdx.x; g < hi; g += 256) {
-    const int st = B.stream ? B.stream[g] : 0;
-    atomicAdd(&h[la_bin(B, key, g, st, nokey, e)], 1u);
+  // four events a thread per round, their loads issued before the first LDS add
+  for (int64_t g = lo + (FC ? 256 * w + lane : threadIdx.x); g < hi + (FC ? 256 * w + lane : threadIdx.x);
+       g += 1024) {
+    int st[4], kx[4];
+    int64_t c[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int64_t x = g + (FC ? 64 : 256) * u;
+      const bool in = x < hi;
+      st[u] = in ? (B.stream ? B.stream[x] : 0) : -2;
+      kx[u] = in && B.partitioned ? key[x] : 0;
+      c[u] = FC && in ? B.tclk[x] : INT64_MIN;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (st[u] == -2) continue;
+      uint32_t bin = nokey;
+      if (st[u] >= 0) {
+        if (!B.partitioned) bin = 0;
+        else if (kx[u] < 0 || (uint32_t)kx[u] >= nokey) e |= 1 << 20;  // SWE_KEYS (la_bin)
+        else bin = (uint32_t)kx[u];
+      }
+      atomicAdd(&h[bin], 1u);
+    }
+    if (FC) {
+      int64_t run = INT64_MIN;  // the wave's running max over its chunks
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        int64_t v = c[u];
+        dpp_scan_steps(lane, [&](auto ctl, bool take) {
+          const int64_t y = (int64_t)dpp64<decltype(ctl)::value>((uint64_t)v);
+          if (take) v = max(v, y);
+        });
+        c[u] = max(v, run);
+        run = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(c[u] >> 32), 63) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)c[u], 63));
+      }
+      if (lane == 0) wtot[w] = run;
+      __syncthreads();
+      int64_t pre = carry;
+      for (uint32_t v = 0; v < w; v++) pre = max(pre, wtot[v]);
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int64_t x = g + 64 * u;
+        if (x < hi) rloc[x] = max(c[u], pre);
+      }
+      carry = max(max(carry, max(wtot[0], wtot[1])), max(wtot[2], wtot[3]));
+      __syncthreads();  // (wtot is rewritten next round)
+    }
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nb; b += 256) cnt[(int64_t)b * nseg + blockIdx.x] = h[b];
+  if (FC && threadIdx.x == 0) segmax[blockIdx.x] = carry;
   if (e) atomicOr(err, e);
 }
+// the clock before each segment: exclusive max-scan of the segment maxima seeded with the carried
+// clock (one workgroup; nseg = n / 16384, ~6k at 10^8 events)
+static __global__ __launch_bounds__(1024) void k_la_seg_clock(int64_t* __restrict__ segclk, int32_t nseg,
+                                                             int64_t clock0) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (nseg + 1023) / 1024;
+  const int a = min(nseg, t * per), b = min(nseg, a + per);
+  int64_t m = INT64_MIN;
+  for (int i = a; i < b; i++) m = max(m, segclk[i]);
+  part[t] = m;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // inclusive max-scan of the chunk maxima (Hillis-Steele)
+    const int64_t o = t >= d ? part[t - d] : INT64_MIN;
+    __syncthreads();
+    part[t] = max(part[t], o);
+    __syncthreads();
+  }
+  int64_t run = max(clock0, t > 0 ? part[t - 1] : INT64_MIN);
+  for (int i = a; i < b; i++) {
+    segclk[nseg + i] = run;
+    run = max(run, segclk[i]);
+  }
+}
+// FC (the fused clock): rmax holds the segment-local clock (k_la_ms_count<true>); the events it leaves
+// below the clock carried into the segment (k_la_seg_clock) are raised to it here -- in place of a
+// device-wide max-scan and a clamp
+template <bool FC>
 static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchView B, const int32_t* __restrict__ key,
                                                              int64_t n, uint32_t nokey, int32_t nseg, int bits,
-                                                             const uint32_t* __restrict__ off, int* err) {
+                                                             const uint32_t* __restrict__ off, int* err,
+                                                             int64_t* __restrict__ rmax_out) {
   __shared__ uint32_t cur[LA_MS_BINS];
   const uint32_t nb = nokey + 1u, lane = threadIdx.x;
   const int seg = blockIdx.x;
@@ -297,7 +384,7 @@ static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchVie
       f.st = B.stream ? B.stream[g] : 0;
       f.k = B.partitioned ? key[g] : 0;
       f.ts = B.ts[g];
-      f.clk = B.rmax[g];
+      f.clk = B.rmax[g];  // FC: segment-local (k_la_ms_count<true>), completed in place()
 #pragma unroll
       for (int r = 0; r < 3; r++) {
         if (r > 0 && onecol) {
@@ -311,15 +398,23 @@ static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchVie
     }
   };
   unsigned long long mxs = 0;  // the push's largest clock step after its first send (k_labs_w's check)
-  int64_t pclk = lo > 0 ? B.rmax[lo - 1] : INT64_MIN;  // the clock before the step's first event
+  // the clock before the step's first event
+  const int64_t cin = FC ? D.segclk[nseg + seg] : INT64_MIN;  // FC: the clock carried into the segment
+  int64_t pclk = FC ? cin : (lo > 0 ? B.rmax[lo - 1] : INT64_MIN);
   auto place = [&](const Pf& f, int64_t g0) __attribute__((always_inline)) {
     const int64_t g = g0 + lane;
     const bool valid = g < hi;
+    int64_t clk = f.clk;
+    if (FC) {  // rmax[g] = max(the clock carried into the segment, the segment-local clock): rewritten
+               // only where the carried clock is larger (a segment's first events, on disordered input)
+      clk = max(clk, cin);
+      if (valid && clk != f.clk) rmax_out[g] = clk;
+    }
     {
-      int64_t pc = __shfl_up(f.clk, 1, 64);
+      int64_t pc = __shfl_up(clk, 1, 64);
       if (lane == 0) pc = pclk;
-      if (valid && g >= 1) mxs = max(mxs, (unsigned long long)(f.clk - pc));
-      pclk = __shfl(f.clk, 63, 64);
+      if (valid && g >= 1) mxs = max(mxs, (unsigned long long)(clk - pc));
+      pclk = __shfl(clk, 63, 64);
     }
     const int rl = la_pack_role(D, f.st);
     const uint32_t xv = rl == 0 ? f.v[0] : (rl == 1 ? f.v[1] : (rl == 2 ? f.v[2] : 0u));
@@ -341,7 +436,7 @@ static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchVie
     }
     const uint32_t pos = __shfl(old, (int)ldl, 64) + below;
     if (valid) {
-      const int64_t dt = f.ts - base, dc = f.clk - base;
+      const int64_t dt = f.ts - base, dc = clk - base;
       if (dt != (int64_t)(int32_t)dt || dc != (int64_t)(int32_t)dc || g >= (1ll << 27)) e |= LA_WIDE;
       LaEv16 x;
       x.ts = (int32_t)dt;
@@ -2247,6 +2342,11 @@ struct LabsState {
   uint32_t* ms_cnt = nullptr;
   uint32_t* ms_off = nullptr;
   bool bounds = false;
+  // the fused clock (k_la_ms_count / k_la_seg_clock / k_la_ms_scatter<true>): set by the engine for a
+  // push that skips the device-wide clock scan (the count pass and the scatter then write rmax_out)
+  bool fuse_clock = false;
+  int64_t* rmax_out = nullptr;
+  bool fuses_clock() const { return ms_cnt != nullptr && D.segclk != nullptr && !getenv("SHP_LABS_SCAN_CLOCK"); }
   bool split_ok(int64_t cap) const {
     return D.nk + 1 <= LA_MS_BINS && cap < (1ll << 27) && !getenv("SHP_LABS_SORT");
   }
@@ -2261,7 +2361,10 @@ struct LabsState {
       while ((1u << bits) < nokey + 1u) bits++;
       const size_t nc = (size_t)(nokey + 1) * nseg + 1;
       kt.mark("labs_count", s);
-      k_la_ms_count<<<(unsigned)nseg, 256, 0, s>>>(B, key, B.n, nokey, nseg, ms_cnt, err);
+      const bool fc = fuse_clock;
+      if (fc) k_la_ms_count<true><<<(unsigned)nseg, 256, 0, s>>>(B, key, B.n, nokey, nseg, ms_cnt, err, D.segclk, rmax_out);
+      else k_la_ms_count<false><<<(unsigned)nseg, 256, 0, s>>>(B, key, B.n, nokey, nseg, ms_cnt, err, nullptr, nullptr);
+      if (fc) k_la_seg_clock<<<1, 1024, 0, s>>>(D.segclk, nseg, B.clock0);
       (void)hipMemsetAsync(ms_cnt + nc - 1, 0, sizeof(uint32_t), s);
       kt.mark("labs_mscan", s);
       size_t tb = stmp_bytes;
@@ -2269,7 +2372,8 @@ struct LabsState {
       kt.mark("labs_split", s);
       (void)hipMemsetAsync(D.maxstep, 0, sizeof(unsigned long long), s);
       steps_done = true;
-      k_la_ms_scatter<<<(unsigned)nseg, 64, 0, s>>>(D, B, key, B.n, nokey, nseg, bits, ms_off, err);
+      if (fc) k_la_ms_scatter<true><<<(unsigned)nseg, 64, 0, s>>>(D, B, key, B.n, nokey, nseg, bits, ms_off, err, rmax_out);
+      else k_la_ms_scatter<false><<<(unsigned)nseg, 64, 0, s>>>(D, B, key, B.n, nokey, nseg, bits, ms_off, err, nullptr);
       k_la_ms_bounds<<<(unsigned)((nokey + 255) / 256), 256, 0, s>>>(ms_off, nseg, nokey, kbeg, kcnt);
       kt.mark(nullptr, s);
       sorted = true;
@@ -2296,6 +2400,7 @@ struct LabsState {
       const size_t nc = (size_t)(D.nk + 1) * (size_t)((std::max<int64_t>(cap, 1) + LA_MS_SEG - 1) / LA_MS_SEG) + 1;
       al(ms_cnt, (int64_t)nc);
       al(ms_off, (int64_t)nc);
+      al(D.segclk, 2 * ((std::max<int64_t>(cap, 1) + LA_MS_SEG - 1) / LA_MS_SEG));
       size_t b2 = 0;
       (void)rocprim::exclusive_scan(nullptr, b2, ms_cnt, ms_off, 0u, nc, rocprim::plus<uint32_t>(), s);
       b = std::max(b, b2);
@@ -2349,7 +2454,7 @@ struct LabsState {
     }
     if (D.wtmp) (void)hipFree(D.wtmp);
     if (D.ftmp) (void)hipFree(D.ftmp);
-    void* qs[] = {D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp, D.maxstep, ms_cnt, ms_off, D.snap[0], D.snap[1], D.rc};
+    void* qs[] = {D.cm, D.om, D.p_ev, D.s_ev, D.rec, D.stamps, stmp, D.maxstep, ms_cnt, ms_off, D.snap[0], D.snap[1], D.rc, D.segclk};
     for (void* p : qs)
       if (p) (void)hipFree(p);
     D = LabsDev{};

@@ -610,3 +610,54 @@ def test_labs_segments_vs_oracle_and_unsegmented_state(monkeypatch, step, warm):
     assert sum(len(x) for x in want.values()) > 50
     assert a.stat("labs_fallbacks") == 0
     assert (a.stat("labs_segmiss") > 0) == (warm is not None)
+
+
+def _sawtooth_c4(seed, n=200_000):
+    """C4-shaped stream over many 16384-event multisplit segments whose clock steps back at segment
+    boundaries (each segment starts below the previous one's maximum), plus the local disorder of
+    unordered_c4's mode: the fused clock's carried-in value is what orders those events."""
+    rng = np.random.default_rng(500 + seed)
+    keys = [7, 40, 200][seed % 3]
+    ts = (np.arange(n) * 3).astype(np.int64) + 1_000_000
+    seg = np.arange(n) // 16384
+    ts = ts - (seg % 2) * int(rng.integers(1000, 60_000))  # odd segments start below the last clock
+    if seed % 2:
+        ts = ts + rng.integers(-500, 500, n)
+    key = rng.integers(0, keys, n).astype(np.int32)
+    st = rng.integers(0, 3, n).astype(np.int32)
+    pr = (rng.integers(0, 10000, n) / 100.0).astype(np.float32)
+    return ts, key, st, pr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("batch", [70_001, 1 << 16])
+def test_labs_fused_clock_across_segments(seed, batch, monkeypatch):
+    """The multisplit's fused clock (k_la_ms_count<true> segment-local scan, k_la_seg_clock, the
+    scatter's carried-in fix-up) over pushes of several 16384-event segments whose clock steps back
+    at the boundaries: records equal the device-wide scan's (SHP_LABS_SCAN_CLOCK=1) and the oracle's."""
+    from siddhi_amd.native import HipEngine
+    ts, key, st, pr = _sawtooth_c4(seed)
+    cq = program_for(4)
+
+    def drive(env):
+        if env:
+            monkeypatch.setenv("SHP_LABS_SCAN_CLOCK", "1")
+        else:
+            monkeypatch.delenv("SHP_LABS_SCAN_CLOCK", raising=False)
+        e = HipEngine(cq.program_json(), 0, max_keys=256, max_batch=1 << 17)
+        assert e.path == 4
+        for lo in range(0, len(ts), batch):
+            hi = min(len(ts), lo + batch)
+            e.push(ts[lo:hi], key[lo:hi], st[lo:hi], [pr[lo:hi]] * 3, [None] * 3)
+        return per_key(e.fetch())
+    fused, scanned = drive(False), drive(True)
+    assert compare(scanned, fused) is None, compare(scanned, fused)
+    o = OracleEngine(cq.program_json(), 0)
+    for lo in range(0, len(ts), batch):
+        hi = min(len(ts), lo + batch)
+        o.push(ts[lo:hi], key[lo:hi], st[lo:hi], [pr[lo:hi]] * 3, [None] * 3)
+    if not o.timer_ties():
+        want = per_key(o.fetch())
+        assert compare(want, fused) is None, compare(want, fused)
+    assert sum(len(x) for x in fused.values()) > 100
