@@ -352,6 +352,9 @@ static __global__ __launch_bounds__(64) void k_la_ms_scatter(LabsDev D, BatchVie
                                                              int64_t n, uint32_t nokey, int32_t nseg, int bits,
                                                              const uint32_t* __restrict__ off, int* err,
                                                              int64_t* __restrict__ rmax_out) {
+  // the keys' cursors.  The fixed 16 KB table also sets the residency: 10 waves a CU measured best
+  // (C4 scatter 2.63 ms; 24 waves with only the 4 KB 1000 keys need: 3.29 ms, 6 waves: 2.87, 5: 4.09 --
+  // its partial-line writes contend, profiles/r06_scatter_occupancy.txt)
   __shared__ uint32_t cur[LA_MS_BINS];
   const uint32_t nb = nokey + 1u, lane = threadIdx.x;
   const int seg = blockIdx.x;
