@@ -97,6 +97,9 @@ def parse():
                     help="SURVEY §8d(b) end-to-end host ingest: steps of N events from page-locked host columns "
                          "through shp_stage_batch / shp_run_staged (records back to host memory); 0: skip")
     ap.add_argument("--e2e-batch", type=int, default=12_500_000, help="events per staged host batch")
+    ap.add_argument("--e2e-modes", default=None,
+                    help="comma list of end-to-end forms to run (default all: serial, pipelined, pipelined_ts32, "
+                         "pipelined_narrow); tools/gpu_e2e_trace.sh traces one at a time")
     return ap.parse_args()
 
 
@@ -289,7 +292,7 @@ def main():
         del batches
         torch.cuda.empty_cache()
         e2e = end_to_end(cq, L, native, spec, K, a.e2e_batch, N, a.e2e_steps, (a.warmup + 2 * a.steps + 4) * N,
-                         force, mlay, layout, local)
+                         force, mlay, layout, local, a.e2e_modes)
 
     if rank == 0:
         value = ev_total / elapsed
@@ -523,7 +526,7 @@ def batch_latency(eng, L, native, spec, K, layout, n, batches, start):
             "what": "shp_push_batch_device entry -> match payload in host memory"}
 
 
-def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout, device):
+def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout, device, only=None):
     """the step's N events from page-locked host SoA columns (the Java host's
     ColumnarBatch segments, pinned with shp_host_register) to match records in host memory, in
     batches of nb events: (1) serial -- shp_push_batch_compact per batch, the copy, the run and the
@@ -581,6 +584,8 @@ def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout,
 
     res = {}
     modes = ("serial", "pipelined", "pipelined_ts32") + (("pipelined_narrow",) if K <= 65536 else ())
+    if only:
+        modes = tuple(m for m in modes if m in only.split(","))
     for mode in modes:
         e = native.HipEngine(cq.program_json(), 0, max_keys=K, max_batch=nb, max_matches=int(nb * 1.1) + 4096,
                              device=device, force_general=force, match_layout=native.LAYOUT_COMPACT)
@@ -638,7 +643,7 @@ def end_to_end(cq, L, native, spec, K, nb, N, steps, start, force, mlay, layout,
     torch.cuda.synchronize()
     h2d = 4 * (1 << 30) / (time.perf_counter() - t0) / 1e9
     del hb, db, host
-    best = max([m for m in modes if m != "serial"], key=lambda k: res[k]["value"])
+    best = max([m for m in modes if m != "serial"] or list(modes), key=lambda k: res[k]["value"])
     return {"value": res[best]["value"], "unit": "events/s", "ms_per_step": res[best]["ms_per_step"],
             "mode": best, "batch_events": nb, "batches_per_step": nsub, "steps": steps, "forms": res,
             "h2d_copy_gbs": h2d,
