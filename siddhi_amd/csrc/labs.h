@@ -2049,6 +2049,55 @@ static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, co
   if (e) atomicOr(err, e);
 }
 
+// first index in (lo, hi] whose clock reaches thr, given c[lo] < thr (hi when none does), over a
+// non-decreasing clock array: a push's clock is close to linear in the index, so an interpolated
+// guess probed with both neighbours (three loads at once, one latency) usually ends the search;
+// bisection steps between the guesses bound the worst case
+__device__ __forceinline__ int64_t la_clock_lb(const int64_t* __restrict__ c, int64_t lo, int64_t hi, int64_t rlo,
+                                               int64_t rhi, int64_t thr) {
+  bool interp = true;
+  while (hi - lo > 1) {
+    int64_t m;
+    if (interp && rhi > rlo) {
+      const double f = (double)(thr - rlo) / (double)(rhi - rlo);
+      m = lo + (int64_t)(f * (double)(hi - lo));
+      m = m <= lo ? lo + 1 : (m >= hi ? hi - 1 : m);
+    } else {
+      m = lo + ((hi - lo) >> 1);
+    }
+    const bool pl = interp && m - 1 > lo, pr = interp && m + 1 < hi;
+    interp = !interp;
+    const int64_t rm = c[m];
+    const int64_t rp = pl ? c[m - 1] : 0, rn = pr ? c[m + 1] : 0;
+    if (rm >= thr) {
+      hi = m;
+      rhi = rm;
+      if (pl) {
+        if (rp >= thr) {
+          hi = m - 1;
+          rhi = rp;
+        } else {
+          lo = m - 1;
+          rlo = rp;
+        }
+      }
+    } else {
+      lo = m;
+      rlo = rm;
+      if (pr) {
+        if (rn >= thr) {
+          hi = m + 1;
+          rhi = rn;
+        } else {
+          lo = m + 1;
+          rlo = rn;
+        }
+      }
+    }
+  }
+  return hi;
+}
+
 // k_labs_w's records of each key (its region of D.rec) to the push's output at the key's offset,
 // with the fire event found as k_labs_pos does
 static __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B, MatchOut O, const uint32_t* __restrict__ kbeg,
@@ -2079,19 +2128,18 @@ static __global__ __launch_bounds__(256) void k_labs_out(LabsDev D, BatchView B,
     int64_t a = x.flo, b = min((int64_t)x.fhi, B.n - 1);
     if (x.thr == INT64_MIN) b = a;  // (an exact block's firing at a known send)
     if (D.rc && a < b) {  // the 64-event block first reaching thr (rc: each block's last clock), then within it
-      int64_t ja = a >> 6, jb = b >> 6;
-      while (ja < jb) {
-        const int64_t mid = ja + ((jb - ja) >> 1);
-        if (D.rc[mid] >= x.thr) jb = mid;
-        else ja = mid + 1;
+      int64_t ja = a >> 6;
+      const int64_t jb = b >> 6;
+      if (ja < jb) {
+        const int64_t r0 = D.rc[ja];
+        if (r0 < x.thr) ja = la_clock_lb(D.rc, ja, jb, r0, D.rc[jb], x.thr);
       }
       a = max(a, ja << 6);
       b = min(b, (ja << 6) + 63);
     }
-    while (a < b) {
-      const int64_t mid = a + ((b - a) >> 1);
-      if (B.rmax[mid] >= x.thr) b = mid;
-      else a = mid + 1;
+    if (a < b) {
+      const int64_t r0 = B.rmax[a];
+      if (r0 < x.thr) a = la_clock_lb(B.rmax, a, b, r0, B.rmax[b], x.thr);
     }
     O.key[m] = B.partitioned ? k : 0;
     O.ts[m] = x.due;
