@@ -16,6 +16,7 @@ echo "pmc c2 done"
 for c in 3b 4 5; do
   k=1000000; [ $c = 4 ] && k=1000; [ $c = 5 ] && k=100000
   BENCH_ARGS="--no-expanded" NO_LV=1 CFG=$c KEYS=$k bash tools/pmc_cfg.sh > gpurun_out/pmc_cfg_$c.log 2>&1 || { tail -5 gpurun_out/pmc_cfg_$c.log; exit 1; }
+  [ $c = 4 ] && cp gpurun_out/pmc_4_traffic.json gpurun_out/pmc_4o_traffic.json  # (the 4d pass below rewrites it)
   echo "pmc c$c done"
 done
 BENCH_ARGS="--no-expanded --disorder 0.01" NO_LV=1 CFG=4 KEYS=1000 PMC_DISORDER=0.01 bash tools/pmc_cfg.sh > gpurun_out/pmc_cfg_4d.log 2>&1 || { tail -5 gpurun_out/pmc_cfg_4d.log; exit 1; }
