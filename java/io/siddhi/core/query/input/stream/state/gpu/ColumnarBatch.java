@@ -40,6 +40,7 @@ import static java.lang.foreign.ValueLayout.JAVA_DOUBLE;
 import static java.lang.foreign.ValueLayout.JAVA_FLOAT;
 import static java.lang.foreign.ValueLayout.JAVA_INT;
 import static java.lang.foreign.ValueLayout.JAVA_LONG;
+import static java.lang.foreign.ValueLayout.JAVA_SHORT;
 
 final class ColumnarBatch {
 
@@ -87,8 +88,15 @@ final class ColumnarBatch {
         final List<Object[]> rows = new ArrayList<>();
         final List<Long> rowTs = new ArrayList<>();
         long n;
+        // the narrow form (shp_stage_batch_narrow): ts as 4-byte offsets from the batch's first ts and
+        // 2-byte key ids, kept beside the wide columns; `wide` once an offset leaves the int range
+        final MemorySegment ts32, key16;
+        long base;
+        boolean wide;
 
         Columns() {
+            ts32 = narrow ? arena.allocate(JAVA_INT, capacity) : null;
+            key16 = narrow ? arena.allocate(JAVA_SHORT, capacity) : null;
             ts = arena.allocate(JAVA_LONG, capacity);
             key = arena.allocate(JAVA_INT, capacity);
             stream = arena.allocate(JAVA_INT, capacity);
@@ -107,6 +115,10 @@ final class ColumnarBatch {
 
         List<MemorySegment> segments() {
             List<MemorySegment> l = new ArrayList<>(List.of(ts, key, stream));
+            if (narrow) {
+                l.add(ts32);
+                l.add(key16);
+            }
             l.addAll(Arrays.asList(cols));
             l.addAll(Arrays.asList(nulls));
             return l;
@@ -123,6 +135,7 @@ final class ColumnarBatch {
     private final long capacity;
     private final Column[] columns;
     private final NativeDictionary strings;           // string-attribute dictionary (shared with the filters)
+    private final boolean narrow;                     // PIPELINED with max_keys <= 65536: narrow columns too
     private Columns open;                             // the set appends go to (null only inside a flush)
     private Columns decoded;                          // the set of the last committed push (keyAt / tsAt / streamAt)
     private final ArrayDeque<Columns> staged = new ArrayDeque<>();  // PIPELINED: staged, oldest first
@@ -138,12 +151,15 @@ final class ColumnarBatch {
     private final long minTrim;
     private long trimAt;
 
-    /** @param sets 1 (SYNC / DEFERRED) or 2 (PIPELINED: the second set fills while the first is staged) */
-    ColumnarBatch(Arena arena, long capacity, Column[] columns, NativeDictionary strings, long minTrim, int sets) {
+    /** @param sets   1 (SYNC / DEFERRED) or 2 (PIPELINED: the second set fills while the first is staged)
+     *  @param narrow keep the narrow form's columns too (key ids below 65536) */
+    ColumnarBatch(Arena arena, long capacity, Column[] columns, NativeDictionary strings, long minTrim, int sets,
+                  boolean narrow) {
         this.arena = arena;
         this.capacity = capacity;
         this.columns = columns;
         this.strings = strings;
+        this.narrow = narrow;
         this.minTrim = Math.max(1, minTrim);
         this.trimAt = this.minTrim;
         open = new Columns();
@@ -154,7 +170,7 @@ final class ColumnarBatch {
     }
 
     ColumnarBatch(Arena arena, long capacity, Column[] columns, NativeDictionary strings, long minTrim) {
-        this(arena, capacity, columns, strings, minTrim, 1);
+        this(arena, capacity, columns, strings, minTrim, 1, false);
     }
 
     /** Page-locks every column segment (shp_host_register) so shp_stage_batch's copies run at DMA rate
@@ -206,6 +222,18 @@ final class ColumnarBatch {
         }
         o.ts.setAtIndex(JAVA_LONG, n, timestamp);
         o.key.setAtIndex(JAVA_INT, n, keyId);
+        if (narrow) {
+            if (n == 0) {
+                o.base = timestamp;
+                o.wide = false;
+            }
+            long d = timestamp - o.base;
+            if (d != (int) d) {
+                o.wide = true;
+            }
+            o.ts32.setAtIndex(JAVA_INT, n, (int) d);
+            o.key16.setAtIndex(JAVA_SHORT, n, (short) keyId);   // (ids < 65536: read back unsigned)
+        }
         o.stream.setAtIndex(JAVA_INT, n, streamIndex);
         for (int c = 0; c < columns.length; c++) {
             Column col = columns[c];
@@ -249,6 +277,23 @@ final class ColumnarBatch {
         o.descriptor.set(ADDRESS, 48, MemorySegment.NULL);  // clock: the events' own ts
         o.descriptor.set(ADDRESS, 56, MemorySegment.NULL);  // seq: the engine's running count
         return o.descriptor;
+    }
+
+    /** The open rows can go in the narrow form (shp_stage_batch_narrow). */
+    boolean narrowOk() {
+        return narrow && open.n > 0 && !open.wide;
+    }
+
+    long narrowBase() {
+        return open.base;
+    }
+
+    MemorySegment ts32() {
+        return open.ts32;
+    }
+
+    MemorySegment key16() {
+        return open.key16;
     }
 
     /** After a failed push or stage: the engine did not take the rows (its sequence counter did not

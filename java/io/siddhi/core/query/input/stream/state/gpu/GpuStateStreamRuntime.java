@@ -304,8 +304,10 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
                 throw new SiddhiAppCreationException("shp_engine_stat failed", t);
             }
             matches = arena.allocate(ShpNative.MATCHES);
+            // PIPELINED with 2-byte key ids possible: the narrow form's columns too (10 B/event for one
+            // 4-byte column instead of 16; bench.py end_to_end "pipelined_narrow")
             cb = new ColumnarBatch(arena, maxBatch, info.columns, strings, 1 << 12,
-                    policy == FlushPolicy.PIPELINED ? 2 : 1);
+                    policy == FlushPolicy.PIPELINED ? 2 : 1, policy == FlushPolicy.PIPELINED && maxKeys <= 65536);
             if (policy == FlushPolicy.PIPELINED) {
                 try {
                     cb.pin();
@@ -502,7 +504,12 @@ public final class GpuStateStreamRuntime extends StateStreamRuntime {
         }
         int rc;
         try {
-            rc = (int) ShpNative.STAGE_BATCH.invokeExact(engine, batch.descriptor());
+            if (batch.narrowOk()) {   // ts offsets from the batch's first ts and 2-byte key ids
+                rc = (int) ShpNative.STAGE_BATCH_NARROW.invokeExact(engine, batch.descriptor(), batch.narrowBase(),
+                        batch.ts32(), batch.key16());
+            } else {
+                rc = (int) ShpNative.STAGE_BATCH.invokeExact(engine, batch.descriptor());
+            }
         } catch (Throwable t) {
             batch.discard();
             throw new SiddhiAppRuntimeException("shp_stage_batch failed: " + t, t);

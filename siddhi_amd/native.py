@@ -273,6 +273,7 @@ class HipEngine:
         self.S = L.shp_engine_num_states(h)
         self.col_bytes = _column_bytes(program_json)
         self.max_batch = max_batch
+        self.max_keys = max_keys
         self.layout = int(match_layout)
         self._pending = None
 

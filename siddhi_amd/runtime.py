@@ -126,12 +126,13 @@ class _QueryRun:
         # the next one is built -- (rows, ts, key, stream) -- run at the next push or at a drain point
         self.pipelined = rt.pipelined and self.compact and hasattr(engine, "stage")
         self.inflight = None
+        self.narrow_batches = 0  # staged in the narrow form (tests)
 
 
 class SiddhiAppRuntime:
     def __init__(self, text: str, engine_factory: Callable, start_clock: Optional[int] = None,
                  batch_size: int = 1 << 20, native_lowering: bool = False, compact: bool = False,
-                 retain: bool = True, min_trim: int = 4096, pipelined: bool = False):
+                 retain: bool = True, min_trim: int = 4096, pipelined: bool = False, narrow: bool = False):
         """native_lowering: engines are created from the SiddhiQL text by the library
         (shp_engine_create_siddhiql), as the Java host does; string values then use the library's
         dictionary, shared with the lowering's filter constants.
@@ -144,10 +145,16 @@ class SiddhiAppRuntime:
         flush stages its batch (shp_stage_batch: the H2D on the engine's copy stream) and runs the
         batch staged before it (shp_run_staged), so batch i+1's copies overlap batch i's kernels; the
         callbacks of a batch arrive one flush later, and every drain point
-        (shutdown, advance_time, heartbeat) runs the batch still staged first."""
+        (shutdown, advance_time, heartbeat) runs the batch still staged first.
+        narrow (with pipelined): a staged batch whose ts lie within 2^31 ms of its first goes in the
+        narrow form (shp_stage_batch_narrow: 4-byte ts offsets from that first ts, 2-byte key ids, as
+        ColumnarBatch's narrow column sets under max_keys <= 65536); other batches in the wide form."""
         if pipelined and batch_size == 1:
             raise ValueError("pipelined ingest needs batched flushes (batch_size > 1)")
+        if narrow and not pipelined:
+            raise ValueError("the narrow ingest form is a form of the pipelined flush")
         self.pipelined = pipelined
+        self.narrow = narrow
         self.compact = compact
         self.retain = retain
         self.min_trim = min_trim
@@ -348,7 +355,14 @@ class SiddhiAppRuntime:
         null_ptrs = [m if m.any() else None for m in nulls]
         if qr.pipelined:
             # stage this batch, then run the one staged before it: its kernels overlap these copies
-            qr.engine.stage(ts, key, stream, cols, null_ptrs)
+            d = ts - ts[0] if n else ts
+            if (self.narrow and getattr(qr.engine, "max_keys", 1 << 30) <= 65536 and n
+                    and int(d.min()) >= -(1 << 31) and int(d.max()) < (1 << 31)):
+                qr.engine.stage(ts, key, stream, cols, null_ptrs, ts32=d.astype(np.int32), ts_base=int(ts[0]),
+                                key16=key.astype(np.uint16))
+                qr.narrow_batches += 1
+            else:
+                qr.engine.stage(ts, key, stream, cols, null_ptrs)
             if qr.inflight is not None:
                 self._finish(qr)
             qr.inflight = (list(evs), ts, key, stream)

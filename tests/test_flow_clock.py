@@ -402,6 +402,7 @@ class _StagedOracle(OracleEngine):
         super().__init__(program_json, start)
         self.staged = []
         self.max_staged = 0
+        self.narrow = 0
 
     def stat(self, which):
         assert which == "match_layout"
@@ -413,8 +414,15 @@ class _StagedOracle(OracleEngine):
         out["layout"] = 0
         return out
 
-    def stage(self, ts, key, stream, cols, nulls):
+    max_keys = 65536  # (so the mirror's narrow form applies)
+
+    def stage(self, ts, key, stream, cols, nulls, ts32=None, ts_base=0, key16=None):
+        """The narrow form is pushed as what the engine's k_widen_ts / k_widen_key rebuild from it."""
         assert len(self.staged) < 2, "two batches staged: run one first"
+        if ts32 is not None:
+            ts = ts_base + ts32.astype(np.int64)
+            key = key16.astype(np.int32)
+            self.narrow += 1
         self.staged.append(tuple(np.array(a, copy=True) for a in (ts, key, stream)) +
                            ([np.array(c, copy=True) for c in cols], [None if m is None else m.copy() for m in nulls]))
         self.max_staged = max(self.max_staged, len(self.staged))
@@ -441,56 +449,60 @@ def test_pipelined_flush_needs_batches():
                                                              pipelined=True)
 
 
+@pytest.mark.parametrize("narrow", [False, True])
 @pytest.mark.parametrize("case", ["c5", "c4", "live", "heartbeat"])
-def test_pipelined_flush_host_logic(case, c5_case, c4_case, live_case):
+def test_pipelined_flush_host_logic(case, narrow, c5_case, c4_case, live_case):
     """The pipelined flush's ordering on the CPU: batch i runs after batch i+1 is staged, the rows join
     the history in run order, and every clock move / drain point runs the staged batch first -- the
     same rows as the unpipelined mirror and the Direct transcription."""
     f = _staged_oracle_factory
     if case == "c5":
         sends, want = c5_case
-        q = _run_mirror(f, synth.QUERIES[5], sends, 4096, compact=True, pipelined=True)
+        q = _run_mirror(f, synth.QUERIES[5], sends, 4096, compact=True, pipelined=True, narrow=narrow)
         _assert_rows_close(_by_key(q.rows), want)
     elif case == "c4":
         sends, want = c4_case
-        q = _run_mirror(f, C4_TIMER_APP, sends, 997, compact=True, pipelined=True)
+        q = _run_mirror(f, C4_TIMER_APP, sends, 997, compact=True, pipelined=True, narrow=narrow)
         assert _by_key(q.rows) == want
     elif case == "live":
         sends, adv, want = live_case
-        q = _run_mirror(f, LIVE_APP, sends, 500, compact=True, pipelined=True, advances=adv, start_clock=sends[0][1])
+        q = _run_mirror(f, LIVE_APP, sends, 500, compact=True, pipelined=True, narrow=narrow, advances=adv,
+                        start_clock=sends[0][1])
         assert _by_key(q.rows) == want
     else:
-        at_sends, rows, _ = _heartbeat_run(f, 64, compact=True, pipelined=True)
+        at_sends, rows, _ = _heartbeat_run(f, 64, compact=True, pipelined=True, narrow=narrow)
         assert at_sends == []  # the sends' batch is still staged at the first read (one flush late)
         assert [r for _, r in rows] == [["GOOG"], ["WSO2"], ["GOOG"]]
         q = None
     if q is not None:
         # (live mode's Thread.sleep every 97 sends drains before a 500-row batch fills)
         assert q.pipelined and q.inflight is None and q.engine.max_staged == (1 if case == "live" else 2)
+        assert (q.narrow_batches > 0) == narrow and q.engine.narrow == q.narrow_batches
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("narrow", [False, True])
 @pytest.mark.parametrize("case", ["c5", "c4", "live", "heartbeat"])
-def test_pipelined_flush_hip(case, c5_case, c4_case, live_case):
+def test_pipelined_flush_hip(case, narrow, c5_case, c4_case, live_case):
     """The mirror's pipelined flush through shp_stage_batch / shp_run_staged on the GPU: the same rows
     as the oracle (PAIRS32 for C5, the labs path's FULL records for C4, the lanes for live mode)."""
     if case == "c5":
         sends, want = c5_case
-        q = _run_mirror(_hip_factory(C5_KEYS), synth.QUERIES[5], sends, 4096, compact=True, pipelined=True)
-        assert q.layout == 3 and q.pipelined
+        q = _run_mirror(_hip_factory(C5_KEYS), synth.QUERIES[5], sends, 4096, compact=True, pipelined=True, narrow=narrow)
+        assert q.layout == 3 and q.pipelined and (q.narrow_batches > 0) == narrow
         _assert_rows_close(_by_key(q.rows), want)
     elif case == "c4":
         sends, want = c4_case
-        q = _run_mirror(_hip_factory(64), C4_TIMER_APP, sends, 997, compact=True, pipelined=True)
-        assert q.engine.path == 4 and q.pipelined
+        q = _run_mirror(_hip_factory(64), C4_TIMER_APP, sends, 997, compact=True, pipelined=True, narrow=narrow)
+        assert q.engine.path == 4 and q.pipelined and (q.narrow_batches > 0) == narrow
         assert _by_key(q.rows) == want
     elif case == "live":
         sends, adv, want = live_case
-        q = _run_mirror(_hip_factory(64), LIVE_APP, sends, 500, compact=True, pipelined=True, advances=adv,
+        q = _run_mirror(_hip_factory(64), LIVE_APP, sends, 500, compact=True, pipelined=True, narrow=narrow, advances=adv,
                         start_clock=sends[0][1])
         assert q.pipelined
         assert _by_key(q.rows) == want
     else:
-        at_sends, rows, _ = _heartbeat_run(_hip_factory(256), 64, compact=True, pipelined=True)
+        at_sends, rows, _ = _heartbeat_run(_hip_factory(256), 64, compact=True, pipelined=True, narrow=narrow)
         assert [r for _, r in rows] == [["GOOG"], ["WSO2"], ["GOOG"]]
         assert [t for t, _ in rows] == [1544512386100, 1544512386800, 1544512387200]

@@ -471,3 +471,10 @@ def test_pipelined_flush_stages_then_runs_the_older_batch():
     assert cs.index("staged.pollFirst()") < cs.index("commitRows(c)") < cs.index("decoded = c")
     for getter in ("int keyAt(long i)", "long tsAt(long i)", "int streamAt(long i)"):
         assert "decoded." in _method(cb, getter)
+    # the narrow form (the mirror's narrow=True): 4-byte ts offsets from the batch's first ts, 2-byte ids
+    assert "batch.narrowOk()" in st and "ShpNative.STAGE_BATCH_NARROW.invokeExact(engine, batch.descriptor()" in st
+    assert "policy == FlushPolicy.PIPELINED && maxKeys <= 65536" in rt
+    app = _method(cb, "void append(long timestamp, int keyId, int streamIndex, Object[] data)")
+    assert "o.base = timestamp" in app and "if (d != (int) d)" in app and "o.wide = true" in app
+    assert "o.key16.setAtIndex(JAVA_SHORT, n, (short) keyId)" in app
+    assert "return narrow && open.n > 0 && !open.wide;" in _method(cb, "boolean narrowOk()")
