@@ -975,8 +975,15 @@ __host__ __device__ inline bool la_fz1(const LaPredD& p) {
 // from the committed state, the broken blocks by the exact rule (the records and state of the others
 // stand).
 constexpr uint32_t LA_XMARK = 0xFFFFFFFFu;
+// The exact variant runs only the marked slots, wave-wide; unlimited it takes 143 registers (three
+// waves a SIMD).  Built for four (128) it takes C4 at 1 % disorder from 18.5 to 14.5 ms (five: 15.9,
+// six: 18.4 -- their spills), while a limit on the ordered variant only costs it (five: 7.8 -> 8.5 ms;
+// profiles/r06_wpe_ab.txt)
+#ifndef SHP_LABS_XWPE
+#define SHP_LABS_XWPE 4
+#endif
 template <bool FZ1, bool XB>
-static __global__ __launch_bounds__(64) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
+static __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(XB ? SHP_LABS_XWPE : 1))) void k_labs_w(LabsDev D, BatchView B, const uint32_t* __restrict__ perm,
                                                const uint32_t* __restrict__ kbeg, const uint32_t* __restrict__ kcnt,
                                                int H, int* err) {
   __shared__ LaWait A[64];      // the pairs on the absent state's lists, list (= completion) order
