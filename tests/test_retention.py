@@ -175,3 +175,23 @@ def test_engine_oldest_live_seq_against_oracle(cfg, keys, ms):
         if cfg in (3, "3b"):
             assert floor == want, (lo, floor, want)
         assert floor <= hi
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("narrow", [False, True])
+@pytest.mark.parametrize("cfg,n,keys,ms,layout", [(2, 60_000, 2_000, 0.25, 3), ("3b", 40_000, 500, 1, 4),
+                                                  (5, 40_000, 1_500, 0.2, 3), (4, 20_000, 100, 5, 0)])
+def test_pipelined_batches_compact_with_engine_retention(cfg, n, keys, ms, layout, narrow):
+    """The pipelined flush (FlushPolicy.PIPELINED's mirror: shp_stage_batch[_narrow] / shp_run_staged,
+    one batch in flight) with compact records decoded per run -- PAIRS32, CHAIN32 (the rings walk the
+    runs in stage order), FULL for C4 -- rows kept from shp_engine_oldest_live_seq on: the output equal
+    to the oracle's."""
+    evs = _events(cfg, n, keys, ms)
+    want = _rows(_run(_oracle_factory, cfg, evs, retain=False))
+    rt = _run(_hip_factory(max(keys, 256)), cfg, evs, batch_size=997, compact=True, min_trim=256, pipelined=True,
+              narrow=narrow)
+    q = rt.queries["q"]
+    assert q.layout == layout and q.pipelined and q.inflight is None
+    assert (q.narrow_batches > 0) == narrow
+    assert _rows(rt) == want
+    assert len(want) > 100 or cfg == 3
