@@ -1,4 +1,5 @@
 #!/bin/bash
+# (SHP_LA_SCAT_LDS, the LDS padding this A/B used, was removed after it: profiles/r06_scatter_occupancy.txt)
 # GPU box: C4 multisplit scatter duration against its resident waves (dynamic LDS padded by SHP_LA_SCAT_LDS)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
