@@ -1,0 +1,94 @@
+"""C4 at its configured size (10^8 events, 1000 keys, one push) on the HIP path.
+
+* Against the oracle at 10^7 events (four pushes), compared as whole record arrays: every match's key,
+  timer ts, emission event and (e1, e2) sequence numbers, ordered per key (the engine writes records
+  in key order, the oracle in emission order; per key both are the reference's emission order).
+* At the full 10^8 events in one push, generated in HBM (the bench's stream, `shp_synth_fill`):
+  the size-independent property that the push clock computed inside the multisplit (the default) and
+  the device-wide max-scan (`SHP_LABS_SCAN_CLOCK=1`) give bit-identical records -- ordered, and with
+  1 % of the events moved back up to 8 s (the exact blocks in `k_labs_w`).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from diff_util import program_for, run, small_stream
+from oracle.oracle import OracleEngine
+
+pytestmark = pytest.mark.gpu
+
+KEYS = 1000
+
+
+def _records(mb):
+    """(key, ts, type, pos, x seq, y seq) per match, stably sorted by key (per-key order kept)."""
+    m = len(mb["key"])
+    assert (mb["slot_len"][:, :3].sum(axis=1) == 2).all()  # C4: one x and one y slot per match
+    refs = mb["refs"].reshape(m, 2) if m else np.zeros((0, 2), np.int64)
+    order = np.argsort(mb["key"], kind="stable")
+    return [np.asarray(a)[order] for a in (mb["key"], mb["ts"], mb["type"], mb["pos"], refs[:, 0], refs[:, 1])]
+
+
+def test_c4_1e7_events_vs_oracle_whole_arrays():
+    from siddhi_amd.native import HipEngine
+    cq = program_for(4)
+    g = small_stream(4, 10_000_000, KEYS)
+    o = OracleEngine(cq.program_json(), 0)
+    want = run(o, cq, g, 2_500_000)
+    if o.timer_ties():
+        pytest.skip("cross-key scheduler ties (TreeMultimap): parity-unpinned")
+    e = HipEngine(cq.program_json(), 0, max_keys=KEYS, max_batch=2_500_000)
+    assert e.path == 4
+    got = run(e, cq, g, 2_500_000)
+    assert len(want["key"]) > 500_000
+    for a, b, name in zip(_records(want), _records(got), ("key", "ts", "type", "pos", "x", "y")):
+        assert np.array_equal(a, b), name
+
+
+def _push_full(L, native, cq, dev, scan_clock, monkeypatch):
+    if scan_clock:
+        monkeypatch.setenv("SHP_LABS_SCAN_CLOCK", "1")
+    else:
+        monkeypatch.delenv("SHP_LABS_SCAN_CLOCK", raising=False)
+    ts, key, price, stream = dev
+    n = ts.numel()
+    e = native.HipEngine(cq.program_json(), 0, max_keys=KEYS, max_batch=n, max_matches=n)
+    assert e.path == 4
+    ncol = max(1, len(cq.columns))
+    colp = (ctypes.c_void_p * ncol)(*([price.data_ptr()] * ncol))
+    b = native.ShpBatch(n, ts.data_ptr(), key.data_ptr(), stream.data_ptr(), ctypes.cast(colp, ctypes.c_void_p), None)
+    mt = native.ShpMatches()
+    rc = L.shp_push_batch_device(e.h, ctypes.byref(b), ctypes.byref(mt))
+    assert rc == 0, L.shp_last_error(e.h)
+    out = native.matches_to_numpy(mt)
+    fb = e.stat("labs_fallbacks")
+    e.close()
+    return out, fb
+
+
+@pytest.mark.parametrize("disorder", [0.0, 0.01])
+def test_c4_1e8_events_fused_clock_equals_device_scan(disorder, monkeypatch):
+    import torch
+    from siddhi_amd import native, synth
+    L = native.lib()
+    cq = program_for(4)
+    spec = synth.CONFIGS[4]
+    n = 100_000_000
+    ts = torch.empty(n, dtype=torch.int64, device="cuda")
+    key = torch.empty(n, dtype=torch.int32, device="cuda")
+    price = torch.empty(n, dtype=torch.float32, device="cuda")
+    stream = torch.empty(n, dtype=torch.int32, device="cuda")
+    assert L.shp_synth_fill(4, 0, n, KEYS, spec.n_streams, int(spec.dense), ts.data_ptr(), key.data_ptr(),
+                            price.data_ptr(), None, stream.data_ptr(), None) == 0
+    if disorder:
+        gg = torch.Generator(device="cuda").manual_seed(1000)
+        back = torch.rand(n, device="cuda", generator=gg) < disorder
+        ts -= back.to(torch.int64) * torch.randint(0, 8000, (n,), device="cuda", generator=gg)
+    torch.cuda.synchronize()
+    a, fa = _push_full(L, native, cq, (ts, key, price, stream), False, monkeypatch)
+    b, fb = _push_full(L, native, cq, (ts, key, price, stream), True, monkeypatch)
+    assert len(a["key"]) > 5_000_000 and len(a["key"]) == len(b["key"])
+    for name in ("key", "ts", "type", "pos", "slot_len", "refs"):
+        assert np.array_equal(a[name], b[name]), name
+    assert fa == fb
