@@ -21,6 +21,15 @@ pytestmark = pytest.mark.gpu
 KEYS = 1000
 
 
+def _fetch(L, native, e):
+    """shp_fetch_matches: the last device push's records copied to host memory (FULL rows with
+    num_states slots each, in reference emission order; AGG rows as produced)."""
+    mt = native.ShpMatches()
+    rc = L.shp_fetch_matches(e.h, ctypes.byref(mt))
+    assert rc == 0, L.shp_last_error(e.h)
+    return native.matches_to_numpy(mt)
+
+
 def _records(mb):
     """(key, ts, type, pos, x seq, y seq) per match, stably sorted by key (per-key order kept)."""
     m = len(mb["key"])
@@ -61,7 +70,7 @@ def _push_full(L, native, cq, dev, scan_clock, monkeypatch):
     mt = native.ShpMatches()
     rc = L.shp_push_batch_device(e.h, ctypes.byref(b), ctypes.byref(mt))
     assert rc == 0, L.shp_last_error(e.h)
-    out = native.matches_to_numpy(mt)
+    out = _fetch(L, native, e)  # (mt holds device pointers: the records stay in HBM)
     fb = e.stat("labs_fallbacks")
     e.close()
     return out, fb
