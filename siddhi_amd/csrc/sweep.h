@@ -1731,7 +1731,10 @@ struct SweepState {
   int64_t w_units = 0;  // k_sw_win: units the status array holds
   bool win_off = true;  // k_sw_win is opt-in: SHP_WIN=1 (tests/test_win_sweep.py, A/B)
   bool last_win = false;  // the last run() launched k_sw_win
-  int64_t st_len = 65536;
+  // events per super-tile (one scatter workgroup): 131072 measured 37.6 against 37.3 G events/s at
+  // 65536 on C2, 29.75 against 29.6 G on C5 -- fewer tiles, a smaller count pass and scan
+  // (profiles/r06_stlen_ab.txt; SHP_SW_STLEN overrides it for diagnostics)
+  int64_t st_len = 131072;
   int32_t nst_max = 1;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
