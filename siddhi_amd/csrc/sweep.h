@@ -1731,10 +1731,13 @@ struct SweepState {
   int64_t w_units = 0;  // k_sw_win: units the status array holds
   bool win_off = true;  // k_sw_win is opt-in: SHP_WIN=1 (tests/test_win_sweep.py, A/B)
   bool last_win = false;  // the last run() launched k_sw_win
-  // events per super-tile (one scatter workgroup): 131072 measured 37.6 against 37.3 G events/s at
-  // 65536 on C2, 29.75 against 29.6 G on C5 -- fewer tiles, a smaller count pass and scan
-  // (profiles/r06_stlen_ab.txt; SHP_SW_STLEN overrides it for diagnostics)
-  int64_t st_len = 131072;
+  // events per super-tile (one scatter workgroup).  Pushes of 64M events and more take 131072: 37.6
+  // against 37.3 G events/s at 65536 on C2, 29.75 against 29.6 G on C5 (fewer tiles, a smaller count
+  // pass and scan; profiles/r06_stlen_ab.txt).  Smaller pushes keep 65536, which is also the
+  // allocation's granularity: at 12.5M events 131072 leaves 95 workgroups for 256 CUs (scatter 0.20 ->
+  // 0.34 ms).  SHP_SW_STLEN sets both, for diagnostics.
+  int64_t st_len = 65536;
+  int64_t st_len_big = 131072;
   int32_t nst_max = 1;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -1924,7 +1927,7 @@ struct SweepState {
       D.lk_bits = 0;
       while ((1u << D.lk_bits) <= mx) D.lk_bits++;
     }
-    if (getenv("SHP_SW_STLEN")) st_len = std::max<int64_t>(4096, atoll(getenv("SHP_SW_STLEN")));  // diagnostics
+    if (getenv("SHP_SW_STLEN")) st_len = st_len_big = std::max<int64_t>(4096, atoll(getenv("SHP_SW_STLEN")));
     nst_max = (int32_t)std::max<int64_t>(1, (cap + st_len - 1) / st_len);
     D.st_len = st_len;
     {
@@ -2048,7 +2051,8 @@ struct SweepState {
   void run(const BatchView& B, const int32_t* key, const MatchOut& O, int* err, hipStream_t s, KTimer& kt) {
     if (B.n <= 0) return;
     if (B.nulls[0]) D.maybe_null = 1;
-    D.nst = (int32_t)((B.n + st_len - 1) / st_len);
+    D.st_len = B.n >= (64ll << 20) ? st_len_big : st_len;
+    D.nst = (int32_t)((B.n + D.st_len - 1) / D.st_len);
     (void)hipMemsetAsync(D.tsmax, 0, 2 * sizeof(unsigned long long), s);
     // overflow flags describe this push only: flags a failed push left must not be promoted to
     // spilled owners by a later push's SWE_SPILL re-run
