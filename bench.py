@@ -316,11 +316,12 @@ def main():
                         and pm.get("lib_sha16") == _lib_sha16(native.LIB_PATH)):
                     ks = pm.get("kernels", {})
                     traffic = ks.get(dom, {}).get("hbm_bytes_per_launch")
-                    # the whole push: every kernel of the run but the input generator and the
+                    # the whole push: every kernel of the run but the input generator, the torch
+                    # kernels that move events back for --disorder (both before timing) and the
                     # one-time state initialisation (one launch each per push)
                     step_traffic = sum(v["hbm_bytes_per_launch"] for k, v in ks.items()
                                        if k not in ("synth", "sw_init", "labs_init", "cseq_init", "fast_init", "iota")
-                                       and not k.startswith("__amd_rocclr"))
+                                       and not k.startswith("__amd_rocclr") and "at::native" not in k)
                     pmc_src = os.path.relpath(a.pmc, ROOT)
             except Exception:
                 traffic = step_traffic = None

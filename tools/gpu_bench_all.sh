@@ -17,7 +17,7 @@ for c in ${CONFIGS:-c3b c5 c4 c3 c1}; do
     c3bfull) run c3bfull 400 --config 3b --cseq-layout full --no-cpu-baseline ;;
     c5) run c5 400 --config 5 ;;
     c4) run c4 500 --config 4 ;;
-    c4d) run c4d 500 --config 4 --disorder 0.01 --no-cpu-baseline --e2e-steps 0 ;;
+    c4d) run c4d 500 --config 4 --disorder 0.01 --no-cpu-baseline --e2e-steps 0 --pmc profiles/pmc_traffic_c4d_0.01.json ;;
     c4lanes) run c4lanes 700 --config 4 --path general --steps 2 --warmup 1 --latency-batches 0 ;;
     c3) run c3 400 --config 3 ;;
     c1) run c1 500 --config 1 --steps 3 --warmup 1 ;;
